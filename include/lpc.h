@@ -1,0 +1,175 @@
+/*
+ * lpc.h -- C ABI of liblpc.so, the MI355X-native per-bounce engine of the
+ * LightPyCL drop-in (package lightpycl_amd).
+ *
+ * The reference (ngchihuan/LightPyCL) drives its hot path through PyOpenCL:
+ *   self.prg.intersect(queue, (n,), None, ...)            iterative_tracer.py:288
+ *   self.prg.intersect_postproc(queue, (n,), None, ...)   iterative_tracer.py:303
+ *   self.prg.reflect_refract_rays(queue, (n,), None, ...) iterative_tracer.py:318
+ *   self.prg.angular_project(queue, (n,), None, ...)      iterative_tracer.py:546
+ * around a host loop (iterative_tracer.py:241-391).  The entry points below
+ * replace those launches and that loop.  Conventions:
+ *   - every function returns 0 on success, a negative LPC_E* code on error;
+ *     lpc_last_error() gives the message (the reference raises PyOpenCL
+ *     exceptions; the Python layer turns a non-zero status into RuntimeError);
+ *   - "host" arguments are caller-owned host buffers, copied in/out before
+ *     the call returns; "dev" arguments are device pointers (hipMalloc'd or
+ *     torch tensors' data_ptr) on the handle's device;
+ *   - float3 data crosses the boundary in the reference's layout: (n,4)
+ *     float32 rows, w ignored on input and written as 0 on output;
+ *   - one handle per GPU; a handle is not thread-safe (the reference uses a
+ *     single in-order queue per tracer, iterative_tracer.py:74).
+ */
+#ifndef LPC_H
+#define LPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LPC_ABI_VERSION 1
+
+enum {
+    LPC_OK = 0,
+    LPC_E_ARG = -1,      /* bad argument (null pointer, size, no scene, ...) */
+    LPC_E_HIP = -2,      /* HIP runtime error (message has the hipError string) */
+    LPC_E_STATE = -3,    /* call out of order (e.g. iterate before set_rays) */
+    LPC_E_NOMEM = -4     /* device allocation failed */
+};
+
+typedef struct lpc_handle lpc_handle;
+
+/* ---- library / device --------------------------------------------------- */
+int lpc_abi_version(void);
+/* Number of visible HIP devices (0 if none). */
+int lpc_device_count(int *count);
+/* Open a handle on HIP device `device` (replaces CL_Tracer.__init__'s
+ * platform/device/context/queue setup, iterative_tracer.py:36-74). */
+int lpc_open(int device, lpc_handle **out);
+int lpc_close(lpc_handle *h);
+/* Last error message of `h` (or of the last failed lpc_open when h is NULL). */
+const char *lpc_last_error(const lpc_handle *h);
+/* Device name / CU count of the handle's GPU (diagnostics). */
+int lpc_device_info(lpc_handle *h, char *name, int name_len, int *cu_count);
+
+/* ---- scene (iterative_tracer.py:121-169) -------------------------------- */
+/* Upload the flattened scene.  v0,v1,v2: host (tri_count,4) float32 rows;
+ * mesh_id: host int32[tri_count], contiguous runs per mesh as the reference
+ * builds them (:137-150); material tables host [mesh_count] (:122-135).
+ * The reference's slot arithmetic for mesh_id changes (.cl:260-265) is
+ * reproduced, so non-contiguous or empty meshes behave as in the reference. */
+int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const float *v1,
+                     const float *v2, const int32_t *mesh_id, int32_t mesh_count,
+                     const int32_t *mat_type, const float *ior, const float *refl,
+                     const float *diss);
+
+/* ---- one bounce on host arrays (iterative_tracer.py:280-348) ------------- */
+/* Runs intersect + intersect_postproc + reflect_refract_rays (fused on the
+ * device) for n rays.  pow and meas are read and written back (dissipation
+ * .cl:392, measured state .cl:466-471).  prev_mid = rays_current_mid (-2 just
+ * emitted, -1 outside, >=0 mesh).  Children origins equal dest (.cl:319,324,
+ * 456,461), so only dest is returned.  Optional outputs may be NULL:
+ * n1_mid, n2_mid, entering, isect_idx. */
+int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float *dir4,
+                    float *pow, int32_t *meas, const int32_t *prev_mid, float max_ray_len,
+                    float ior_env, float *dest4, int32_t *isect_mid, float *r_dir4,
+                    float *r_pow, int32_t *r_meas, float *t_dir4, float *t_pow,
+                    int32_t *t_meas, int32_t *n1_mid, int32_t *n2_mid, int32_t *entering,
+                    int32_t *isect_idx);
+
+/* ---- reference-kernel drop-ins on device buffers ------------------------- */
+/* Same argument meaning and (n,4)/[ray][mesh] layouts as the .cl kernels, for
+ * a host that keeps its own device buffers and launch sequence.  The scene
+ * (vertices, mesh ids, materials) is the one given to lpc_scene_upload; the
+ * .cl kernels' mesh_v0/v1/v2/mesh_id/mesh_* arguments are therefore implicit.
+ * Launches are stream-ordered on the handle's stream and synchronised before
+ * return, as the reference's event.wait() does. */
+/* __kernel intersect (.cl:243-289): per [ray][mesh] min t / argmin / count. */
+int lpc_intersect(lpc_handle *h, int64_t n, const float *dev_origin4, const float *dev_dir4,
+                  float max_ray_len, float *dev_isect_min_ray_len, int32_t *dev_isects_count,
+                  int32_t *dev_isect_idx_tmp);
+/* __kernel intersect_postproc (.cl:105-240). */
+int lpc_intersect_postproc(lpc_handle *h, int64_t n, const float *dev_origin4,
+                           const float *dev_dir4, float *dev_dest4,
+                           const int32_t *dev_prev_mid, int32_t *dev_n1_mid,
+                           int32_t *dev_n2_mid, int32_t *dev_entering,
+                           int32_t *dev_isect_mid, int32_t *dev_isect_idx,
+                           const float *dev_isect_min_ray_len,
+                           const int32_t *dev_isects_count,
+                           const int32_t *dev_isect_idx_tmp, float max_ray_len);
+/* __kernel reflect_refract_rays (.cl:346-474); children origins written too. */
+int lpc_reflect_refract_rays(lpc_handle *h, int64_t n, const float *dev_origin4,
+                             const float *dev_dest4, const float *dev_dir4, float *dev_pow,
+                             int32_t *dev_meas, const int32_t *dev_n1_mid,
+                             const int32_t *dev_n2_mid, float *dev_r_origin4,
+                             float *dev_r_dir4, float *dev_r_pow, int32_t *dev_r_meas,
+                             float *dev_t_origin4, float *dev_t_dir4, float *dev_t_pow,
+                             int32_t *dev_t_meas, const int32_t *dev_isect_mid,
+                             const int32_t *dev_isect_idx, float ior_env);
+
+/* ---- device-resident trace (iterative_tracer.py:241-391 on the GPU) ------- */
+typedef struct {
+    int64_t n_in;            /* rays traced this iteration                       */
+    int64_t n_reflect;       /* kept reflected children (meas == 0)               */
+    int64_t n_refract;       /* kept refracted children                           */
+    int64_t n_measured;      /* rays that hit a measure surface this iteration    */
+    double power_next;       /* sum of next-population power (float64)            */
+} lpc_iter_stats;
+
+/* Load the initial population from host (n,4) rows and power[n]; prev_mid = -2,
+ * meas = 0 (:117-118).  Also keeps a device copy for lpc_trace_reset. */
+int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const float *dir4,
+                       const float *pow, float max_ray_len, float ior_env);
+/* Restore the population given to lpc_trace_set_rays (device-to-device) and
+ * zero the measured record / per-mesh power. */
+int lpc_trace_reset(lpc_handle *h);
+/* One iteration over the whole current population (processed in chunks of at
+ * most lpc_set_chunk rays): bounce, on-device compaction into the next
+ * population ([reflected kept ; refracted kept], :366-373), measured-ray record
+ * and per-mesh measured power.  Optional host exports (NULL to skip), sized for
+ * st->n_in = current population (known from the previous call / set_rays):
+ *   out_origin4/out_dest4 (n_in,4), out_pow (n_in) post-dissipation,
+ *   out_meas (n_in)                                    -> the results tuple :355
+ *   out_next_pow (n_reflect + n_refract, capacity 2*n_in) -> termination sum :372 */
+int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
+                      int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st);
+/* Current population size. */
+int lpc_trace_population(lpc_handle *h, int64_t *n);
+/* Measured record so far: count and per-mesh measured power (double[mesh_count]). */
+int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_power);
+/* Copy the measured record to host: pos4 (count,4), pow (count), mesh (count);
+ * any pointer may be NULL. */
+int lpc_trace_fetch_measured(lpc_handle *h, float *pos4, float *pow, int32_t *mesh);
+/* Rays per device chunk (0 = library default). */
+int lpc_set_chunk(lpc_handle *h, int64_t rays_per_chunk);
+
+/* ---- trace-end projection + binning (iterative_tracer.py:503-562) -------- */
+/* angular_project (.cl:509-538) / stereograph_project (.cl:488-506) of n host
+ * points with rotation rows rot4 (4x4 float32 rows, reference R_dev) and
+ * pivot4, followed by np.histogram2d-compatible binning into H[nx][ny]
+ * (float64, += (double)pwr_cor / weight_div, iterative_tracer.py:556-560) over the given float64 bin edges
+ * (nx+1, ny+1; value == last edge goes to the last bin, outside -> dropped).
+ * mode 0 = angular, 1 = stereographic.  x/y/pwr_cor host outputs may be NULL.
+ * If pos4 == NULL the trace's measured record (device-resident) is used. */
+int lpc_project_hist(lpc_handle *h, int mode, int64_t n, const float *pos4, const float *pwr,
+                     const float *rot4, const float *pivot4, const double *xedges, int nx,
+                     const double *yedges, int ny, double weight_div, double *H,
+                     float *x, float *y, float *pwr_cor);
+
+/* ---- profiling ------------------------------------------------------------ */
+typedef struct {
+    double intersect_ms;     /* sum of k_intersect durations (HIP events)       */
+    double shade_ms;         /* postproc+Fresnel+compaction kernels             */
+    int64_t intersect_launches;
+    int64_t pairs;           /* ray-triangle pairs examined by k_intersect      */
+} lpc_prof;
+/* Enable (1) / disable (0) per-launch HIP-event timing of the hot kernels. */
+int lpc_prof_enable(lpc_handle *h, int on);
+int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LPC_H */

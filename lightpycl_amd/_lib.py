@@ -1,0 +1,119 @@
+"""ctypes binding of liblpc.so (include/lpc.h).
+
+The library is built in-tree (``lightpycl_amd/liblpc.so``) by
+:func:`lightpycl_amd.build.build`.  There is no fallback: if the library is
+missing or no HIP device is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblpc.so")
+
+_lib = None
+
+
+class LpcError(RuntimeError):
+    """Error returned by liblpc (carries the library's message)."""
+
+
+class IterStats(ctypes.Structure):
+    _fields_ = [("n_in", ctypes.c_int64), ("n_reflect", ctypes.c_int64),
+                ("n_refract", ctypes.c_int64), ("n_measured", ctypes.c_int64),
+                ("power_next", ctypes.c_double)]
+
+
+class Prof(ctypes.Structure):
+    _fields_ = [("intersect_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
+                ("intersect_launches", ctypes.c_int64), ("pairs", ctypes.c_int64)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F32 = ctypes.c_float
+_F64 = ctypes.c_double
+_INT = ctypes.c_int
+
+# name -> argtypes (all functions return int status except lpc_last_error)
+_PROTOS = {
+    "lpc_abi_version": [],
+    "lpc_device_count": [_P],
+    "lpc_open": [_INT, _P],
+    "lpc_close": [_P],
+    "lpc_device_info": [_P, _P, _INT, _P],
+    "lpc_scene_upload": [_P, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
+    "lpc_bounce_host": [_P, _I64, _P, _P, _P, _P, _P, _F32, _F32, _P, _P, _P, _P, _P, _P, _P,
+                        _P, _P, _P, _P, _P],
+    "lpc_intersect": [_P, _I64, _P, _P, _F32, _P, _P, _P],
+    "lpc_intersect_postproc": [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F32],
+    "lpc_reflect_refract_rays": [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                 _P, _P, _P, _P, _F32],
+    "lpc_trace_set_rays": [_P, _I64, _P, _P, _P, _F32, _F32],
+    "lpc_trace_reset": [_P],
+    "lpc_trace_iterate": [_P, _P, _P, _P, _P, _P, _P],
+    "lpc_trace_population": [_P, _P],
+    "lpc_trace_measured": [_P, _P, _P],
+    "lpc_trace_fetch_measured": [_P, _P, _P, _P],
+    "lpc_set_chunk": [_P, _I64],
+    "lpc_project_hist": [_P, _INT, _I64, _P, _P, _P, _P, _P, _INT, _P, _INT, _F64, _P, _P, _P,
+                         _P],
+    "lpc_prof_enable": [_P, _INT],
+    "lpc_prof_read": [_P, _P, _INT],
+}
+
+EXPORTED = tuple(_PROTOS) + ("lpc_last_error",)
+
+
+def load(path: str = LIB_PATH):
+    """Load liblpc.so and declare every entry point of include/lpc.h."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LpcError(f"liblpc.so not built ({path}); run lightpycl_amd.build.build() "
+                       "(hipcc --offload-arch=gfx950)")
+    L = ctypes.CDLL(path)
+    for name, args in _PROTOS.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    L.lpc_last_error.argtypes = [_P]
+    L.lpc_last_error.restype = ctypes.c_char_p
+    if L.lpc_abi_version() != 1:
+        raise LpcError("liblpc ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, handle=None):
+    if rc != 0:
+        msg = load().lpc_last_error(handle)
+        raise LpcError(f"liblpc error {rc}: {msg.decode() if msg else ''}")
+
+
+def ptr(a):
+    """Data pointer of a contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def f32(a, shape=None):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+    return a.reshape(shape) if shape is not None else a
+
+
+def i32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    check(load().lpc_device_count(ctypes.byref(c)))
+    return c.value

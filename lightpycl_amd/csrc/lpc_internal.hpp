@@ -1,0 +1,103 @@
+// lpc_internal.hpp -- argument structs shared by the kernels and the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lpck {
+
+struct Piece { int32_t lo, hi; };   // filter-record range [lo, hi), length % 4 == 0
+
+struct RaysIn {                       // a ray population (SoA)
+    const float *ox, *oy, *oz, *dx, *dy, *dz, *pw;
+    const int32_t *pmid;              // previous intersected mesh (-2 emitted, -1 outside)
+};
+struct RaysOut {
+    float *ox, *oy, *oz, *dx, *dy, *dz, *pw;
+    int32_t *pmid;
+};
+
+struct ShadeOutPtrs {                 // per-ray outputs of k_shade (SoA)
+    float *destx, *desty, *destz, *pw;
+    int32_t *imid, *meas;
+    float *rdx, *rdy, *rdz, *rpw;
+    int32_t *rms;
+    float *tdx, *tdy, *tdz, *tpw;
+    int32_t *tms;
+    int32_t *iidx, *n1, *n2, *ent;    // optional (NULL iidx disables all four)
+};
+
+struct ShadeArgs {
+    RaysIn in;
+    const int32_t *meas_in;           // NULL -> 0 (device loop population)
+    int64_t n;
+    int32_t K;
+    const float *st;                  // [K][n] per-slot min t
+    const int32_t *si, *sc;           // [K][n] argmin, hit count
+    const int32_t *mat_type;
+    const float *ior, *refl, *diss, *verts;
+    float max_ray_len, ior_env;
+    ShadeOutPtrs o;
+};
+
+struct DevAcc {                       // device-side counters of one iteration
+    unsigned long long nR, nT;        // kept reflected / refracted (running within iteration)
+    unsigned long long m_total;       // measured record length (persistent)
+    unsigned long long nM_iter;       // measured this iteration
+    double pow_next;                  // float64 sum of kept children power
+    unsigned int dmax2_bits;          // max |dir|^2 of kept children (float bits)
+    unsigned int pad;
+};
+
+struct CompactArgs {
+    int64_t n, nb;                    // rays in chunk, 1024-ray tiles
+    ShadeOutPtrs o;
+    int32_t *blk_cnt;                 // [3][nb]
+    long long *blk_off;               // [3][nb]
+    double *blk_pow;                  // [nb]
+    DevAcc *acc;
+    RaysOut nR, nT;                   // next population: reflected block, refracted staging
+    float *mx, *my, *mz, *mp;         // measured record
+    int32_t *mm;
+};
+
+struct PostprocAosArgs {
+    int64_t n;
+    int32_t K;
+    const float4 *origin, *dir;
+    float4 *dest;
+    const int32_t *prev_mid;
+    int32_t *n1, *n2, *entering, *imid, *iidx;
+    const float *tmin;
+    const int32_t *cnt, *itmp;
+    const int32_t *mat_type;
+    float max_ray_len;
+};
+
+struct FresnelAosArgs {
+    int64_t n;
+    const float4 *origin, *dest, *dir;
+    float *pow;
+    int32_t *meas;
+    const int32_t *n1, *n2, *imid, *iidx;
+    float4 *r_origin, *r_dir, *t_origin, *t_dir;
+    float *r_pow, *t_pow;
+    int32_t *r_meas, *t_meas;
+    const int32_t *mat_type;
+    const float *ior, *refl, *diss, *verts;
+    float ior_env;
+};
+
+struct ProjArgs {
+    int64_t n;
+    int mode;                         // 0 angular, 1 stereographic
+    const float4 *pos4;               // either pos4 or px/py/pz
+    const float *px, *py, *pz, *pwr;
+    const float *rot, *piv;           // device copies: rot 4x4 rows, pivot 4
+    float *x, *y, *pc;                // optional outputs
+    const double *xe, *ye;
+    int nx, ny;
+    double div;                       // H += pc / div  (dx*dy, float64)
+    double *H;
+};
+
+}  // namespace lpck

@@ -1,0 +1,465 @@
+// lpc_kernels.hip -- gfx950 kernels of the LightPyCL per-bounce path.
+//
+//   k_intersect      the hot loop: every ray against every triangle of one
+//                    "piece" (a slice of one mesh run).  Two rays per lane,
+//                    packed-FP32 bounding-sphere filter with the triangle record
+//                    broadcast from SGPRs (s_load), exact Moller-Trumbore only
+//                    for filter candidates -> per-piece (t_min, argmin, count).
+//                    Replaces __kernel intersect (.cl:243-289).
+//   k_combine        pieces -> per-mesh slots with the reference's
+//                    first-minimum-wins rule and slot arithmetic (.cl:260-288).
+//   k_shade          intersect_postproc (.cl:105-240) + reflect_refract_rays
+//                    (.cl:346-474) fused, one lane per ray, SoA in / SoA out.
+//   k_count/k_scan/k_scatter
+//                    on-device compaction of the kept children in the
+//                    reference order [reflected ; refracted] (iterative_tracer.py
+//                    :366-373), measured-ray record and float64 power sums.
+//   k_project_hist   angular/stereographic projection (.cl:488-538) and
+//                    np.histogram2d-compatible binning (iterative_tracer.py:534-562).
+// Layout in HBM: SoA float/int32 arrays per ray; triangle records AoS (32 B
+// filter record, 48 B exact record, 36 B vertices), see DESIGN.md.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "lpc_math.hpp"
+#include "lpc_internal.hpp"
+
+using namespace lpc;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+namespace lpck {
+
+// ---------------------------------------------------------------------------
+// k_intersect
+// grid = (ceil(n/512), pieces), block = 256; thread t handles rays
+// base+t and base+256+t (coalesced SoA loads, packed FP32 pairs).
+__global__ __launch_bounds__(256) void k_intersect(RaysIn R, int64_t n,
+                                                   const FiltGroup *__restrict__ grp,
+                                                   const ExactRec *__restrict__ xrec,
+                                                   const Piece *__restrict__ pieces, float eps,
+                                                   float max_ray_len, float *__restrict__ pt,
+                                                   int32_t *__restrict__ pi,
+                                                   int32_t *__restrict__ pc)
+{
+    const int p = blockIdx.y;
+    const int64_t r0 = (int64_t)blockIdx.x * 512 + threadIdx.x;
+    const int64_t r1 = r0 + 256;
+    const int64_t q0 = r0 < n ? r0 : n - 1;
+    const int64_t q1 = r1 < n ? r1 : n - 1;
+    const f3 O0 = mk3(R.ox[q0], R.oy[q0], R.oz[q0]);
+    const f3 O1 = mk3(R.ox[q1], R.oy[q1], R.oz[q1]);
+    const f3 D0 = mk3(R.dx[q0], R.dy[q0], R.dz[q0]);
+    const f3 D1 = mk3(R.dx[q1], R.dy[q1], R.dz[q1]);
+    // unit direction for the filter only (its rounding is inside the margin)
+    const float s0 = 1.0f / sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z);
+    const float s1 = 1.0f / sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z);
+    const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
+    const f2 nx = {D0.x * s0, D1.x * s1}, ny = {D0.y * s0, D1.y * s1}, nz = {D0.z * s0, D1.z * s1};
+
+    float t0 = max_ray_len, t1 = max_ray_len;
+    int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
+    const Piece pc_ = pieces[p];
+    const int32_t g_lo = pc_.lo >> 2, g_hi = pc_.hi >> 2;
+    FiltGroup G = grp[g_lo];
+    for (int32_t g = g_lo; g < g_hi; ++g) {
+        const FiltGroup Gn = grp[g + 1];      // prefetch (the array has one spare group)
+        f2 d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f2 wx = G.cx[k] - ox, wy = G.cy[k] - oy, wz = G.cz[k] - oz;
+            const f2 ww = wx * wx + wy * wy + wz * wz;
+            const f2 wd = wx * nx + wy * ny + wz * nz;
+            const f2 tq = G.negA[k] - wd * wd;        // one SGPR operand per packed FMA
+            d[k] = ww * G.onemB[k] + tq;
+        }
+        const float m = fminf(fminf(fminf(d[0].x, d[0].y), fminf(d[1].x, d[1].y)),
+                              fminf(fminf(d[2].x, d[2].y), fminf(d[3].x, d[3].y)));
+        if (m <= 0.0f) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (d[k].x <= 0.0f || d[k].y <= 0.0f) {
+                    const int32_t idx = G.idx[k];
+                    const ExactRec x = xrec[idx];
+                    const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
+                    const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
+                    const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
+                    if (d[k].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+                    if (d[k].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+                }
+            }
+        }
+        G = Gn;
+    }
+    const int64_t o = (int64_t)p * n;
+    if (r0 < n) { pt[o + r0] = t0; pi[o + r0] = i0; pc[o + r0] = c0; }
+    if (r1 < n) { pt[o + r1] = t1; pi[o + r1] = i1; pc[o + r1] = c1; }
+}
+
+// ---------------------------------------------------------------------------
+// k_combine: slot j of ray r = ordered combination of the pieces of the run
+// that flushes into slot j (first minimum wins, counts add).  Slots no run
+// writes keep the reference's initial state (max_ray_len, idx 0, count 0)
+// unless keep_unwritten (drop-in mode: caller's buffer is left untouched).
+__global__ __launch_bounds__(256) void k_combine(int64_t n, int32_t K,
+                                                 const int32_t *__restrict__ slot_plo,
+                                                 const int32_t *__restrict__ slot_phi,
+                                                 const float *__restrict__ pt,
+                                                 const int32_t *__restrict__ pi,
+                                                 const int32_t *__restrict__ pc,
+                                                 float max_ray_len, float *__restrict__ st,
+                                                 int32_t *__restrict__ si, int32_t *__restrict__ sc,
+                                                 int64_t sj, int64_t sr, int keep_unwritten)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    for (int32_t j = 0; j < K; ++j) {
+        const int32_t lo = slot_plo[j], hi = slot_phi[j];
+        const int64_t a = (int64_t)j * sj + r * sr;
+        if (lo >= hi) {
+            if (!keep_unwritten) { st[a] = max_ray_len; si[a] = 0; sc[a] = 0; }
+            continue;
+        }
+        float t = max_ray_len;
+        int32_t idx = -1, cnt = 0;
+        for (int32_t p = lo; p < hi; ++p) {
+            const int64_t b = (int64_t)p * n + r;
+            const float tp = pt[b];
+            if (tp < t) { t = tp; idx = pi[b]; }
+            cnt += pc[b];
+        }
+        st[a] = t; si[a] = idx; sc[a] = cnt;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
+__global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n) return;
+    const f3 O = mk3(A.in.ox[r], A.in.oy[r], A.in.oz[r]);
+    const f3 D = mk3(A.in.dx[r], A.in.dy[r], A.in.dz[r]);
+    const int32_t prev = A.in.pmid[r];
+    const int64_t n = A.n;
+    auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
+        const int64_t a = (int64_t)j * n + r;
+        t = A.st[a]; c = A.sc[a]; i = A.si[a];
+    };
+    const PostOut po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
+    const f3 dest = ray_dest(O, D, po.t_min);
+    const int32_t meas_in = A.meas_in ? A.meas_in[r] : 0;
+    auto tri = [&](int32_t idx, f3 &v0, f3 &v1, f3 &v2) {
+        const float *v = A.verts + (int64_t)idx * 9;
+        v0 = mk3(v[0], v[1], v[2]); v1 = mk3(v[3], v[4], v[5]); v2 = mk3(v[6], v[7], v[8]);
+    };
+    const ShadeOut s = shade(O, D, dest, A.in.pw[r], meas_in, po.hit_mesh, po.hit_idx, po.n1,
+                             po.n2, A.mat_type, A.ior, A.refl, A.diss, A.ior_env, tri);
+    A.o.destx[r] = dest.x; A.o.desty[r] = dest.y; A.o.destz[r] = dest.z;
+    A.o.imid[r] = po.hit_mesh;
+    A.o.pw[r] = s.pow;
+    A.o.meas[r] = s.meas;
+    A.o.rdx[r] = s.r_dir.x; A.o.rdy[r] = s.r_dir.y; A.o.rdz[r] = s.r_dir.z;
+    A.o.rpw[r] = s.r_pow; A.o.rms[r] = s.r_meas;
+    A.o.tdx[r] = s.t_dir.x; A.o.tdy[r] = s.t_dir.y; A.o.tdz[r] = s.t_dir.z;
+    A.o.tpw[r] = s.t_pow; A.o.tms[r] = s.t_meas;
+    if (A.o.iidx) {
+        A.o.iidx[r] = po.hit_idx; A.o.n1[r] = po.n1; A.o.n2[r] = po.n2; A.o.ent[r] = po.entering;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Compaction.  A tile is 1024 rays = 4 sub-tiles of 256 (one lane per ray).
+static __device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+static __device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_count(CompactArgs A)
+{
+    __shared__ int32_t s_cnt[3][4];
+    __shared__ double s_pow[4];
+    __shared__ float s_dm[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * 1024;
+    int32_t cR = 0, cT = 0, cM = 0;
+    double pk = 0.0;
+    float dm = 0.0f;
+    for (int sub = 0; sub < 4; ++sub) {
+        const int64_t r = tile + sub * 256 + threadIdx.x;
+        if (r < A.n) {
+            const bool fR = A.o.rms[r] == 0, fT = A.o.tms[r] == 0, fM = A.o.meas[r] == 1;
+            cR += fR; cT += fT; cM += fM;
+            if (fR) {
+                pk += (double)A.o.rpw[r];
+                dm = fmaxf(dm, A.o.rdx[r] * A.o.rdx[r] + A.o.rdy[r] * A.o.rdy[r] + A.o.rdz[r] * A.o.rdz[r]);
+            }
+            if (fT) {
+                pk += (double)A.o.tpw[r];
+                dm = fmaxf(dm, A.o.tdx[r] * A.o.tdx[r] + A.o.tdy[r] * A.o.tdy[r] + A.o.tdz[r] * A.o.tdz[r]);
+            }
+        }
+    }
+    // wave reductions (fixed order -> deterministic)
+    for (int o = 32; o >= 1; o >>= 1) {
+        cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); cM += __shfl_xor(cM, o, 64);
+    }
+    pk = wave_sum(pk);
+    dm = wave_max(dm);
+    if (lane == 0) {
+        s_cnt[0][wv] = cR; s_cnt[1][wv] = cT; s_cnt[2][wv] = cM; s_pow[wv] = pk; s_dm[wv] = dm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int64_t b = blockIdx.x, nb = A.nb;
+        A.blk_cnt[0 * nb + b] = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+        A.blk_cnt[1 * nb + b] = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+        A.blk_cnt[2 * nb + b] = s_cnt[2][0] + s_cnt[2][1] + s_cnt[2][2] + s_cnt[2][3];
+        A.blk_pow[b] = ((s_pow[0] + s_pow[1]) + s_pow[2]) + s_pow[3];
+        const float m = fmaxf(fmaxf(s_dm[0], s_dm[1]), fmaxf(s_dm[2], s_dm[3]));
+        atomicMax(&A.acc->dmax2_bits, __float_as_uint(m));
+    }
+}
+
+// Single-block exclusive scan of the per-tile counts + fixed-order sums.
+__global__ __launch_bounds__(1024) void k_scan(CompactArgs A)
+{
+    __shared__ long long s_sc[3][1024];
+    __shared__ double s_d[1024];
+    __shared__ long long s_base[3];
+    const int t = threadIdx.x;
+    const int64_t nb = A.nb;
+    const int64_t per = (nb + 1023) / 1024;
+    const int64_t lo = t * per, hi = (lo + per < nb) ? lo + per : nb;
+    if (t == 0) {
+        s_base[0] = (long long)A.acc->nR;
+        s_base[1] = (long long)A.acc->nT;
+        s_base[2] = (long long)A.acc->m_total;
+    }
+    long long loc[3] = {0, 0, 0};
+    double lp = 0.0;
+    for (int64_t i = lo; i < hi; ++i) {
+        loc[0] += A.blk_cnt[i]; loc[1] += A.blk_cnt[nb + i]; loc[2] += A.blk_cnt[2 * nb + i];
+        lp += A.blk_pow[i];
+    }
+    for (int f = 0; f < 3; ++f) s_sc[f][t] = loc[f];
+    s_d[t] = lp;
+    __syncthreads();
+    // inclusive Hillis-Steele scan over 1024 thread totals
+    for (int off = 1; off < 1024; off <<= 1) {
+        long long v0 = 0, v1 = 0, v2 = 0;
+        if (t >= off) { v0 = s_sc[0][t - off]; v1 = s_sc[1][t - off]; v2 = s_sc[2][t - off]; }
+        __syncthreads();
+        s_sc[0][t] += v0; s_sc[1][t] += v1; s_sc[2][t] += v2;
+        __syncthreads();
+    }
+    long long run[3];
+    for (int f = 0; f < 3; ++f) run[f] = s_base[f] + s_sc[f][t] - loc[f];
+    for (int64_t i = lo; i < hi; ++i) {
+        for (int f = 0; f < 3; ++f) {
+            A.blk_off[f * nb + i] = run[f];
+            run[f] += A.blk_cnt[f * nb + i];
+        }
+    }
+    // fixed-order tree sum of the kept power
+    for (int off = 512; off >= 1; off >>= 1) {
+        __syncthreads();
+        if (t < off) s_d[t] += s_d[t + off];
+    }
+    __syncthreads();
+    const double pow_next = s_d[0];
+    if (t == 1023) {
+        A.acc->nR = (unsigned long long)(s_base[0] + s_sc[0][1023]);
+        A.acc->nT = (unsigned long long)(s_base[1] + s_sc[1][1023]);
+        const long long mt = s_sc[2][1023];
+        A.acc->m_total = (unsigned long long)(s_base[2] + mt);
+        A.acc->nM_iter += (unsigned long long)mt;
+    }
+    if (t == 0) A.acc->pow_next += pow_next;
+}
+
+__global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
+{
+    __shared__ int32_t s_w[3][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * 1024;
+    const int64_t nb = A.nb;
+    int64_t base[3] = {A.blk_off[blockIdx.x], A.blk_off[nb + blockIdx.x], A.blk_off[2 * nb + blockIdx.x]};
+    for (int sub = 0; sub < 4; ++sub) {
+        const int64_t r = tile + sub * 256 + threadIdx.x;
+        const bool in = r < A.n;
+        const bool fR = in && A.o.rms[r] == 0;
+        const bool fT = in && A.o.tms[r] == 0;
+        const bool fM = in && A.o.meas[r] == 1;
+        const uint64_t bR = __ballot(fR), bT = __ballot(fT), bM = __ballot(fM);
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        const int pR = __popcll(bR & below), pT = __popcll(bT & below), pM = __popcll(bM & below);
+        if (lane == 0) { s_w[0][wv] = __popcll(bR); s_w[1][wv] = __popcll(bT); s_w[2][wv] = __popcll(bM); }
+        __syncthreads();
+        int32_t wo[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
+        for (int w = 0; w < 4; ++w)
+            for (int f = 0; f < 3; ++f) {
+                if (w < wv) wo[f] += s_w[f][w];
+                tot[f] += s_w[f][w];
+            }
+        if (fR || fT || fM) {
+            const float dx = A.o.destx[r], dy = A.o.desty[r], dz = A.o.destz[r];
+            const int32_t mid = A.o.imid[r];
+            if (fR) {
+                const int64_t q = base[0] + wo[0] + pR;
+                A.nR.ox[q] = dx; A.nR.oy[q] = dy; A.nR.oz[q] = dz;
+                A.nR.dx[q] = A.o.rdx[r]; A.nR.dy[q] = A.o.rdy[r]; A.nR.dz[q] = A.o.rdz[r];
+                A.nR.pw[q] = A.o.rpw[r]; A.nR.pmid[q] = mid;
+            }
+            if (fT) {
+                const int64_t q = base[1] + wo[1] + pT;
+                A.nT.ox[q] = dx; A.nT.oy[q] = dy; A.nT.oz[q] = dz;
+                A.nT.dx[q] = A.o.tdx[r]; A.nT.dy[q] = A.o.tdy[r]; A.nT.dz[q] = A.o.tdz[r];
+                A.nT.pw[q] = A.o.tpw[r]; A.nT.pmid[q] = mid;
+            }
+            if (fM) {
+                const int64_t q = base[2] + wo[2] + pM;
+                A.mx[q] = dx; A.my[q] = dy; A.mz[q] = dz; A.mp[q] = A.o.pw[r]; A.mm[q] = mid;
+            }
+        }
+        for (int f = 0; f < 3; ++f) base[f] += tot[f];
+        __syncthreads();
+    }
+}
+
+// Append the refracted block after the reflected one (next population).
+__global__ __launch_bounds__(256) void k_append(RaysOut dst, RaysIn src, const DevAcc *acc)
+{
+    const int64_t nR = (int64_t)acc->nR, nT = (int64_t)acc->nT;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nT;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = nR + i;
+        dst.ox[q] = src.ox[i]; dst.oy[q] = src.oy[i]; dst.oz[q] = src.oz[i];
+        dst.dx[q] = src.dx[i]; dst.dy[q] = src.dy[i]; dst.dz[q] = src.dz[i];
+        dst.pw[q] = src.pw[i]; dst.pmid[q] = src.pmid[i];
+    }
+}
+
+// SoA xyz -> (n,4) rows with w = 0
+__global__ __launch_bounds__(256) void k_pack4(int64_t n, const float *__restrict__ x,
+                                               const float *__restrict__ y,
+                                               const float *__restrict__ z, float4 *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = make_float4(x[i], y[i], z[i], 0.0f);
+}
+
+// (n,4) rows -> SoA xyz
+__global__ __launch_bounds__(256) void k_unpack4(int64_t n, const float4 *__restrict__ in,
+                                                 float *__restrict__ x, float *__restrict__ y,
+                                                 float *__restrict__ z)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { const float4 v = in[i]; x[i] = v.x; y[i] = v.y; z[i] = v.z; }
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in kernels on the reference's (n,4) / [ray][mesh] device buffers.
+__global__ __launch_bounds__(256) void k_postproc_aos(PostprocAosArgs A)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n) return;
+    const int32_t K = A.K;
+    auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
+        const int64_t a = r * K + j;
+        t = A.tmin[a]; c = A.cnt[a]; i = A.itmp[a];
+    };
+    const PostOut po = postproc(K, A.prev_mid[r], A.mat_type, A.max_ray_len, slot);
+    const float4 o4 = A.origin[r], d4 = A.dir[r];
+    const f3 dest = ray_dest(mk3(o4.x, o4.y, o4.z), mk3(d4.x, d4.y, d4.z), po.t_min);
+    if (po.hit_mesh >= 0) A.entering[r] = po.entering;
+    A.n1[r] = po.n1; A.n2[r] = po.n2;
+    A.dest[r] = make_float4(dest.x, dest.y, dest.z, 0.0f);
+    A.imid[r] = po.hit_mesh; A.iidx[r] = po.hit_idx;
+}
+
+__global__ __launch_bounds__(256) void k_fresnel_aos(FresnelAosArgs A)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n) return;
+    const float4 o4 = A.origin[r], d4 = A.dir[r], e4 = A.dest[r];
+    const f3 dest = mk3(e4.x, e4.y, e4.z);
+    auto tri = [&](int32_t idx, f3 &v0, f3 &v1, f3 &v2) {
+        const float *v = A.verts + (int64_t)idx * 9;
+        v0 = mk3(v[0], v[1], v[2]); v1 = mk3(v[3], v[4], v[5]); v2 = mk3(v[6], v[7], v[8]);
+    };
+    const float pw_in = A.pow[r];
+    const ShadeOut s = shade(mk3(o4.x, o4.y, o4.z), mk3(d4.x, d4.y, d4.z), dest, pw_in, A.meas[r],
+                             A.imid[r], A.iidx[r], A.n1[r], A.n2[r], A.mat_type, A.ior, A.refl,
+                             A.diss, A.ior_env, tri);
+    if (s.pow != pw_in) A.pow[r] = s.pow;
+    A.meas[r] = s.meas;
+    const float4 e0 = make_float4(dest.x, dest.y, dest.z, 0.0f);
+    A.r_origin[r] = e0; A.t_origin[r] = e0;
+    A.r_dir[r] = make_float4(s.r_dir.x, s.r_dir.y, s.r_dir.z, 0.0f);
+    A.t_dir[r] = make_float4(s.t_dir.x, s.t_dir.y, s.t_dir.z, 0.0f);
+    A.r_pow[r] = s.r_pow; A.r_meas[r] = s.r_meas;
+    A.t_pow[r] = s.t_pow; A.t_meas[r] = s.t_meas;
+}
+
+// ---------------------------------------------------------------------------
+// Projection + binning.  Bin index = searchsorted(edges, v, 'right') - 1 with
+// the value equal to the last edge counted in the last bin (numpy histogramdd).
+static __device__ __forceinline__ int bin_of(double v, const double *__restrict__ e, int nbins)
+{
+    if (!(v >= e[0]) || !(v <= e[nbins])) return -1;   // outside (or NaN)
+    if (v == e[nbins]) return nbins - 1;
+    int lo = 0, hi = nbins;                              // e[lo] <= v < e[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (e[mid] <= v) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_project_hist(ProjArgs A)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    f3 p;
+    if (A.pos4) { const float4 v = A.pos4[i]; p = mk3(v.x, v.y, v.z); }
+    else p = mk3(A.px[i], A.py[i], A.pz[i]);
+    const f3 piv = mk3(A.piv[0], A.piv[1], A.piv[2]);
+    const f3 R0 = mk3(A.rot[0], A.rot[1], A.rot[2]);
+    const f3 R1 = mk3(A.rot[4], A.rot[5], A.rot[6]);
+    const f3 R2 = mk3(A.rot[8], A.rot[9], A.rot[10]);
+    float x, y, pc;
+    if (A.mode == 0) angular_project(p, piv, R0, R1, R2, A.pwr[i], x, y, pc);
+    else stereograph_project(p, piv, R0, R1, R2, A.pwr[i], x, y, pc);
+    if (A.x) { A.x[i] = x; A.y[i] = y; A.pc[i] = pc; }
+    const int bx = bin_of((double)x, A.xe, A.nx), by = bin_of((double)y, A.ye, A.ny);
+    if (bx >= 0 && by >= 0) atomicAdd(&A.H[(int64_t)bx * A.ny + by], (double)pc / A.div);
+}
+
+// Per-measure-mesh power of the measured record, one block per 64K records,
+// fixed-order sums (the host adds the block partials in order).
+__global__ __launch_bounds__(256) void k_mesh_sum(int64_t n, const float *__restrict__ mp,
+                                                  const int32_t *__restrict__ mm, int32_t mesh,
+                                                  double *__restrict__ out)
+{
+    __shared__ double s[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t lo = (int64_t)blockIdx.x * 65536;
+    const int64_t hi = lo + 65536 < n ? lo + 65536 : n;
+    double acc = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256)
+        if (mm[i] == mesh) acc += (double)mp[i];
+    acc = wave_sum(acc);
+    if (lane == 0) s[wv] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = ((s[0] + s[1]) + s[2]) + s[3];
+}
+
+}  // namespace lpck

@@ -1,0 +1,376 @@
+// lpc_math.hpp -- per-ray arithmetic of the LightPyCL bounce, shared by the HIP
+// kernels (lpc.hip) and the CPU-side property tests (tests/csrc/).
+//
+// Two kinds of code live here:
+//  * EXACT functions: the reference's arithmetic (kernel_reflect_refract_intersect.cl)
+//    operation for operation, compiled with FP contraction OFF, single-precision
+//    constants, IEEE division/sqrt.  Decisions (hit/miss, entering, n1/n2, TIR)
+//    and values (t, dest, children) are therefore bit-identical to the CPU oracle.
+//  * the CONSERVATIVE bounding-sphere filter used by the hot loop: a cheap test
+//    that is a superset of the exact Moller-Trumbore acceptance (see
+//    filter_record() for the margin derivation); only pairs that pass it are
+//    re-tested exactly, so the fast path gives the exact result.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define LPC_HD __host__ __device__ __forceinline__
+#else
+#define LPC_HD static inline
+#endif
+
+#if defined(__clang__)
+#define LPC_EXACT _Pragma("clang fp contract(off)")
+#else
+#define LPC_EXACT
+#endif
+
+namespace lpc {
+
+struct f3 { float x, y, z; };
+
+LPC_HD f3 mk3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+LPC_HD f3 add3(f3 a, f3 b) { LPC_EXACT return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+LPC_HD f3 sub3(f3 a, f3 b) { LPC_EXACT return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+LPC_HD f3 scl3(f3 a, float s) { LPC_EXACT return mk3(a.x * s, a.y * s, a.z * s); }
+LPC_HD f3 neg3(f3 a) { return mk3(-a.x, -a.y, -a.z); }
+// OpenCL dot/cross for float3 (sum order x, y, z).
+LPC_HD float dot3(f3 a, f3 b) { LPC_EXACT return a.x * b.x + a.y * b.y + a.z * b.z; }
+LPC_HD f3 cross3(f3 a, f3 b) {
+    LPC_EXACT
+    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+LPC_HD float len3(f3 a) { LPC_EXACT return sqrtf(dot3(a, a)); }
+LPC_HD f3 nrm3(f3 a) { LPC_EXACT float l = len3(a); return mk3(a.x / l, a.y / l, a.z / l); }
+
+// ---------------------------------------------------------------------------
+// Moller-Trumbore exactly as intersect_triangle (.cl:50-101), with the two edge
+// vectors precomputed (E1 = V1-V0, E2 = V2-V0 are the same single roundings the
+// reference performs per call, .cl:72-73).  Returns 1 and t on a u/v hit.
+LPC_HD int mt_exact(f3 O, f3 D, f3 V0, f3 E1, f3 E2, float *t)
+{
+    LPC_EXACT
+    const float EPSILON_NUM = 0.000001f;
+    f3 P = cross3(D, E2);
+    float DEN = dot3(P, E1);
+    if (DEN > -EPSILON_NUM && DEN < EPSILON_NUM) return 0;
+    float iDEN = 1.0f / DEN;
+    f3 T = sub3(O, V0);
+    float u = dot3(P, T) * iDEN;
+    if (u < 0.0f || u > 1.0f) return 0;
+    f3 Q = cross3(T, E1);
+    float v = dot3(Q, D) * iDEN;
+    if (v < 0.0f || u + v > 1.0f) return 0;
+    *t = dot3(Q, E2) * iDEN;
+    return 1;
+}
+
+// Accumulator update of the intersect kernel's inner loop (.cl:277-283).
+LPC_HD void mt_accumulate(f3 O, f3 D, f3 V0, f3 E1, f3 E2, int32_t idx, float eps,
+                          float &tmin, int32_t &imin, int32_t &cnt)
+{
+    float t;
+    if (mt_exact(O, D, V0, E1, E2, &t) && t > eps) {
+        if (t < tmin) { tmin = t; imin = idx; }
+        cnt += 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// intersect_postproc (.cl:105-240) given the per-mesh (slot) results of one ray.
+// `slot(j, t, c)` must return slot j's min t and hit count.
+struct PostOut { int32_t hit_mesh, hit_idx, n1, n2, entering; float t_min; };
+
+template <class SlotFn>
+LPC_HD PostOut postproc(int32_t K, int32_t prev, const int32_t *mat_type, float max_ray_len,
+                        SlotFn slot)
+{
+    LPC_EXACT
+    const float EPSILON = 0.000001f * max_ray_len;
+    PostOut o;
+    o.hit_mesh = -1; o.hit_idx = -1; o.n1 = -1; o.n2 = -1; o.entering = -1;
+    float t_min = max_ray_len;
+    int32_t hit_cnt = 0;
+    for (int32_t j = 0; j < K; ++j) {                                   // .cl:127-135
+        float tj; int32_t cj, ij;
+        slot(j, tj, cj, ij);
+        if (tj < t_min) { t_min = tj; o.hit_mesh = j; o.hit_idx = ij; hit_cnt = cj; }
+    }
+    if (o.hit_mesh >= 0) {
+        int32_t entering = 1 - (hit_cnt % 2);                            // .cl:142
+        o.entering = entering;
+        if (prev == -2 || prev == -1) {                                  // .cl:145-166
+            if (entering == 1) { o.n1 = -1; o.n2 = o.hit_mesh; }
+            else { o.n1 = o.hit_mesh; o.n2 = -1; }
+        } else {                                                         // .cl:167-177
+            if (entering == 1) { o.n1 = prev; o.n2 = o.hit_mesh; }
+            else { o.n1 = o.hit_mesh; o.n2 = -1; }
+        }
+        float t_minmin = t_min, t_maxmin = t_min, t_minmax = max_ray_len;
+        int32_t maxmin_entering = 0, maxmin_idx = -1, minmax_idx = -1;
+        for (int32_t j = 0; j < K; ++j) {                               // .cl:193-214
+            int32_t mt = mat_type[j];
+            if (mt == 0 || mt == 4) {
+                float tj; int32_t cj, ij;
+                slot(j, tj, cj, ij);
+                int32_t ent = 1 - (cj % 2);
+                if (tj <= t_minmin + EPSILON && tj >= t_maxmin) {
+                    t_maxmin = tj; maxmin_idx = j; maxmin_entering = ent;
+                }
+                if (tj > t_minmin + EPSILON && ent == 0 && tj <= t_minmax) {
+                    t_minmax = tj; minmax_idx = j;
+                }
+            }
+        }
+        if (maxmin_entering == 1) { t_min = t_maxmin; o.n2 = maxmin_idx; }   // .cl:216-229
+        else {
+            if (maxmin_idx >= 0) t_min = t_maxmin;
+            if (minmax_idx >= 0) o.n2 = minmax_idx;
+        }
+    }
+    o.t_min = t_min;
+    return o;
+}
+
+// dest = o + d * t_min (.cl:237)
+LPC_HD f3 ray_dest(f3 O, f3 D, float t) { LPC_EXACT return add3(O, scl3(D, t)); }
+
+// ---------------------------------------------------------------------------
+// reflect_refract_rays (.cl:346-474) for one ray, reflect_refract (.cl:293-343)
+// inlined.  Inputs are the ray, its postproc result and the material tables;
+// `tri(idx, v0, v1, v2)` gathers the hit triangle's vertices.
+struct ShadeOut {
+    float pow;                 // possibly dissipated input power (.cl:392)
+    int32_t meas;              // in-ray measured state after the kernel
+    f3 r_dir, t_dir;
+    float r_pow, t_pow;
+    int32_t r_meas, t_meas;
+};
+
+template <class TriFn>
+LPC_HD ShadeOut shade(f3 O, f3 D, f3 dest, float pw, int32_t meas_in, int32_t rmid,
+                      int32_t ridx, int32_t n1id, int32_t n2id, const int32_t *mat_type,
+                      const float *ior, const float *refl, const float *diss, float ior_env,
+                      TriFn tri)
+{
+    LPC_EXACT
+    const float EPSILON_NUM = 0.000001f;
+    ShadeOut s;
+    int32_t mesh_mat = 2;
+    float R_mesh = 0.0f;
+    if (rmid >= 0) { mesh_mat = mat_type[rmid]; R_mesh = refl[rmid]; }
+    float IOR_in = ior_env, IOR_n2 = ior_env;
+    if (n1id >= 0) {                                                     // .cl:385-394
+        IOR_in = ior[n1id];
+        if (mat_type[n1id] == 0 && diss[n1id] > EPSILON_NUM) {
+            float ray_len = len3(sub3(dest, O));
+            pw = pw * expf(-diss[n1id] * ray_len);
+        }
+    }
+    if (n2id >= 0) IOR_n2 = ior[n2id];
+    s.pow = pw;
+    s.meas = meas_in;
+    const f3 zero = mk3(0.0f, 0.0f, 0.0f);
+    // dead children by default (also what the NaN-TIR path leaves)
+    s.r_dir = zero; s.t_dir = zero; s.r_pow = 0.0f; s.t_pow = 0.0f; s.r_meas = -1; s.t_meas = -1;
+    if (meas_in == 0 && rmid >= 0 && (mesh_mat == 0 || mesh_mat == 1)) {   // .cl:408
+        f3 v0, v1, v2;
+        tri(ridx, v0, v1, v2);
+        f3 nrm_in = nrm3(cross3(sub3(v1, v0), sub3(v2, v1)));           // .cl:413
+        // reflect_refract (.cl:293-343)
+        f3 nrm = nrm_in;
+        float n1 = IOR_in, n2 = IOR_n2;
+        float r = n1 / n2;
+        float cosT1 = -dot3(nrm, D);
+        if (cosT1 < 0.0f) { nrm = neg3(nrm_in); cosT1 = -dot3(nrm, D); }
+        float TIR_check = 1.0f - (r * r) * (1.0f - (cosT1 * cosT1));
+        f3 rdir = zero, tdir = zero;
+        float rp = 0.0f, tp = 0.0f;
+        int32_t rm = -1, tm = -1;
+        if (TIR_check >= 0.0f) {
+            float cosT2 = sqrtf(TIR_check);
+            float a = fabsf((n1 * cosT1 - n2 * cosT2) / (n1 * cosT1 + n2 * cosT2));
+            float b = fabsf((n1 * cosT2 - n2 * cosT1) / (n1 * cosT2 + n2 * cosT1));
+            float Rs = a * a, Rp = b * b;
+            float reflect_power = pw * (Rs + Rp) / 2.0f;
+            rdir = add3(D, scl3(nrm, 2.0f * cosT1));
+            rp = reflect_power; rm = 0;
+            tdir = add3(scl3(D, r), scl3(nrm, r * cosT1 - cosT2));
+            tp = pw - reflect_power; tm = 0;
+        } else if (TIR_check < 0.0f) {
+            rdir = add3(D, scl3(nrm, 2.0f * cosT1));
+            rp = pw; rm = 0;
+            tdir = zero; tp = 0.0f; tm = -1;
+        }
+        if (mesh_mat == 0) {                                             // .cl:429-439
+            s.r_dir = rdir; s.r_pow = rp; s.r_meas = rm;
+            s.t_dir = tdir; s.t_pow = tp; s.t_meas = tm;
+        } else {                                                         // .cl:440-452 mirror
+            s.r_dir = rdir; s.r_pow = pw * R_mesh; s.r_meas = rm;
+            s.t_dir = zero; s.t_pow = 0.0f; s.t_meas = -1;
+        }
+    } else {                                                             // .cl:455-472
+        if (mesh_mat == 2 || rmid < 0) s.meas = -1;
+        if (mesh_mat == 3 && rmid >= 0) s.meas = 1;
+    }
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// angular_project (.cl:509-538) and stereograph_project (.cl:488-506).
+LPC_HD void angular_project(f3 p, f3 piv, f3 R0, f3 R1, f3 R2, float pwr, float &x, float &y,
+                            float &pc)
+{
+    LPC_EXACT
+    const float EPSILON = 0.000001f;
+    f3 vec = sub3(p, piv);
+    float u = dot3(vec, R0) + piv.x;
+    float v = dot3(vec, R1) + piv.y;
+    float w = dot3(vec, R2) + piv.z;
+    float l = sqrtf(u * u + v * v + w * w);
+    f3 vr = mk3(u / l, v / l, w / l);
+    float cosT = dot3(mk3(0.0f, 0.0f, 1.0f), vr);
+    float phi = atan2f(v, u);
+    float r = acosf(cosT);
+    float A = 1.0f;
+    if (r > EPSILON) A = sinf(r) / r;
+    x = r * cosf(phi);
+    y = r * sinf(phi);
+    pc = pwr / A;
+}
+
+LPC_HD void stereograph_project(f3 p, f3 piv, f3 R0, f3 R1, f3 R2, float pwr, float &x,
+                                float &y, float &pc)
+{
+    LPC_EXACT
+    f3 vec = sub3(p, piv);
+    float u = dot3(vec, R0) + piv.x;
+    float v = dot3(vec, R1) + piv.y;
+    float w = dot3(vec, R2) + piv.z;
+    float l = sqrtf(u * u + v * v + w * w);
+    float xt = u / (l + w), yt = v / (l + w);
+    float q = 1.0f + xt * xt + yt * yt;
+    float A = 4.0f / (q * q);
+    x = xt; y = yt; pc = pwr / A;
+}
+
+// ---------------------------------------------------------------------------
+// Conservative bounding-sphere filter.
+//
+// For a ray with origin O and unit direction n (computed in float) and a
+// triangle with bounding sphere (c, rho), the squared distance from c to the
+// ray's line is  ww - wd^2  with w = c - O, ww = w.w, wd = w.n.  The filter
+// accepts (candidate) when
+//       d = ww * (1 - B) - A - wd^2  <=  0
+// i.e. dist^2 <= A + B ww.  A and B inflate the sphere enough that every pair
+// the exact Moller-Trumbore test accepts is a candidate:
+//  * rounding of ww, wd, n in float: |error| <= ~16 eps ww  (term kB_round);
+//  * Moller-Trumbore's own error: an accepted pair's line passes within
+//    ~c eps |T| |E|^2/|E1 x E2| of the triangle (the barycentric error of a
+//    nearly-parallel ray times the ray's slope), |T| <= |w| + rho;  with
+//    (a+b)^2 <= (1+h) a^2 + (1+1/h) b^2 this gives the rho^2 and ww terms.
+// The constants are deliberately generous (see tests/test_filter_superset.py,
+// which measures the actual worst case on adversarial inputs).
+// Triangles with an exactly-zero edge are never accepted by Moller-Trumbore
+// (DEN == 0) and get A = +inf ("never", d = +inf).  Triangles with |E1||E2| below
+// 1e-6/Dcap can never reach |DEN| >= 1e-6 for rays with |D| <= Dcap and are
+// "never" too (the engine checks |D| <= Dcap at run time).
+struct FiltRec {
+    float cx, cy, cz;   // sphere centre (float)
+    float onemB;        // 1 - B
+    float negA;         // -A
+    int32_t idx;        // original triangle index
+    int32_t pad0, pad1;
+};
+
+// Four filter records in SoA form: what one iteration of the hot loop reads
+// with a single 128-byte scalar load.
+struct FiltGroup {
+    float cx[4], cy[4], cz[4], onemB[4], negA[4];
+    int32_t idx[4];
+    int32_t pad[8];
+};
+
+struct ExactRec {       // V0, E1 = V1-V0, E2 = V2-V0 (float, exactly as the reference)
+    float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, pad0, pad1, pad2;
+};
+
+// Host: build the filter record of triangle (V0,V1,V2) given as floats.
+#if defined(__HIPCC__)
+static inline __host__ FiltRec filter_record(
+#else
+static inline FiltRec filter_record(
+#endif
+                                    const float *V0, const float *V1, const float *V2,
+                                    int32_t idx, double Dcap)
+{
+    const double eps = 1.0 / 16777216.0;   // 2^-24
+    FiltRec r;
+    r.idx = idx; r.pad0 = 0; r.pad1 = 0;
+    double a[3], b[3], c3[3], p0[3];
+    float e1f[3], e2f[3];
+    for (int k = 0; k < 3; ++k) {
+        p0[k] = V0[k];
+        a[k] = (double)V1[k] - (double)V0[k];
+        b[k] = (double)V2[k] - (double)V0[k];
+        e1f[k] = V1[k] - V0[k];
+        e2f[k] = V2[k] - V0[k];
+    }
+    double n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    double nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+    double aa = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
+    double bb = b[0] * b[0] + b[1] * b[1] + b[2] * b[2];
+    double cm[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    double cc = cm[0] * cm[0] + cm[1] * cm[1] + cm[2] * cm[2];
+    // minimal enclosing sphere of the triangle
+    double ctr[3];
+    bool obtuse = (aa + bb <= cc) || (aa + cc <= bb) || (bb + cc <= aa) || nn <= 0.0;
+    if (obtuse) {
+        const float *P = V1, *Q = V2;            // longest edge midpoint
+        if (aa >= bb && aa >= cc) { P = V0; Q = V1; }
+        else if (bb >= aa && bb >= cc) { P = V0; Q = V2; }
+        for (int k = 0; k < 3; ++k) ctr[k] = 0.5 * ((double)P[k] + (double)Q[k]);
+    } else {
+        // circumcentre: V0 + ((|a|^2 b - |b|^2 a) x n) / (2 |n|^2)
+        double m[3] = {aa * b[0] - bb * a[0], aa * b[1] - bb * a[1], aa * b[2] - bb * a[2]};
+        double x[3] = {m[1] * n[2] - m[2] * n[1], m[2] * n[0] - m[0] * n[2], m[0] * n[1] - m[1] * n[0]};
+        for (int k = 0; k < 3; ++k) ctr[k] = p0[k] + x[k] / (2.0 * nn);
+    }
+    r.cx = (float)ctr[0]; r.cy = (float)ctr[1]; r.cz = (float)ctr[2];
+    double fc[3] = {r.cx, r.cy, r.cz};
+    double rho2 = 0.0;
+    const float *Vs[3] = {V0, V1, V2};
+    for (int v = 0; v < 3; ++v) {
+        double d2 = 0.0;
+        for (int k = 0; k < 3; ++k) { double q = (double)Vs[v][k] - fc[k]; d2 += q * q; }
+        if (d2 > rho2) rho2 = d2;
+    }
+    rho2 *= (1.0 + 1e-6);
+    bool zero_edge = (e1f[0] == 0.0f && e1f[1] == 0.0f && e1f[2] == 0.0f) ||
+                     (e2f[0] == 0.0f && e2f[1] == 0.0f && e2f[2] == 0.0f);
+    double e1n = sqrt((double)e1f[0] * e1f[0] + (double)e1f[1] * e1f[1] + (double)e1f[2] * e1f[2]);
+    double e2n = sqrt((double)e2f[0] * e2f[0] + (double)e2f[1] * e2f[1] + (double)e2f[2] * e2f[2]);
+    bool tiny = e1n * e2n * Dcap * (1.0 + 1e-4) < 1e-6;
+    if (zero_edge || tiny) {           // never a candidate: d = +inf
+        r.onemB = 1.0f; r.negA = INFINITY;
+        return r;
+    }
+    double emax2 = aa > bb ? aa : bb;
+    emax2 = emax2 > cc ? emax2 : cc;
+    double asp = (nn > 0.0) ? emax2 / sqrt(nn) : INFINITY;   // |E|^2 / |E1 x E2|
+    const double h = 0.05, kmt = 256.0, kround = 64.0;
+    double g2 = (1.0 + 1.0 / h) * 2.0 * (kmt * eps * asp) * (kmt * eps * asp);
+    double A = rho2 * ((1.0 + h) + g2);
+    double B = g2 + kround * eps;
+    if (!(B < 0.5)) { r.onemB = -1e30f; r.negA = 0.0f; return r; }   // always a candidate
+    float onemB = (float)(1.0 - B * (1.0 + 1e-6));
+    if ((double)onemB > 1.0 - B) onemB = nextafterf(onemB, -INFINITY);
+    float Af = (float)(A * (1.0 + 1e-6));
+    if ((double)Af < A) Af = nextafterf(Af, INFINITY);
+    r.onemB = onemB; r.negA = -Af;
+    return r;
+}
+
+}  // namespace lpc

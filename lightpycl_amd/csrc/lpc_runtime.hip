@@ -1,0 +1,1011 @@
+// lpc_runtime.hip -- host runtime behind the C ABI of include/lpc.h.
+//
+// One lpc_handle per GPU: a HIP stream, the uploaded scene (filter / exact /
+// vertex records + mesh tables), a chunk workspace and the device-resident ray
+// population of a trace.  All launches go to the handle's stream.
+#include "lpc_kernels.hip"
+#include "lpc.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+using namespace lpck;
+
+namespace {
+
+struct DBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+// 8 SoA arrays (ox oy oz dx dy dz pw | pmid) in one allocation.
+struct Pop {
+    DBuf buf;
+    int64_t cap = 0;
+    float *f(int k) const { return (float *)buf.p + (size_t)k * cap; }
+    int32_t *pmid() const { return (int32_t *)((float *)buf.p + (size_t)7 * cap); }
+    RaysIn in(int64_t off = 0) const {
+        RaysIn r;
+        r.ox = f(0) + off; r.oy = f(1) + off; r.oz = f(2) + off;
+        r.dx = f(3) + off; r.dy = f(4) + off; r.dz = f(5) + off;
+        r.pw = f(6) + off; r.pmid = pmid() + off;
+        return r;
+    }
+    RaysOut out(int64_t off = 0) const {
+        RaysOut r;
+        r.ox = f(0) + off; r.oy = f(1) + off; r.oz = f(2) + off;
+        r.dx = f(3) + off; r.dy = f(4) + off; r.dz = f(5) + off;
+        r.pw = f(6) + off; r.pmid = pmid() + off;
+        return r;
+    }
+};
+
+struct PieceTable {
+    DBuf pieces, slot_plo, slot_phi;
+    int32_t npieces = 0;
+};
+
+const int kShadeF = 12;   // float arrays of the shade outputs
+const int kShadeI = 8;    // int arrays
+
+}  // namespace
+
+struct lpc_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    char name[256] = {0};
+    int cus = 0;
+    // scene
+    int32_t M = 0, K = 0, Mpad = 0;
+    std::vector<float> hv0, hv1, hv2;               // host copies (record rebuilds)
+    std::vector<int32_t> run_lo, run_hi, run_flo, run_fhi;
+    std::vector<int32_t> slot_run;
+    std::vector<int32_t> meas_meshes;
+    DBuf d_frec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
+    double dcap = 16.0;
+    std::map<int32_t, PieceTable> ptabs;
+    // workspace
+    int64_t chunk = 0;                              // rays per chunk (0 -> default)
+    int64_t ws_rays = 0;
+    int64_t ws_part = 0;                            // partial-array elements
+    DBuf w_pt, w_pi, w_pc, w_st, w_si, w_sc, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
+    DBuf w_soa, w_stage;
+    // trace
+    Pop A, B, T, I;
+    int64_t n_cur = 0, n_init = 0;
+    float max_ray_len = 1e3f, ior_env = 1.0f;
+    bool traced_ready = false;
+    DBuf m_buf;                                     // measured: x y z pw | mesh
+    int64_t m_cap = 0, m_total = 0;
+    DBuf d_acc;
+    DBuf d_tmp;                                     // misc small device scratch
+    // profiling
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest;
+    std::vector<hipEvent_t> ev_pool;
+    double prof_isect_ms = 0.0, prof_rest_ms = 0.0;
+    int64_t prof_launches = 0, prof_pairs = 0;
+};
+
+static std::string g_open_err;
+
+static int set_err(lpc_handle *h, int code, const std::string &msg)
+{
+    if (h) h->err = msg; else g_open_err = msg;
+    return code;
+}
+
+#define HIPCHK(h, expr)                                                                     \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return set_err(h, LPC_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define RETIF(x)                  \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
+    } while (0)
+
+static int dalloc(lpc_handle *h, DBuf &b, size_t bytes, bool keep = false)
+{
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return 0;
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess)
+        return set_err(h, LPC_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    if (keep && b.p && b.bytes) {
+        HIPCHK(h, hipMemcpyAsync(p, b.p, b.bytes, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    if (b.p) (void)hipFree(b.p);
+    b.p = p;
+    b.bytes = bytes;
+    return 0;
+}
+
+static void dfree(DBuf &b)
+{
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+static int pop_reserve(lpc_handle *h, Pop &P, int64_t n)
+{
+    if (P.cap >= n && P.buf.p) return 0;
+    int64_t cap = std::max<int64_t>(n, 1024);
+    dfree(P.buf);
+    RETIF(dalloc(h, P.buf, (size_t)cap * 8 * 4));
+    P.cap = cap;
+    return 0;
+}
+
+static inline unsigned grid1(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+
+// ---------------------------------------------------------------------------
+// scene records
+static int build_records(lpc_handle *h)
+{
+    const int32_t M = h->M;
+    std::vector<FiltRec> fr;
+    fr.reserve((size_t)M + 4 * h->run_lo.size());
+    h->run_flo.clear();
+    h->run_fhi.clear();
+    for (size_t r = 0; r < h->run_lo.size(); ++r) {
+        h->run_flo.push_back((int32_t)fr.size());
+        for (int32_t i = h->run_lo[r]; i < h->run_hi[r]; ++i)
+            fr.push_back(filter_record(&h->hv0[4 * (size_t)i], &h->hv1[4 * (size_t)i],
+                                       &h->hv2[4 * (size_t)i], i, h->dcap));
+        while (fr.size() % 4) {   // pad the run with "never" records
+            FiltRec z;
+            z.cx = z.cy = z.cz = 0.0f; z.onemB = 1.0f; z.negA = INFINITY; z.idx = -1;
+            z.pad0 = z.pad1 = 0;
+            fr.push_back(z);
+        }
+        h->run_fhi.push_back((int32_t)fr.size());
+    }
+    h->Mpad = (int32_t)fr.size();
+    // SoA groups of 4 records + one spare group for the loop's prefetch
+    const size_t ng = fr.size() / 4 + 1;
+    std::vector<FiltGroup> gs(ng);
+    memset(gs.data(), 0, ng * sizeof(FiltGroup));
+    for (size_t i = 0; i < fr.size(); ++i) {
+        FiltGroup &G = gs[i / 4];
+        const int k = (int)(i % 4);
+        G.cx[k] = fr[i].cx; G.cy[k] = fr[i].cy; G.cz[k] = fr[i].cz;
+        G.onemB[k] = fr[i].onemB; G.negA[k] = fr[i].negA; G.idx[k] = fr[i].idx;
+    }
+    for (int k = 0; k < 4; ++k) { gs[ng - 1].onemB[k] = 1.0f; gs[ng - 1].negA[k] = INFINITY; gs[ng - 1].idx[k] = -1; }
+    RETIF(dalloc(h, h->d_frec, ng * sizeof(FiltGroup)));
+    HIPCHK(h, hipMemcpy(h->d_frec.p, gs.data(), ng * sizeof(FiltGroup), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Piece table for a launch of n rays: each run split into slices of S records
+// so that blocks_x * pieces fills the GPU.
+static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
+{
+    const int64_t bx = std::max<int64_t>(1, (n + 511) / 512);
+    const int64_t target_blocks = 4096;
+    int32_t g = (int32_t)std::max<int64_t>(1, (target_blocks + bx - 1) / bx);
+    g = std::min<int32_t>(g, 4096);
+    auto it = h->ptabs.find(g);
+    if (it != h->ptabs.end()) { *out = &it->second; return 0; }
+    int64_t S = (h->Mpad + g - 1) / g;
+    S = std::max<int64_t>(256, (S + 3) / 4 * 4);
+    std::vector<Piece> pcs;
+    std::vector<int32_t> rplo, rphi;
+    for (size_t r = 0; r < h->run_flo.size(); ++r) {
+        rplo.push_back((int32_t)pcs.size());
+        for (int64_t a = h->run_flo[r]; a < h->run_fhi[r]; a += S) {
+            Piece p;
+            p.lo = (int32_t)a;
+            p.hi = (int32_t)std::min<int64_t>(a + S, h->run_fhi[r]);
+            pcs.push_back(p);
+        }
+        rphi.push_back((int32_t)pcs.size());
+    }
+    if (pcs.size() > 65535) return set_err(h, LPC_E_ARG, "too many triangle pieces");
+    std::vector<int32_t> splo(h->K), sphi(h->K);
+    for (int32_t j = 0; j < h->K; ++j) {
+        int32_t r = h->slot_run[j];
+        splo[j] = r >= 0 ? rplo[r] : 0;
+        sphi[j] = r >= 0 ? rphi[r] : 0;
+    }
+    PieceTable &t = h->ptabs[g];
+    RETIF(dalloc(h, t.pieces, pcs.size() * sizeof(Piece)));
+    RETIF(dalloc(h, t.slot_plo, splo.size() * 4));
+    RETIF(dalloc(h, t.slot_phi, sphi.size() * 4));
+    HIPCHK(h, hipMemcpy(t.pieces.p, pcs.data(), pcs.size() * sizeof(Piece), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(t.slot_plo.p, splo.data(), splo.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(t.slot_phi.p, sphi.data(), sphi.size() * 4, hipMemcpyHostToDevice));
+    t.npieces = (int32_t)pcs.size();
+    *out = &t;
+    return 0;
+}
+
+static int64_t chunk_rays(const lpc_handle *h)
+{
+    return h->chunk > 0 ? h->chunk : (int64_t)8 << 20;
+}
+
+// Workspace for a chunk of `n` rays (partials sized pieces(n) * n).
+static int ensure_ws(lpc_handle *h, int64_t n)
+{
+    PieceTable *pt;
+    RETIF(piece_table(h, n, &pt));
+    const int64_t pe = (int64_t)pt->npieces * n;
+    if (n <= h->ws_rays && pe <= h->ws_part) return 0;
+    if (pe > h->ws_part) {
+        const int64_t PE = std::max(pe, h->ws_part);
+        RETIF(dalloc(h, h->w_pt, (size_t)PE * 4));
+        RETIF(dalloc(h, h->w_pi, (size_t)PE * 4));
+        RETIF(dalloc(h, h->w_pc, (size_t)PE * 4));
+        h->ws_part = PE;
+    }
+    if (n > h->ws_rays) {
+        const int64_t C = n;
+        RETIF(dalloc(h, h->w_st, (size_t)h->K * C * 4));
+        RETIF(dalloc(h, h->w_si, (size_t)h->K * C * 4));
+        RETIF(dalloc(h, h->w_sc, (size_t)h->K * C * 4));
+        RETIF(dalloc(h, h->w_shf, (size_t)kShadeF * C * 4));
+        RETIF(dalloc(h, h->w_shi, (size_t)kShadeI * C * 4));
+        const int64_t nb = (C + 1023) / 1024;
+        RETIF(dalloc(h, h->w_blk_cnt, (size_t)3 * nb * 4));
+        RETIF(dalloc(h, h->w_blk_off, (size_t)3 * nb * 8));
+        RETIF(dalloc(h, h->w_blk_pow, (size_t)nb * 8));
+        RETIF(dalloc(h, h->w_soa, (size_t)8 * C * 4));
+        RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
+        h->ws_rays = C;
+    }
+    return 0;
+}
+
+static ShadeOutPtrs shade_ptrs(lpc_handle *h, bool extra)
+{
+    const size_t C = (size_t)h->ws_rays;
+    float *f = (float *)h->w_shf.p;
+    int32_t *i = (int32_t *)h->w_shi.p;
+    ShadeOutPtrs o;
+    o.destx = f + 0 * C; o.desty = f + 1 * C; o.destz = f + 2 * C; o.pw = f + 3 * C;
+    o.rdx = f + 4 * C; o.rdy = f + 5 * C; o.rdz = f + 6 * C; o.rpw = f + 7 * C;
+    o.tdx = f + 8 * C; o.tdy = f + 9 * C; o.tdz = f + 10 * C; o.tpw = f + 11 * C;
+    o.imid = i + 0 * C; o.meas = i + 1 * C; o.rms = i + 2 * C; o.tms = i + 3 * C;
+    if (extra) { o.iidx = i + 4 * C; o.n1 = i + 5 * C; o.n2 = i + 6 * C; o.ent = i + 7 * C; }
+    else { o.iidx = o.n1 = o.n2 = o.ent = nullptr; }
+    return o;
+}
+
+static hipEvent_t ev_get(lpc_handle *h)
+{
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Resolve recorded event pairs (after a stream sync).
+static void prof_resolve(lpc_handle *h)
+{
+    for (auto &pr : h->ev_isect) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_isect_ms += ms;
+        h->ev_pool.push_back(pr.first);
+        h->ev_pool.push_back(pr.second);
+    }
+    h->ev_isect.clear();
+    for (auto &pr : h->ev_rest) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_rest_ms += ms;
+        h->ev_pool.push_back(pr.first);
+        h->ev_pool.push_back(pr.second);
+    }
+    h->ev_rest.clear();
+}
+
+// intersect + combine for n rays of `in` into the slot arrays (or a caller's
+// [ray][mesh] buffers when st_user != NULL).
+static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
+                         float *st_user, int32_t *si_user, int32_t *sc_user)
+{
+    RETIF(ensure_ws(h, n));
+    PieceTable *pt;
+    RETIF(piece_table(h, n, &pt));
+    const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
+    dim3 grid((unsigned)((n + 511) / 512), (unsigned)pt->npieces);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+    hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, n,
+                       (const FiltGroup *)h->d_frec.p, (const ExactRec *)h->d_xrec.p,
+                       (const Piece *)pt->pieces.p, eps, max_ray_len, (float *)h->w_pt.p,
+                       (int32_t *)h->w_pi.p, (int32_t *)h->w_pc.p);
+    HIPCHK(h, hipGetLastError());
+    if (h->prof) {
+        (void)hipEventRecord(e1, h->stream);
+        h->ev_isect.push_back({e0, e1});
+        h->prof_launches += 1;
+        h->prof_pairs += n * (int64_t)h->Mpad;
+    }
+    if (st_user) {
+        hipLaunchKernelGGL(k_combine, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
+                           (const int32_t *)pt->slot_plo.p, (const int32_t *)pt->slot_phi.p,
+                           (const float *)h->w_pt.p, (const int32_t *)h->w_pi.p,
+                           (const int32_t *)h->w_pc.p, max_ray_len, st_user, si_user, sc_user,
+                           (int64_t)1, (int64_t)h->K, 1);
+    } else {
+        hipLaunchKernelGGL(k_combine, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
+                           (const int32_t *)pt->slot_plo.p, (const int32_t *)pt->slot_phi.p,
+                           (const float *)h->w_pt.p, (const int32_t *)h->w_pi.p,
+                           (const int32_t *)h->w_pc.p, max_ray_len, (float *)h->w_st.p,
+                           (int32_t *)h->w_si.p, (int32_t *)h->w_sc.p, (int64_t)n, (int64_t)1, 0);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+static int run_shade(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, int64_t n,
+                     float max_ray_len, float ior_env, bool extra)
+{
+    ShadeArgs A;
+    A.in = in; A.meas_in = meas_in; A.n = n; A.K = h->K;
+    A.st = (const float *)h->w_st.p; A.si = (const int32_t *)h->w_si.p; A.sc = (const int32_t *)h->w_sc.p;
+    A.mat_type = (const int32_t *)h->d_mat.p; A.ior = (const float *)h->d_ior.p;
+    A.refl = (const float *)h->d_refl.p; A.diss = (const float *)h->d_diss.p;
+    A.verts = (const float *)h->d_verts.p;
+    A.max_ray_len = max_ray_len; A.ior_env = ior_env;
+    A.o = shade_ptrs(h, extra);
+    hipLaunchKernelGGL(k_shade, dim3(grid1(n)), dim3(256), 0, h->stream, A);
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+// If |D| of any upcoming ray exceeds the filter's Dcap, rebuild the filter
+// records without the tiny-triangle culling (Dcap = inf).
+static int check_dcap(lpc_handle *h, double dmax2)
+{
+    if (dmax2 <= h->dcap * h->dcap * (1.0 - 1e-6)) return 0;
+    h->dcap = INFINITY;
+    return build_records(h);
+}
+
+extern "C" {
+
+int lpc_abi_version(void) { return LPC_ABI_VERSION; }
+
+int lpc_device_count(int *count)
+{
+    if (!count) return set_err(nullptr, LPC_E_ARG, "count is NULL");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return 0;
+}
+
+int lpc_open(int device, lpc_handle **out)
+{
+    if (!out) return set_err(nullptr, LPC_E_ARG, "out is NULL");
+    *out = nullptr;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess || c == 0)
+        return set_err(nullptr, LPC_E_HIP, std::string("no HIP device: ") + hipGetErrorString(e));
+    if (device < 0 || device >= c)
+        return set_err(nullptr, LPC_E_ARG, "device ordinal " + std::to_string(device) + " out of range");
+    lpc_handle *h = new lpc_handle();
+    h->device = device;
+    e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        return set_err(nullptr, LPC_E_HIP, std::string("stream: ") + hipGetErrorString(e));
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+        snprintf(h->name, sizeof(h->name), "%s (%s)", prop.name, prop.gcnArchName);
+        h->cus = prop.multiProcessorCount;
+    }
+    int rc = dalloc(h, h->d_acc, sizeof(DevAcc));
+    if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
+    *out = h;
+    return 0;
+}
+
+int lpc_close(lpc_handle *h)
+{
+    if (!h) return 0;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    DBuf *bufs[] = {&h->d_frec, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
+                    &h->d_diss, &h->w_pt, &h->w_pi, &h->w_pc, &h->w_st, &h->w_si, &h->w_sc,
+                    &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
+                    &h->w_stage, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
+                    &h->d_acc, &h->d_tmp};
+    for (DBuf *b : bufs) dfree(*b);
+    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.slot_plo); dfree(kv.second.slot_phi); }
+    prof_resolve(h);
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return 0;
+}
+
+const char *lpc_last_error(const lpc_handle *h) { return h ? h->err.c_str() : g_open_err.c_str(); }
+
+int lpc_device_info(lpc_handle *h, char *name, int name_len, int *cu_count)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (name && name_len > 0) { strncpy(name, h->name, (size_t)name_len - 1); name[name_len - 1] = 0; }
+    if (cu_count) *cu_count = h->cus;
+    return 0;
+}
+
+int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const float *v1,
+                     const float *v2, const int32_t *mesh_id, int32_t mesh_count,
+                     const int32_t *mat_type, const float *ior, const float *refl,
+                     const float *diss)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (tri_count <= 0 || mesh_count <= 0 || !v0 || !v1 || !v2 || !mesh_id || !mat_type || !ior ||
+        !refl || !diss)
+        return set_err(h, LPC_E_ARG, "scene needs >= 1 triangle, >= 1 mesh and all tables");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const int32_t M = tri_count, K = mesh_count;
+    for (int32_t i = 0; i < M; ++i)
+        if (mesh_id[i] < 0 || mesh_id[i] >= K)
+            return set_err(h, LPC_E_ARG, "mesh_id[" + std::to_string(i) + "] out of range");
+    h->M = M; h->K = K;
+    h->hv0.assign(v0, v0 + 4 * (size_t)M);
+    h->hv1.assign(v1, v1 + 4 * (size_t)M);
+    h->hv2.assign(v2, v2 + 4 * (size_t)M);
+    // runs of equal mesh_id and the slot each one flushes into (.cl:260-265, 286)
+    h->run_lo.clear(); h->run_hi.clear();
+    for (int32_t i = 0; i < M; ++i) {
+        if (i == 0 || mesh_id[i] != mesh_id[i - 1]) { h->run_lo.push_back(i); h->run_hi.push_back(i + 1); }
+        else h->run_hi.back() = i + 1;
+    }
+    const size_t nr = h->run_lo.size();
+    h->slot_run.assign((size_t)K, -1);
+    for (size_t r = 0; r < nr; ++r) {
+        int32_t slot = (r + 1 < nr) ? mesh_id[h->run_lo[r + 1]] - 1 : mesh_id[h->run_lo[r]];
+        if (slot < 0)
+            return set_err(h, LPC_E_ARG, "mesh_id sequence writes below slot 0 (reference would "
+                                         "corrupt another ray's scratch); mesh ids must not decrease to 0");
+        h->slot_run[slot] = (int32_t)r;   // a later run overwrites, as the sequential loop does
+    }
+    h->meas_meshes.clear();
+    for (int32_t j = 0; j < K; ++j) if (mat_type[j] == 3) h->meas_meshes.push_back(j);
+    // exact records and vertices
+    std::vector<ExactRec> xr((size_t)M);
+    std::vector<float> vv((size_t)M * 9);
+    for (int32_t i = 0; i < M; ++i) {
+        const float *a = v0 + 4 * (size_t)i, *b = v1 + 4 * (size_t)i, *c = v2 + 4 * (size_t)i;
+        ExactRec &x = xr[(size_t)i];
+        x.v0x = a[0]; x.v0y = a[1]; x.v0z = a[2];
+        x.e1x = b[0] - a[0]; x.e1y = b[1] - a[1]; x.e1z = b[2] - a[2];
+        x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
+        x.pad0 = x.pad1 = x.pad2 = 0.0f;
+        for (int k = 0; k < 3; ++k) { vv[9 * (size_t)i + k] = a[k]; vv[9 * (size_t)i + 3 + k] = b[k]; vv[9 * (size_t)i + 6 + k] = c[k]; }
+    }
+    h->ptabs.clear();   // piece tables depend on the scene
+    h->dcap = 16.0;
+    RETIF(build_records(h));
+    RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
+    RETIF(dalloc(h, h->d_verts, vv.size() * 4));
+    RETIF(dalloc(h, h->d_mat, (size_t)K * 4));
+    RETIF(dalloc(h, h->d_ior, (size_t)K * 4));
+    RETIF(dalloc(h, h->d_refl, (size_t)K * 4));
+    RETIF(dalloc(h, h->d_diss, (size_t)K * 4));
+    HIPCHK(h, hipMemcpy(h->d_xrec.p, xr.data(), xr.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_verts.p, vv.data(), vv.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_mat.p, mat_type, (size_t)K * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_ior.p, ior, (size_t)K * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_refl.p, refl, (size_t)K * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_diss.p, diss, (size_t)K * 4, hipMemcpyHostToDevice));
+    h->ws_rays = 0; h->ws_part = 0;   // K may have changed
+    h->traced_ready = false;
+    return 0;
+}
+
+static double host_dmax2(int64_t n, const float *dir4)
+{
+    double m = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        const float *d = dir4 + 4 * i;
+        double q = (double)d[0] * d[0] + (double)d[1] * d[1] + (double)d[2] * d[2];
+        if (!(q <= m)) m = q;   // NaN propagates as "large"
+    }
+    return m;
+}
+
+// Upload (n,4) host rows into SoA arrays of a population (rows 0..n).
+static int upload_rays(lpc_handle *h, Pop &P, int64_t n, const float *origin4, const float *dir4,
+                       const float *pow, const int32_t *prev_mid)
+{
+    RETIF(dalloc(h, h->w_stage, (size_t)n * 16));
+    HIPCHK(h, hipMemcpy(h->w_stage.p, origin4, (size_t)n * 16, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, h->stream, n,
+                       (const float4 *)h->w_stage.p, P.f(0), P.f(1), P.f(2));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(h->w_stage.p, dir4, (size_t)n * 16, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, h->stream, n,
+                       (const float4 *)h->w_stage.p, P.f(3), P.f(4), P.f(5));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(P.f(6), pow, (size_t)n * 4, hipMemcpyHostToDevice));
+    if (prev_mid) {
+        HIPCHK(h, hipMemcpy(P.pmid(), prev_mid, (size_t)n * 4, hipMemcpyHostToDevice));
+    } else {
+        std::vector<int32_t> m2((size_t)n, -2);
+        HIPCHK(h, hipMemcpy(P.pmid(), m2.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    return 0;
+}
+
+static int copy_pop(lpc_handle *h, Pop &dst, const Pop &src, int64_t n)
+{
+    for (int k = 0; k < 7; ++k)
+        HIPCHK(h, hipMemcpyAsync(dst.f(k), src.f(k), (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(dst.pmid(), src.pmid(), (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
+    return 0;
+}
+
+int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float *dir4,
+                    float *pow, int32_t *meas, const int32_t *prev_mid, float max_ray_len,
+                    float ior_env, float *dest4, int32_t *isect_mid, float *r_dir4, float *r_pow,
+                    int32_t *r_meas, float *t_dir4, float *t_pow, int32_t *t_meas,
+                    int32_t *n1_mid, int32_t *n2_mid, int32_t *entering, int32_t *isect_idx)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
+    if (n < 0 || !origin4 || !dir4 || !pow || !meas || !prev_mid || !dest4 || !isect_mid ||
+        !r_dir4 || !r_pow || !r_meas || !t_dir4 || !t_pow || !t_meas)
+        return set_err(h, LPC_E_ARG, "bounce_host: missing buffer");
+    if (n == 0) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    RETIF(check_dcap(h, host_dmax2(n, dir4)));
+    const int64_t C = std::min(n, chunk_rays(h));
+    RETIF(ensure_ws(h, C));
+    Pop P;
+    RETIF(pop_reserve(h, P, C));
+    DBuf dmeas;
+    RETIF(dalloc(h, dmeas, (size_t)C * 4));
+    int rc = 0;
+    for (int64_t base = 0; base < n && !rc; base += C) {
+        const int64_t nc = std::min(C, n - base);
+        rc = upload_rays(h, P, nc, origin4 + 4 * base, dir4 + 4 * base, pow + base, prev_mid + base);
+        if (rc) break;
+        if (hipMemcpy(dmeas.p, meas + base, (size_t)nc * 4, hipMemcpyHostToDevice) != hipSuccess) { rc = set_err(h, LPC_E_HIP, "meas upload"); break; }
+        rc = run_intersect(h, P.in(), nc, max_ray_len, nullptr, nullptr, nullptr);
+        if (!rc) rc = run_shade(h, P.in(), (const int32_t *)dmeas.p, nc, max_ray_len, ior_env, true);
+        if (rc) break;
+        ShadeOutPtrs o = shade_ptrs(h, true);
+        hipError_t e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) { rc = set_err(h, LPC_E_HIP, std::string("bounce: ") + hipGetErrorString(e)); break; }
+        auto d2h = [&](void *dst, const void *src, size_t bytes) {
+            if (!rc && dst && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = set_err(h, LPC_E_HIP, "bounce: D2H");
+        };
+        auto pack = [&](float *dst4, const float *x, const float *y, const float *z) {
+            hipLaunchKernelGGL(k_pack4, dim3(grid1(nc)), dim3(256), 0, h->stream, nc, x, y, z,
+                               (float4 *)h->w_stage.p);
+            if (hipStreamSynchronize(h->stream) != hipSuccess) { rc = set_err(h, LPC_E_HIP, "pack"); return; }
+            d2h(dst4 + 4 * base, h->w_stage.p, (size_t)nc * 16);
+        };
+        RETIF(dalloc(h, h->w_stage, (size_t)nc * 16));
+        pack(dest4, o.destx, o.desty, o.destz);
+        pack(r_dir4, o.rdx, o.rdy, o.rdz);
+        pack(t_dir4, o.tdx, o.tdy, o.tdz);
+        d2h(pow + base, o.pw, (size_t)nc * 4);
+        d2h(meas + base, o.meas, (size_t)nc * 4);
+        d2h(isect_mid + base, o.imid, (size_t)nc * 4);
+        d2h(r_pow + base, o.rpw, (size_t)nc * 4);
+        d2h(r_meas + base, o.rms, (size_t)nc * 4);
+        d2h(t_pow + base, o.tpw, (size_t)nc * 4);
+        d2h(t_meas + base, o.tms, (size_t)nc * 4);
+        if (n1_mid) d2h(n1_mid + base, o.n1, (size_t)nc * 4);
+        if (n2_mid) d2h(n2_mid + base, o.n2, (size_t)nc * 4);
+        if (entering) d2h(entering + base, o.ent, (size_t)nc * 4);
+        if (isect_idx) d2h(isect_idx + base, o.iidx, (size_t)nc * 4);
+    }
+    dfree(P.buf);
+    dfree(dmeas);
+    if (h->prof) { (void)hipStreamSynchronize(h->stream); prof_resolve(h); }
+    return rc;
+}
+
+// ---- reference-kernel drop-ins ------------------------------------------------
+int lpc_intersect(lpc_handle *h, int64_t n, const float *dev_origin4, const float *dev_dir4,
+                  float max_ray_len, float *dev_tmin, int32_t *dev_cnt, int32_t *dev_itmp)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
+    if (n < 0 || !dev_origin4 || !dev_dir4 || !dev_tmin || !dev_cnt || !dev_itmp)
+        return set_err(h, LPC_E_ARG, "intersect: missing buffer");
+    if (n == 0) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    const int64_t C = std::min(n, chunk_rays(h));
+    RETIF(ensure_ws(h, C));
+    float *s = (float *)h->w_soa.p;
+    const size_t Cw = (size_t)h->ws_rays;
+    for (int64_t base = 0; base < n; base += C) {
+        const int64_t nc = std::min(C, n - base);
+        hipLaunchKernelGGL(k_unpack4, dim3(grid1(nc)), dim3(256), 0, h->stream, nc,
+                           (const float4 *)dev_origin4 + base, s, s + Cw, s + 2 * Cw);
+        hipLaunchKernelGGL(k_unpack4, dim3(grid1(nc)), dim3(256), 0, h->stream, nc,
+                           (const float4 *)dev_dir4 + base, s + 3 * Cw, s + 4 * Cw, s + 5 * Cw);
+        RaysIn in;
+        in.ox = s; in.oy = s + Cw; in.oz = s + 2 * Cw; in.dx = s + 3 * Cw; in.dy = s + 4 * Cw;
+        in.dz = s + 5 * Cw; in.pw = nullptr; in.pmid = nullptr;
+        RETIF(run_intersect(h, in, nc, max_ray_len, dev_tmin + base * h->K, dev_cnt + base * h->K,
+                            dev_itmp + base * h->K));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->prof) prof_resolve(h);
+    return 0;
+}
+
+int lpc_intersect_postproc(lpc_handle *h, int64_t n, const float *dev_origin4,
+                           const float *dev_dir4, float *dev_dest4, const int32_t *dev_prev_mid,
+                           int32_t *dev_n1_mid, int32_t *dev_n2_mid, int32_t *dev_entering,
+                           int32_t *dev_isect_mid, int32_t *dev_isect_idx,
+                           const float *dev_tmin, const int32_t *dev_cnt,
+                           const int32_t *dev_itmp, float max_ray_len)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
+    if (n < 0 || !dev_origin4 || !dev_dir4 || !dev_dest4 || !dev_prev_mid || !dev_n1_mid ||
+        !dev_n2_mid || !dev_entering || !dev_isect_mid || !dev_isect_idx || !dev_tmin ||
+        !dev_cnt || !dev_itmp)
+        return set_err(h, LPC_E_ARG, "intersect_postproc: missing buffer");
+    if (n == 0) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    PostprocAosArgs A;
+    A.n = n; A.K = h->K;
+    A.origin = (const float4 *)dev_origin4; A.dir = (const float4 *)dev_dir4;
+    A.dest = (float4 *)dev_dest4; A.prev_mid = dev_prev_mid;
+    A.n1 = dev_n1_mid; A.n2 = dev_n2_mid; A.entering = dev_entering;
+    A.imid = dev_isect_mid; A.iidx = dev_isect_idx;
+    A.tmin = dev_tmin; A.cnt = dev_cnt; A.itmp = dev_itmp;
+    A.mat_type = (const int32_t *)h->d_mat.p; A.max_ray_len = max_ray_len;
+    hipLaunchKernelGGL(k_postproc_aos, dim3(grid1(n)), dim3(256), 0, h->stream, A);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lpc_reflect_refract_rays(lpc_handle *h, int64_t n, const float *dev_origin4,
+                             const float *dev_dest4, const float *dev_dir4, float *dev_pow,
+                             int32_t *dev_meas, const int32_t *dev_n1_mid,
+                             const int32_t *dev_n2_mid, float *dev_r_origin4, float *dev_r_dir4,
+                             float *dev_r_pow, int32_t *dev_r_meas, float *dev_t_origin4,
+                             float *dev_t_dir4, float *dev_t_pow, int32_t *dev_t_meas,
+                             const int32_t *dev_isect_mid, const int32_t *dev_isect_idx,
+                             float ior_env)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
+    if (n < 0 || !dev_origin4 || !dev_dest4 || !dev_dir4 || !dev_pow || !dev_meas ||
+        !dev_n1_mid || !dev_n2_mid || !dev_r_origin4 || !dev_r_dir4 || !dev_r_pow ||
+        !dev_r_meas || !dev_t_origin4 || !dev_t_dir4 || !dev_t_pow || !dev_t_meas ||
+        !dev_isect_mid || !dev_isect_idx)
+        return set_err(h, LPC_E_ARG, "reflect_refract_rays: missing buffer");
+    if (n == 0) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    FresnelAosArgs A;
+    A.n = n;
+    A.origin = (const float4 *)dev_origin4; A.dest = (const float4 *)dev_dest4;
+    A.dir = (const float4 *)dev_dir4; A.pow = dev_pow; A.meas = dev_meas;
+    A.n1 = dev_n1_mid; A.n2 = dev_n2_mid; A.imid = dev_isect_mid; A.iidx = dev_isect_idx;
+    A.r_origin = (float4 *)dev_r_origin4; A.r_dir = (float4 *)dev_r_dir4;
+    A.t_origin = (float4 *)dev_t_origin4; A.t_dir = (float4 *)dev_t_dir4;
+    A.r_pow = dev_r_pow; A.t_pow = dev_t_pow; A.r_meas = dev_r_meas; A.t_meas = dev_t_meas;
+    A.mat_type = (const int32_t *)h->d_mat.p; A.ior = (const float *)h->d_ior.p;
+    A.refl = (const float *)h->d_refl.p; A.diss = (const float *)h->d_diss.p;
+    A.verts = (const float *)h->d_verts.p; A.ior_env = ior_env;
+    hipLaunchKernelGGL(k_fresnel_aos, dim3(grid1(n)), dim3(256), 0, h->stream, A);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+// ---- device-resident trace ------------------------------------------------------
+int lpc_set_chunk(lpc_handle *h, int64_t rays_per_chunk)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (rays_per_chunk < 0) return set_err(h, LPC_E_ARG, "negative chunk");
+    h->chunk = rays_per_chunk;
+    return 0;
+}
+
+static int reset_measured(lpc_handle *h)
+{
+    h->m_total = 0;
+    DevAcc z;
+    memset(&z, 0, sizeof(z));
+    HIPCHK(h, hipMemcpy(h->d_acc.p, &z, sizeof(z), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const float *dir4,
+                       const float *pow, float max_ray_len, float ior_env)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
+    if (n < 0 || (n > 0 && (!origin4 || !dir4 || !pow))) return set_err(h, LPC_E_ARG, "set_rays: missing buffer");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    RETIF(check_dcap(h, host_dmax2(n, dir4)));
+    RETIF(pop_reserve(h, h->I, std::max<int64_t>(n, 1)));
+    if (n > 0) RETIF(upload_rays(h, h->I, n, origin4, dir4, pow, nullptr));
+    h->n_init = n;
+    h->max_ray_len = max_ray_len;
+    h->ior_env = ior_env;
+    h->traced_ready = true;
+    return lpc_trace_reset(h);
+}
+
+int lpc_trace_reset(lpc_handle *h)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_reset before trace_set_rays");
+    HIPCHK(h, hipSetDevice(h->device));
+    RETIF(pop_reserve(h, h->A, std::max<int64_t>(h->n_init, 1)));
+    if (h->n_init > 0) RETIF(copy_pop(h, h->A, h->I, h->n_init));
+    h->n_cur = h->n_init;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return reset_measured(h);
+}
+
+int lpc_trace_population(lpc_handle *h, int64_t *n)
+{
+    if (!h || !n) return set_err(h, LPC_E_ARG, "null argument");
+    *n = h->n_cur;
+    return 0;
+}
+
+static int ensure_measured(lpc_handle *h, int64_t need)
+{
+    if (need <= h->m_cap) return 0;
+    int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * h->m_cap, 1 << 16));
+    DBuf nb;
+    RETIF(dalloc(h, nb, (size_t)cap * 5 * 4));
+    if (h->m_total > 0) {
+        for (int k = 0; k < 5; ++k)
+            HIPCHK(h, hipMemcpyAsync((char *)nb.p + (size_t)k * cap * 4,
+                                     (char *)h->m_buf.p + (size_t)k * h->m_cap * 4,
+                                     (size_t)h->m_total * 4, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    dfree(h->m_buf);
+    h->m_buf = nb;
+    h->m_cap = cap;
+    return 0;
+}
+
+int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
+                      int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_iterate before trace_set_rays");
+    HIPCHK(h, hipSetDevice(h->device));
+    lpc_iter_stats S;
+    memset(&S, 0, sizeof(S));
+    const int64_t N = h->n_cur;
+    S.n_in = N;
+    if (N == 0) { if (st) *st = S; return 0; }
+    const int64_t C = std::min(N, chunk_rays(h));
+    RETIF(ensure_ws(h, C));
+    RETIF(pop_reserve(h, h->B, 2 * N));
+    RETIF(pop_reserve(h, h->T, N));
+    RETIF(ensure_measured(h, h->m_total + N));
+    DevAcc acc;
+    memset(&acc, 0, sizeof(acc));
+    acc.m_total = (unsigned long long)h->m_total;
+    HIPCHK(h, hipMemcpy(h->d_acc.p, &acc, sizeof(acc), hipMemcpyHostToDevice));
+    const size_t mc = (size_t)h->m_cap;
+    float *mf = (float *)h->m_buf.p;
+    for (int64_t base = 0; base < N; base += C) {
+        const int64_t nc = std::min(C, N - base);
+        const RaysIn in = h->A.in(base);
+        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+        RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
+        ShadeOutPtrs o = shade_ptrs(h, false);
+        if (out_origin4 || out_dest4 || out_pow || out_meas) {
+            auto pack = [&](float *dst4, const float *x, const float *y, const float *z) -> int {
+                hipLaunchKernelGGL(k_pack4, dim3(grid1(nc)), dim3(256), 0, h->stream, nc, x, y, z,
+                                   (float4 *)h->w_stage.p);
+                HIPCHK(h, hipStreamSynchronize(h->stream));
+                HIPCHK(h, hipMemcpy(dst4 + 4 * base, h->w_stage.p, (size_t)nc * 16, hipMemcpyDeviceToHost));
+                return 0;
+            };
+            if (out_origin4) RETIF(pack(out_origin4, in.ox, in.oy, in.oz));
+            if (out_dest4) RETIF(pack(out_dest4, o.destx, o.desty, o.destz));
+            if (out_pow) HIPCHK(h, hipMemcpy(out_pow + base, o.pw, (size_t)nc * 4, hipMemcpyDeviceToHost));
+            if (out_meas) HIPCHK(h, hipMemcpy(out_meas + base, o.meas, (size_t)nc * 4, hipMemcpyDeviceToHost));
+        }
+        CompactArgs A;
+        A.n = nc; A.nb = (nc + 1023) / 1024; A.o = o;
+        A.blk_cnt = (int32_t *)h->w_blk_cnt.p; A.blk_off = (long long *)h->w_blk_off.p;
+        A.blk_pow = (double *)h->w_blk_pow.p; A.acc = (DevAcc *)h->d_acc.p;
+        A.nR = h->B.out(); A.nT = h->T.out();
+        A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
+        A.mm = (int32_t *)(mf + 4 * mc);
+        hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, h->stream, A);
+        hipLaunchKernelGGL(k_scatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
+        HIPCHK(h, hipGetLastError());
+        if (h->prof) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(&acc, h->d_acc.p, sizeof(acc), hipMemcpyDeviceToHost));
+    const int64_t nR = (int64_t)acc.nR, nT = (int64_t)acc.nT;
+    if (nT > 0) {
+        hipLaunchKernelGGL(k_append, dim3((unsigned)std::min<int64_t>(grid1(nT), 8192)), dim3(256), 0,
+                           h->stream, h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
+        HIPCHK(h, hipGetLastError());
+    }
+    if (out_next_pow && nR + nT > 0) {
+        HIPCHK(h, hipMemcpyAsync(out_next_pow, h->B.f(6), (size_t)(nR + nT) * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->prof) prof_resolve(h);
+    std::swap(h->A, h->B);
+    h->n_cur = nR + nT;
+    h->m_total = (int64_t)acc.m_total;
+    S.n_reflect = nR; S.n_refract = nT; S.n_measured = (int64_t)acc.nM_iter;
+    S.power_next = acc.pow_next;
+    float dm2;
+    memcpy(&dm2, &acc.dmax2_bits, 4);
+    RETIF(check_dcap(h, (double)dm2));
+    if (st) *st = S;
+    return 0;
+}
+
+static int mesh_power(lpc_handle *h, double *out)
+{
+    for (int32_t j = 0; j < h->K; ++j) out[j] = 0.0;
+    if (h->m_total == 0) return 0;
+    const int64_t nb = (h->m_total + 65535) / 65536;
+    RETIF(dalloc(h, h->d_tmp, (size_t)nb * 8));
+    std::vector<double> part((size_t)nb);
+    const size_t mc = (size_t)h->m_cap;
+    const float *mf = (const float *)h->m_buf.p;
+    for (int32_t j : h->meas_meshes) {
+        hipLaunchKernelGGL(k_mesh_sum, dim3((unsigned)nb), dim3(256), 0, h->stream, h->m_total,
+                           mf + 3 * mc, (const int32_t *)(mf + 4 * mc), j, (double *)h->d_tmp.p);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(part.data(), h->d_tmp.p, (size_t)nb * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        double s = 0.0;
+        for (double v : part) s += v;
+        out[j] = s;
+    }
+    return 0;
+}
+
+int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_pow)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (count) *count = h->m_total;
+    if (mesh_pow) RETIF(mesh_power(h, mesh_pow));
+    return 0;
+}
+
+int lpc_trace_fetch_measured(lpc_handle *h, float *pos4, float *pow, int32_t *mesh)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int64_t n = h->m_total;
+    if (n == 0) return 0;
+    const size_t mc = (size_t)h->m_cap;
+    const float *mf = (const float *)h->m_buf.p;
+    if (pos4) {
+        RETIF(dalloc(h, h->w_stage, (size_t)n * 16));
+        hipLaunchKernelGGL(k_pack4, dim3(grid1(n)), dim3(256), 0, h->stream, n, mf, mf + mc,
+                           mf + 2 * mc, (float4 *)h->w_stage.p);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, hipMemcpy(pos4, h->w_stage.p, (size_t)n * 16, hipMemcpyDeviceToHost));
+    }
+    if (pow) HIPCHK(h, hipMemcpy(pow, mf + 3 * mc, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (mesh) HIPCHK(h, hipMemcpy(mesh, mf + 4 * mc, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lpc_project_hist(lpc_handle *h, int mode, int64_t n, const float *pos4, const float *pwr,
+                     const float *rot4, const float *pivot4, const double *xedges, int nx,
+                     const double *yedges, int ny, double weight_div, double *H, float *x,
+                     float *y, float *pwr_cor)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if ((mode != 0 && mode != 1) || nx <= 0 || ny <= 0 || !rot4 || !pivot4 || !xedges || !yedges || !H)
+        return set_err(h, LPC_E_ARG, "project_hist: bad argument");
+    if (pos4 && !pwr) return set_err(h, LPC_E_ARG, "project_hist: pwr is NULL");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!pos4) n = h->m_total;
+    if (n < 0) return set_err(h, LPC_E_ARG, "project_hist: negative n");
+    // device scratch: [rot 16 f | piv 4 f | xe | ye | H | (pos4, pwr) | (x, y, pc)]
+    const size_t o_rot = 0, o_xe = 128, o_ye = o_xe + (size_t)(nx + 1) * 8;
+    const size_t o_H = (o_ye + (size_t)(ny + 1) * 8 + 255) / 256 * 256;
+    const size_t o_in = (o_H + (size_t)nx * ny * 8 + 255) / 256 * 256;
+    const size_t in_bytes = pos4 ? (size_t)n * 20 : 0;
+    const size_t o_out = (o_in + in_bytes + 255) / 256 * 256;
+    const size_t out_bytes = x ? (size_t)n * 12 : 0;
+    RETIF(dalloc(h, h->d_tmp, o_out + out_bytes + 16));
+    char *d = (char *)h->d_tmp.p;
+    float rp[20];
+    memcpy(rp, rot4, 16 * 4);
+    memcpy(rp + 16, pivot4, 4 * 4);
+    HIPCHK(h, hipMemcpy(d + o_rot, rp, sizeof(rp), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(d + o_xe, xedges, (size_t)(nx + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(d + o_ye, yedges, (size_t)(ny + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemsetAsync(d + o_H, 0, (size_t)nx * ny * 8, h->stream));
+    ProjArgs A;
+    memset(&A, 0, sizeof(A));
+    A.n = n; A.mode = mode;
+    if (pos4) {
+        HIPCHK(h, hipMemcpy(d + o_in, pos4, (size_t)n * 16, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(d + o_in + (size_t)n * 16, pwr, (size_t)n * 4, hipMemcpyHostToDevice));
+        A.pos4 = (const float4 *)(d + o_in);
+        A.pwr = (const float *)(d + o_in + (size_t)n * 16);
+    } else {
+        const size_t mc = (size_t)h->m_cap;
+        const float *mf = (const float *)h->m_buf.p;
+        A.px = mf; A.py = mf + mc; A.pz = mf + 2 * mc; A.pwr = mf + 3 * mc;
+    }
+    A.rot = (const float *)(d + o_rot);
+    A.piv = (const float *)(d + o_rot) + 16;
+    if (x) { A.x = (float *)(d + o_out); A.y = A.x + n; A.pc = A.y + n; }
+    A.xe = (const double *)(d + o_xe); A.ye = (const double *)(d + o_ye);
+    A.nx = nx; A.ny = ny; A.div = weight_div; A.H = (double *)(d + o_H);
+    if (n > 0) {
+        hipLaunchKernelGGL(k_project_hist, dim3(grid1(n)), dim3(256), 0, h->stream, A);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(H, d + o_H, (size_t)nx * ny * 8, hipMemcpyDeviceToHost));
+    if (x && n > 0) {
+        HIPCHK(h, hipMemcpy(x, A.x, (size_t)n * 4, hipMemcpyDeviceToHost));
+        if (y) HIPCHK(h, hipMemcpy(y, A.y, (size_t)n * 4, hipMemcpyDeviceToHost));
+        if (pwr_cor) HIPCHK(h, hipMemcpy(pwr_cor, A.pc, (size_t)n * 4, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int lpc_prof_enable(lpc_handle *h, int on)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    h->prof = on != 0;
+    return 0;
+}
+
+int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
+{
+    if (!h || !out) return set_err(h, LPC_E_ARG, "null argument");
+    (void)hipStreamSynchronize(h->stream);
+    prof_resolve(h);
+    out->intersect_ms = h->prof_isect_ms;
+    out->shade_ms = h->prof_rest_ms;
+    out->intersect_launches = h->prof_launches;
+    out->pairs = h->prof_pairs;
+    if (reset) { h->prof_isect_ms = h->prof_rest_ms = 0.0; h->prof_launches = h->prof_pairs = 0; }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,224 @@
+"""Python front of liblpc: one :class:`Engine` per GPU.
+
+Flattens LightPyCL meshes exactly as ``CL_Tracer.iterative_tracer`` does
+(``/root/reference/iterative_tracer.py:121-158``), uploads them, and exposes the
+per-bounce entry points of ``include/lpc.h`` with numpy arrays.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, f32, i32, ptr
+
+
+def flatten_meshes(meshes):
+    """(v0, v1, v2, mesh_id, mat_type, ior, refl, diss) as iterative_tracer.py:121-151 builds
+    them: per-mesh material records and the concatenated tribuf() vertex rows."""
+    K = len(meshes)
+    if K == 0:
+        raise ValueError("iterative_tracer needs at least one mesh")
+    mat_type = np.zeros(K, np.int32)
+    ior = np.zeros(K, np.float32)
+    refl = np.zeros(K, np.float32)
+    diss = np.zeros(K, np.float32)
+    v0s, v1s, v2s, ids = [], [], [], []
+    for j, mesh in enumerate(meshes):
+        mat = mesh.getMaterialBuf()
+        mat_type[j] = np.int32(mat.get("type"))
+        ior[j] = np.float32(mat.get("IOR"))
+        refl[j] = np.float32(mat.get("R"))
+        diss[j] = np.float32(mat.get("dissipation"))
+        tb = mesh.tribuf()
+        v0s.append(np.array(tb[0], dtype=np.float32).reshape(-1, 4))
+        v1s.append(np.array(tb[1], dtype=np.float32).reshape(-1, 4))
+        v2s.append(np.array(tb[2], dtype=np.float32).reshape(-1, 4))
+        ids.append(np.zeros(len(tb[0]), np.int32) + j)
+    v0 = np.ascontiguousarray(np.concatenate(v0s), dtype=np.float32)
+    v1 = np.ascontiguousarray(np.concatenate(v1s), dtype=np.float32)
+    v2 = np.ascontiguousarray(np.concatenate(v2s), dtype=np.float32)
+    mesh_id = np.ascontiguousarray(np.concatenate(ids), dtype=np.int32)
+    return v0, v1, v2, mesh_id, mat_type, ior, refl, diss
+
+
+def default_device() -> int:
+    for key in ("LPC_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(key, "") != "":
+            return int(os.environ[key])
+    return 0
+
+
+class Engine:
+    """A liblpc handle on one GPU (HIP device ordinal ``device``)."""
+
+    def __init__(self, device=None):
+        self.L = _lib.load()
+        self.device = default_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        check(self.L.lpc_open(self.device, ctypes.byref(h)), None)
+        self.h = h
+        self.tri_count = 0
+        self.mesh_count = 0
+
+    # -- lifecycle -----------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.lpc_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc):
+        check(rc, self.h)
+
+    def info(self):
+        buf = ctypes.create_string_buffer(256)
+        cu = ctypes.c_int(0)
+        self._c(self.L.lpc_device_info(self.h, buf, 256, ctypes.byref(cu)))
+        return buf.value.decode(), cu.value
+
+    # -- scene ---------------------------------------------------------------
+    def upload_arrays(self, v0, v1, v2, mesh_id, mat_type, ior, refl, diss):
+        v0, v1, v2 = f32(v0, (-1, 4)), f32(v1, (-1, 4)), f32(v2, (-1, 4))
+        mesh_id, mat_type = i32(mesh_id), i32(mat_type)
+        ior, refl, diss = f32(ior), f32(refl), f32(diss)
+        M, K = v0.shape[0], mat_type.shape[0]
+        self._c(self.L.lpc_scene_upload(self.h, M, ptr(v0), ptr(v1), ptr(v2), ptr(mesh_id), K,
+                                        ptr(mat_type), ptr(ior), ptr(refl), ptr(diss)))
+        self.tri_count, self.mesh_count = M, K
+        self.mat_type = mat_type
+
+    def upload_meshes(self, meshes):
+        arrs = flatten_meshes(meshes)
+        self.upload_arrays(*arrs)
+        return arrs
+
+    # -- one bounce on host arrays (partition-loop body) ------------------------
+    def bounce(self, origin4, dir4, pow_, meas, prev_mid, max_ray_len=1e3, ior_env=1.0):
+        o, d = f32(origin4, (-1, 4)), f32(dir4, (-1, 4))
+        n = o.shape[0]
+        pw = f32(pow_).reshape(-1).copy()
+        ms = i32(meas).reshape(-1).copy()
+        pm = i32(prev_mid).reshape(-1)
+        out = {k: np.zeros((n, 4), np.float32) for k in ("dest", "r_dir", "t_dir")}
+        for k in ("r_pow", "t_pow"):
+            out[k] = np.zeros(n, np.float32)
+        for k in ("isect_mid", "r_meas", "t_meas", "n1", "n2", "entering", "isect_idx"):
+            out[k] = np.zeros(n, np.int32)
+        self._c(self.L.lpc_bounce_host(
+            self.h, n, ptr(o), ptr(d), ptr(pw), ptr(ms), ptr(pm), np.float32(max_ray_len),
+            np.float32(ior_env), ptr(out["dest"]), ptr(out["isect_mid"]), ptr(out["r_dir"]),
+            ptr(out["r_pow"]), ptr(out["r_meas"]), ptr(out["t_dir"]), ptr(out["t_pow"]),
+            ptr(out["t_meas"]), ptr(out["n1"]), ptr(out["n2"]), ptr(out["entering"]),
+            ptr(out["isect_idx"])))
+        out["pow"] = pw
+        out["meas"] = ms
+        return out
+
+    # -- device-resident trace -----------------------------------------------
+    def set_chunk(self, rays):
+        self._c(self.L.lpc_set_chunk(self.h, int(rays)))
+
+    def set_rays(self, origin4, dir4, pow_, max_ray_len=1e3, ior_env=1.0):
+        o, d = f32(origin4, (-1, 4)), f32(dir4, (-1, 4))
+        pw = f32(pow_).reshape(-1)
+        n = o.shape[0]
+        if d.shape[0] != n or pw.shape[0] != n:
+            raise ValueError("origin, direction and power must have the same ray count")
+        self._c(self.L.lpc_trace_set_rays(self.h, n, ptr(o), ptr(d), ptr(pw),
+                                          np.float32(max_ray_len), np.float32(ior_env)))
+        return n
+
+    def reset(self):
+        self._c(self.L.lpc_trace_reset(self.h))
+
+    def population(self):
+        n = ctypes.c_int64(0)
+        self._c(self.L.lpc_trace_population(self.h, ctypes.byref(n)))
+        return n.value
+
+    def iterate(self, export=False):
+        """One iteration over the device population.  With ``export`` returns the
+        reference's results tuple arrays and the next population's powers."""
+        st = _lib.IterStats()
+        if not export:
+            self._c(self.L.lpc_trace_iterate(self.h, None, None, None, None, None, ctypes.byref(st)))
+            return st, None
+        n = self.population()
+        org = np.empty((n, 4), np.float32)
+        dst = np.empty((n, 4), np.float32)
+        pw = np.empty(n, np.float32)
+        ms = np.empty(n, np.int32)
+        nxt = np.empty(max(2 * n, 1), np.float32)
+        self._c(self.L.lpc_trace_iterate(self.h, ptr(org), ptr(dst), ptr(pw), ptr(ms), ptr(nxt),
+                                         ctypes.byref(st)))
+        return st, dict(origin=org, dest=dst, pow=pw, meas=ms,
+                        next_pow=nxt[: st.n_reflect + st.n_refract])
+
+    def measured(self):
+        """(count, per-mesh measured power float64[K])."""
+        c = ctypes.c_int64(0)
+        mp = np.zeros(max(self.mesh_count, 1), np.float64)
+        self._c(self.L.lpc_trace_measured(self.h, ctypes.byref(c), ptr(mp)))
+        return c.value, mp[: self.mesh_count]
+
+    def fetch_measured(self):
+        """Measured record: pos (Nm,4) float32, pwr (Nm,) float32, mesh (Nm,) int32."""
+        c = ctypes.c_int64(0)
+        self._c(self.L.lpc_trace_measured(self.h, ctypes.byref(c), None))
+        n = c.value
+        pos = np.zeros((n, 4), np.float32)
+        pw = np.zeros(n, np.float32)
+        mm = np.zeros(n, np.int32)
+        if n:
+            self._c(self.L.lpc_trace_fetch_measured(self.h, ptr(pos), ptr(pw), ptr(mm)))
+        return pos, pw, mm
+
+    # -- projection + histogram ---------------------------------------------
+    def project_hist(self, pos4, pwr, limits, points, mode=0, rot=None, pivot=None,
+                     want_xy=False):
+        """angular (mode 0) / stereographic (1) projection + np.histogram2d binning of
+        pwr_cor / (dx*dy).  pos4=None bins the device-resident measured record."""
+        _, xe, ye = np.histogram2d(np.zeros(0), np.zeros(0), bins=points, range=limits)
+        xe = np.ascontiguousarray(xe, np.float64)
+        ye = np.ascontiguousarray(ye, np.float64)
+        nx, ny = xe.size - 1, ye.size - 1
+        dx = np.float64(limits[0][1] - limits[0][0]) / np.float64(points)
+        dy = np.float64(limits[1][1] - limits[1][0]) / np.float64(points)
+        # rotation rows as the reference's R_dev (iterative_tracer.py:545); only rows 0-2
+        # (xyz) are read by the kernel
+        rot = f32(np.eye(4, dtype=np.float32) if rot is None else rot, (4, 4))
+        piv = f32(np.zeros(4, np.float32) if pivot is None else pivot).reshape(4)
+        H = np.zeros((nx, ny), np.float64)
+        if pos4 is None:
+            n = 0
+            p4 = pw = None
+        else:
+            p4 = f32(pos4, (-1, 4))
+            pw = f32(pwr).reshape(-1)
+            n = p4.shape[0]
+        x = y = pc = None
+        if want_xy:
+            cnt = n if pos4 is not None else self.measured()[0]
+            x, y, pc = (np.zeros(cnt, np.float32) for _ in range(3))
+        self._c(self.L.lpc_project_hist(self.h, int(mode), n, ptr(p4), ptr(pw), ptr(rot), ptr(piv),
+                                        ptr(xe), nx, ptr(ye), ny, float(dx * dy), ptr(H), ptr(x),
+                                        ptr(y), ptr(pc)))
+        return (H, xe, ye) if not want_xy else (H, xe, ye, x, y, pc)
+
+    # -- profiling -------------------------------------------------------------
+    def prof_enable(self, on=True):
+        self._c(self.L.lpc_prof_enable(self.h, 1 if on else 0))
+
+    def prof_read(self, reset=True):
+        p = _lib.Prof()
+        self._c(self.L.lpc_prof_read(self.h, ctypes.byref(p), 1 if reset else 0))
+        return dict(intersect_ms=p.intersect_ms, shade_ms=p.shade_ms,
+                    intersect_launches=p.intersect_launches, pairs=p.pairs)

@@ -1,0 +1,297 @@
+"""``CL_Tracer`` -- drop-in for LightPyCL's ``iterative_tracer`` module, running the
+per-bounce hot path on an MI355X through liblpc (HIP, gfx950).
+
+Mirrors ``/root/reference/iterative_tracer.py``:
+  * ``CL_Tracer(platform_name, device_name, debug)`` (:36-74): the platform /
+    device strings are accepted for compatibility; the GPU is the HIP device
+    ``device=`` (default: ``$LPC_DEVICE``, ``$LOCAL_RANK`` or 0);
+  * ``iterative_tracer(light_source, meshes, trace_iterations, trace_until_dissipated,
+    max_ray_len, ior_env)`` (:77-393) -> ``self.results``, a list of per-iteration
+    tuples ``(rays_origin (N,4) f32, rays_dest (N,4) f32, rays_pow, rays_meas (N,) i32)``
+    in the reference's ray order and shapes;
+  * ``get_measured_rays`` (:395-411), the binning / beam-width analyses (:413-709),
+    ``pickle_results`` / ``load_pickle_results`` (:711-751), ``save_traced_scene``.
+
+Extra keyword ``keep_results=False`` selects the aggregate mode: no per-ray results
+cross PCIe; measured rays and per-mesh measured power stay on the device
+(``get_measured_rays`` / ``measured_power`` / the binning calls read them there).
+"""
+from __future__ import annotations
+
+import pickle
+import time
+
+import numpy as np
+
+from .engine import Engine, flatten_meshes
+
+
+def f32_sorted_sum(a):
+    """``sum(np.sort(a))`` as the reference evaluates it (:115, :372): np.sort along the
+    last axis, then a sequential float32 accumulation."""
+    flat = np.sort(np.asarray(a), axis=-1).reshape(-1).astype(np.float32)
+    if flat.size == 0:
+        return np.float32(0.0)
+    return np.add.accumulate(flat, dtype=np.float32)[-1]
+
+
+def _rot(axis):
+    if axis in ("y", "Y"):
+        return lambda x: np.matrix([[np.cos(x), 0, np.sin(x), 0], [0, 1, 0, 0], [-np.sin(x), 0, np.cos(x), 0],
+                                    [0, 0, 0, 0]])
+    if axis in ("z", "Z"):
+        return lambda x: np.matrix([[np.cos(x), -np.sin(x), 0, 0], [np.sin(x), np.cos(x), 0, 0], [0, 0, 1, 0],
+                                    [0, 0, 0, 0]])
+    return lambda x: np.matrix([[1, 0, 0, 0], [0, np.cos(x), -np.sin(x), 0], [0, np.sin(x), np.cos(x), 0],
+                                [0, 0, 0, 0]])
+
+
+class CL_Tracer:
+    """Iterative optical ray tracer (reference class ``CL_Tracer``)."""
+
+    results = None
+    geometry = None
+
+    def __init__(self, platform_name="NVIDIA", device_name="770", debug=False, device=None,
+                 verbose=False):
+        self.debug = debug
+        self.verbose = verbose
+        self.platform_name, self.device_name = platform_name, device_name
+        self.engine = Engine(device)
+        name, cus = self.engine.info()
+        self.device_label = f"{name} ({cus} CUs)"
+        if self.verbose:
+            print("Using HIP device:", self.device_label)
+        self.meshes = None
+        self.tri_count = 0
+        self.iteration_counts = []
+        self.power_left = []
+        self._aggregate = False
+        self.hist_data = None
+
+    # ------------------------------------------------------------------------
+    def iterative_tracer(self, light_source, meshes, trace_iterations=100, trace_until_dissipated=0.99,
+                         max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True):
+        """Trace until ``trace_iterations`` bounces, until less than
+        (1 - trace_until_dissipated) of the input power is left, or until no ray is
+        left (iterative_tracer.py:241-391).  Returns ``self.results``."""
+        max_ray_len = np.float32(max_ray_len)
+        ior_env = np.float32(ior_env)
+        origin = dirs = power = None
+        for k, light in enumerate(light_source):                       # :99-113
+            if k == 0:
+                origin = np.float32(light.rays_origin)
+                dirs = np.float32(light.rays_dir)
+                power = np.float32(light.rays_power)
+            else:
+                origin = np.append(origin, light.rays_origin, axis=0).astype(np.float32)
+                dirs = np.append(dirs, light.rays_dir, axis=0).astype(np.float32)
+                power = np.append(power, light.rays_power, axis=0).astype(np.float32)
+        origin = np.asarray(origin, dtype=np.float32)
+        dirs = np.asarray(dirs, dtype=np.float32)
+        power = np.asarray(power, dtype=np.float32)
+        input_power = f32_sorted_sum(power)                            # :115
+        pow_shape0 = power.shape
+
+        arrs = flatten_meshes(meshes)                                  # :121-151
+        self.engine.upload_arrays(*arrs)
+        self.tri_count = np.int32(arrs[0].shape[0])
+        self.meshes = meshes
+        self.geometry = (arrs[0], arrs[1], arrs[2])
+        n = self.engine.set_rays(origin, dirs, power.reshape(-1), max_ray_len, ior_env)
+
+        self.results = []
+        self.iteration_counts = []
+        self.power_left = []
+        self._aggregate = not keep_results
+        thr = (1.0 - trace_until_dissipated) * input_power              # :383
+        t0 = time.time()
+        for t_iter in range(int(trace_iterations)):                     # :241
+            self.iteration_counts.append(n)
+            st, ex = self.engine.iterate(export=keep_results)
+            if keep_results:
+                org = origin if t_iter == 0 else ex["origin"]
+                pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
+                self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355
+                power_in_scene = f32_sorted_sum(ex["next_pow"])         # :372
+            else:
+                power_in_scene = st.power_next
+            n = st.n_reflect + st.n_refract
+            self.power_left.append(float(power_in_scene) / float(input_power) if input_power else 0.0)
+            if self.verbose:
+                print(f"iteration {t_iter + 1}: {st.n_in} rays, {n} children kept, "
+                      f"{100.0 * self.power_left[-1]:.4f} % power left")
+            if power_in_scene < thr:
+                break
+            if n == 0:
+                break
+        self.sim_time = time.time() - t0
+        return self.results
+
+    # ------------------------------------------------------------------------
+    def ray_bounces(self):
+        """Rays processed over all iterations (the examples' proc_ray_count)."""
+        return int(sum(self.iteration_counts))
+
+    def measured_power(self):
+        """Per-mesh measured power (float64[K]) accumulated on the device."""
+        return self.engine.measured()[1]
+
+    def get_measured_rays(self):
+        """End points and powers of every ray that hit a measure surface (:395-411)."""
+        if self._aggregate:
+            pos, pw, _ = self.engine.fetch_measured()
+            return pos, pw
+        pos = pwr = None
+        for k, (_o, dest, pw, ms) in enumerate(self.results):
+            idx = np.where(ms >= .9)[0]
+            if k == 0:
+                pos, pwr = dest[idx], pw[idx]
+            else:
+                pos = np.concatenate((pos, dest[idx]), axis=0)
+                pwr = np.concatenate((pwr.flatten(), pw[idx].flatten()), axis=0)
+        return pos, pwr
+
+    def get_binned_data(self, limits=((-10, 10), (-10, 10)), points=500):
+        (pos, pwr) = self.get_measured_rays()
+        self.hist_data = np.histogram2d(x=pos[:, 0], y=pos[:, 1], bins=points, range=limits, weights=pwr)
+        return self.hist_data
+
+    def _project(self, mode, limits, points, rot=None):
+        if self._aggregate:
+            H, xe, ye = self.engine.project_hist(None, None, limits, points, mode=mode, rot=rot)
+        else:
+            pos, pwr = self.get_measured_rays()
+            H, xe, ye = self.engine.project_hist(pos, np.asarray(pwr).reshape(-1), limits, points,
+                                                 mode=mode, rot=rot)
+        return H, xe, ye
+
+    def get_binned_data_angular(self, limits=((-1, 1), (-1, 1)), points=500):
+        """angular_project on the GPU + histogram2d binning on the GPU (:534-562)."""
+        self.hist_data = self._project(0, limits, points)
+        return self.hist_data
+
+    def get_binned_data_stereographic(self, limits=((-1, 1), (-1, 1)), points=500):
+        """stereograph_project on the GPU + binning (:503-531)."""
+        self.hist_data = self._project(1, limits, points)
+        return self.hist_data
+
+    def replicate_lightsources_and_plot(self, limits=((-10, 10), (-10, 10)), points=500, axis="z", sources=36,
+                                        use_3D=True, plot=True):
+        """Emulate ``sources`` rotated copies of the source by rotating the measured rays
+        (:564-657); the histogram is accumulated on the GPU per rotation."""
+        R = _rot(axis)
+        H = None
+        for k in np.arange(sources):
+            ang = k * 2.0 * np.pi / sources
+            h, xe, ye = self._project(0, limits, points, rot=np.asarray(R(ang), dtype=np.float32))
+            H = h if H is None else H + h
+        self.hist_data = (H, xe, ye)
+        if plot:
+            self._plot(H, xe * 180.0 / np.pi, ye * 180.0 / np.pi, use_3D, "replicated_sources")
+        return self.hist_data
+
+    def plot_binned_data(self, limits=((-10, 10), (-10, 10)), points=500, use_3d=True, use_angular=False,
+                         hist_data=None):
+        if hist_data is None:
+            if use_angular:
+                self.get_binned_data_angular(limits=limits, points=points)
+            else:
+                (pos, pwr) = self.get_measured_rays()
+                H, xc, yc = np.histogram2d(x=np.array(pos[:, 0].flatten()), y=np.array(pos[:, 1].flatten()),
+                                           bins=points, range=limits, weights=np.array(np.float64(pwr).flatten()))
+                self.hist_data = (H.astype(np.float64), xc, yc)
+        else:
+            self.hist_data = hist_data
+        H, xe, ye = self.hist_data
+        self._plot(H, xe, ye, use_3d, "binned")
+
+    @staticmethod
+    def _plot(H, xe, ye, use_3d, tag):
+        import matplotlib.pyplot as plt  # optional dependency
+        fig = plt.figure()
+        if use_3d:
+            ax = fig.add_subplot(projection="3d")
+            X, Y = np.meshgrid(xe[0:-1], ye[0:-1])
+            ax.plot_surface(X, Y, H, rstride=1, cstride=1, linewidth=0, antialiased=False)
+        else:
+            plt.imshow(np.log10(H), extent=[xe[0], xe[-1], ye[0], ye[-1]], interpolation="nearest", origin="lower")
+            plt.colorbar()
+        plt.savefig(f"./{tag}_{'3D' if use_3d else '2D'}_data.pdf")
+
+    def plot_elevation_histogram(self, points=500, pole=[0, 0, 1, 0]):
+        (pos, pwr) = self.get_measured_rays()
+        pos0 = np.array(np.divide(pos, np.matrix(np.linalg.norm(pos, axis=1)).T))
+        pwr = np.float64(pwr).flatten()
+        elevation = np.arccos(np.dot(pos0, pole)).flatten()
+        (H, x) = np.histogram(elevation, bins=points, weights=pwr)
+        x = (x[0:-1] + x[1:]) / 2.0
+        dx = x[1] - x[0]
+        H = H / (np.sin(x) * dx)
+        import matplotlib.pyplot as plt  # optional dependency
+        plt.plot(x * 180.0 / np.pi, H)
+        plt.savefig("./elevation_power_distribution.pdf")
+        return H, x
+
+    def get_beam_width_half_power(self, points=500, pole=[0, 0, 1, 0]):
+        """Elevation at which the cumulative measured power reaches half (:443-466)."""
+        (pos, pwr0) = self.get_measured_rays()
+        pos0 = np.array(np.divide(pos, np.matrix(np.linalg.norm(pos, axis=1)).T))
+        pwr0 = np.float64(pwr0).reshape(-1)
+        elevation0 = np.arccos(np.dot(pos0, pole)).reshape(-1)
+        order = np.argsort(elevation0, kind="stable")
+        elevation = elevation0[order]
+        cums = np.cumsum(pwr0[order])
+        half = cums[-1] / 2.0
+        idx = np.where(np.absolute(cums - half) == min(np.absolute(cums - half)))
+        return cums[-1], elevation[idx] / np.pi * 180.0, cums[idx] / cums[-1] * 100.0
+
+    def get_beam_HWHM(self, points=500, pole=[0, 0, 1, 0]):
+        """Half-width at half-maximum of the elevation intensity (:468-501)."""
+        (pos, pwr0) = self.get_measured_rays()
+        pos0 = np.array(np.divide(pos, np.matrix(np.linalg.norm(pos, axis=1)).T))
+        pwr0 = np.float64(pwr0).reshape(-1)
+        elevation0 = np.arccos(np.dot(pos0, pole)).reshape(-1)
+        order = np.argsort(elevation0, kind="stable")
+        (H, x) = np.histogram(a=elevation0[order], bins=points, weights=pwr0[order])
+        x = (x[0:-1] + x[1:]) / 2.0
+        H = (H.T / np.sin(x)).flatten()
+        hmax = max(H) / 2.0
+        idx = np.where(np.absolute(H - hmax) == min(np.absolute(H - hmax)))[0]
+        el = x[idx]
+        within = np.sum(pwr0[np.where(elevation0 < el)])
+        return sum(pwr0), el / np.pi * 180.0, within / sum(pwr0) * 100.0
+
+    def pickle_results(self):
+        """Pickle (results, meshes) to ./<timestamp>-tracer_results.txt (:711-733)."""
+        fname = "./{0}-tracer_results.txt".format(time.strftime("%Y.%m.%d.%H.%M.%S"))
+        try:
+            with open(fname, "wb") as f:
+                pickle.dump((self.results, self.meshes), f, protocol=pickle.HIGHEST_PROTOCOL)
+        except Exception:
+            print("Pickling results failed.")
+            return None
+        return fname
+
+    def load_pickle_results(self, path):
+        """Load results written by :meth:`pickle_results` (only load files you wrote)."""
+        with open(path, "rb") as f:
+            (self.results, self.meshes) = pickle.load(f)
+        self._aggregate = False
+
+    def save_traced_scene(self, dxf_file):
+        """DXF export of rays and facets; needs the optional ``dxfwrite`` package."""
+        from dxfwrite import DXFEngine as dxf  # noqa: optional dependency
+        drawing = dxf.drawing(dxf_file)
+        drawing.add_layer('Rays', color=3)
+        drawing.add_layer('Geometry', color=5)
+        for res in self.results:
+            for r0, rd in zip(res[0], res[1]):
+                drawing.add(dxf.face3d([r0[0:3], rd[0:3], rd[0:3]], layer="Rays"))
+        for t0, t1, t2 in zip(*self.geometry):
+            drawing.add(dxf.face3d([t0[0:3], t1[0:3], t2[0:3]], layer="Geometry"))
+        drawing.save()
+
+
+# alias with the north star's spelling
+CLTracer = CL_Tracer

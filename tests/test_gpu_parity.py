@@ -1,0 +1,216 @@
+"""GPU parity: liblpc (HIP, gfx950) against the CPU oracle on the same seeded inputs.
+
+Bar (DESIGN.md "Parity"): every intersection decision, index, destination and
+Fresnel child is BIT-EXACT (the hot loop's filter only selects candidates; the
+accept/reject and t are the reference arithmetic).  Documented tolerances only
+where a transcendental enters: dissipation exp() (2 ulp, rel 4e-7 on powers of
+rays that crossed a dissipative medium) and the angular projection
+(acos/atan2/sin/cos: bins may move for points within 1e-6 of an edge; histogram
+L1 rel <= 1e-5).
+"""
+import numpy as np
+import pytest
+
+from lightpycl_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+SCENES = [("parabolic", 2000), ("lens", 2000), ("eye", 600), ("cube", 2000), ("nested_cubes", 10),
+          ("synthetic", 700)]
+
+
+def rays_of(sc):
+    o = np.concatenate([np.asarray(s.rays_origin, np.float32) for s in sc.sources])
+    d = np.concatenate([np.asarray(s.rays_dir, np.float32) for s in sc.sources])
+    p = np.concatenate([np.asarray(s.rays_power, np.float32).reshape(-1) for s in sc.sources])
+    return o, d, p
+
+
+def _cmp_bounce(g, o, dissipative):
+    hit = o["isect_mid"] >= 0
+    for k in ("isect_mid", "n1", "n2", "r_meas", "t_meas", "meas"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    np.testing.assert_array_equal(g["isect_idx"], o["isect_idx"], err_msg="isect_idx")
+    np.testing.assert_array_equal(g["entering"][hit], o["entering"][hit], err_msg="entering")
+    np.testing.assert_array_equal(g["dest"][:, :3], o["dest"][:, :3], err_msg="dest")
+    for k in ("r_dir", "t_dir"):
+        np.testing.assert_array_equal(g[k][:, :3], o[k][:, :3], err_msg=k)
+    if dissipative:
+        for k in ("pow", "r_pow", "t_pow"):
+            np.testing.assert_allclose(g[k], o[k], rtol=4e-7, atol=0, err_msg=k)
+    else:
+        for k in ("pow", "r_pow", "t_pow"):
+            np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+
+
+@pytest.mark.parametrize("name,n", SCENES)
+def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
+    sc = scenes.BUILDERS[name](n=n, seed=3)
+    o4, d4, pw = rays_of(sc)
+    engine.upload_meshes(sc.meshes)
+    S = oracle_mod.Scene(sc.meshes)
+    diss = bool(np.any((S.mat_type == 0) & (S.diss > 1e-6)))
+    meas = np.zeros(len(pw), np.int32)
+    prev = np.full(len(pw), -2, np.int32)
+    g = engine.bounce(o4, d4, pw, meas, prev, sc.max_ray_len, sc.ior_env)
+    o = oracle_mod.bounce(S, o4, d4, pw, meas, prev, sc.max_ray_len, sc.ior_env)
+    _cmp_bounce(g, o, diss)
+    # second level: the oracle's kept children (prev_mid >= 0 exercises n1/n2 hand-over)
+    keep = np.where(np.concatenate((o["r_meas"], o["t_meas"])) == 0)[0]
+    if keep.size == 0:
+        return
+    o2 = np.concatenate((o["r_origin"], o["t_origin"]))[keep]
+    d2 = np.concatenate((o["r_dir"], o["t_dir"]))[keep]
+    p2 = np.concatenate((o["r_pow"], o["t_pow"]))[keep]
+    m2 = np.concatenate((o["isect_mid"], o["isect_mid"]))[keep]
+    z = np.zeros(keep.size, np.int32)
+    g2 = engine.bounce(o2, d2, p2, z, m2, sc.max_ray_len, sc.ior_env)
+    r2 = oracle_mod.bounce(S, o2, d2, p2, z, m2, sc.max_ray_len, sc.ior_env)
+    _cmp_bounce(g2, r2, diss)
+
+
+@pytest.mark.parametrize("name,n", [("parabolic", 3000), ("lens", 3000), ("eye", 300), ("cube", 3000),
+                                    ("nested_cubes", 10)])
+def test_trace_results_match_oracle(oracle_mod, name, n):
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    sc = scenes.BUILDERS[name](n=n, seed=5)
+    ref, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env)
+    tr = CL_Tracer(device=0)
+    res = tr.iterative_tracer(light_source=sc.sources, meshes=sc.meshes, trace_iterations=sc.iterations,
+                              trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env)
+    assert [len(r[3]) for r in res] == info["counts"]
+    assert tr.tri_count == info["tri_count"]
+    diss = name == "cube"
+    for it, (a, b) in enumerate(zip(res, ref)):
+        np.testing.assert_array_equal(a[0][:, :3], b[0][:, :3], err_msg=f"origin it{it}")
+        np.testing.assert_array_equal(a[1][:, :3], b[1][:, :3], err_msg=f"dest it{it}")
+        assert a[2].shape == b[2].shape and a[3].dtype == np.int32
+        np.testing.assert_array_equal(a[3], b[3], err_msg=f"meas it{it}")
+        if diss:
+            np.testing.assert_allclose(a[2], b[2], rtol=1e-5, atol=0)
+        else:
+            np.testing.assert_array_equal(a[2], b[2], err_msg=f"pow it{it}")
+    pos, pwr = tr.get_measured_rays()
+    rpos, rpwr = oracle_mod.measured_rays(ref)
+    np.testing.assert_array_equal(pos[:, :3], rpos[:, :3])
+    np.testing.assert_allclose(np.sum(np.float64(pwr)), np.sum(np.float64(rpwr)), rtol=1e-6)
+
+
+@pytest.mark.parametrize("name,n", [("parabolic", 4000), ("lens", 4000), ("synthetic", 1000)])
+def test_aggregate_mode_and_histogram(oracle_mod, name, n):
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    sc = scenes.BUILDERS[name](n=n, seed=11)
+    ref, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env)
+    tr = CL_Tracer(device=0)
+    tr.iterative_tracer(light_source=sc.sources, meshes=sc.meshes, trace_iterations=sc.iterations,
+                        trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env,
+                        keep_results=False)
+    assert tr.iteration_counts == info["counts"]
+    pos, pwr = tr.get_measured_rays()
+    rpos, rpwr = oracle_mod.measured_rays(ref)
+    np.testing.assert_array_equal(pos[:, :3], rpos[:, :3])          # same order: iteration, then ray
+    np.testing.assert_array_equal(pwr, np.asarray(rpwr).reshape(-1))
+    np.testing.assert_allclose(tr.measured_power(), info["mesh_power"], rtol=1e-12)
+    H, xe, ye = tr.get_binned_data_angular(limits=sc.hist_limits, points=sc.hist_points)
+    Hr, xr, yr = oracle_mod.binned_angular(rpos, rpwr, limits=sc.hist_limits, points=sc.hist_points)
+    np.testing.assert_array_equal(xe, xr)
+    np.testing.assert_array_equal(ye, yr)
+    l1 = np.abs(H - Hr).sum() / np.abs(Hr).sum()
+    assert l1 <= 1e-5, l1
+
+
+def test_chunked_trace_equals_unchunked(oracle_mod):
+    from lightpycl_amd.engine import Engine
+    sc = scenes.lens(n=5000, seed=2)
+    o4, d4, pw = rays_of(sc)
+    out = []
+    for chunk in (0, 777):
+        e = Engine(0)
+        e.upload_meshes(sc.meshes)
+        e.set_chunk(chunk)
+        e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+        its = []
+        for _ in range(6):
+            st, ex = e.iterate(export=True)
+            its.append(ex)
+        out.append((its, e.measured()))
+        e.close()
+    for a, b in zip(out[0][0], out[1][0]):
+        for k in ("origin", "dest", "pow", "meas", "next_pow"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert out[0][1][0] == out[1][1][0]
+
+
+def test_edge_cases(engine, oracle_mod):
+    sc = scenes.parabolic(n=1000, seed=4)
+    engine.upload_meshes(sc.meshes)
+    S = oracle_mod.Scene(sc.meshes)
+    # empty population
+    g = engine.bounce(np.zeros((0, 4), np.float32), np.zeros((0, 4), np.float32), np.zeros(0, np.float32),
+                      np.zeros(0, np.int32), np.zeros(0, np.int32))
+    assert g["dest"].shape == (0, 4)
+    # single ray, ray along the axis, ray pointing away from every surface (no hit)
+    o4 = np.array([[0, 0, 0, 0], [0, 0, 0, 0], [1e4, 1e4, 1e4, 0]], np.float32)
+    d4 = np.array([[0, 0, -1, 0], [0.6, 0.0, 0.8, 0], [1, 0, 0, 0]], np.float32)
+    pw = np.ones(3, np.float32)
+    z = np.zeros(3, np.int32)
+    pm = np.full(3, -2, np.int32)
+    g = engine.bounce(o4, d4, pw, z, pm, sc.max_ray_len, sc.ior_env)
+    o = oracle_mod.bounce(S, o4, d4, pw, z, pm, sc.max_ray_len, sc.ior_env)
+    _cmp_bounce(g, o, False)
+    assert g["isect_mid"][2] == -1 and g["meas"][2] == -1
+    # ragged count (not a multiple of the 512-ray block) and already-measured input rays
+    rng = np.random.default_rng(0)
+    n = 1237
+    o4, d4, pw = rays_of(scenes.parabolic(n=n, seed=9))
+    meas = rng.integers(-1, 2, n).astype(np.int32)
+    pm = rng.integers(-2, 2, n).astype(np.int32)
+    g = engine.bounce(o4, d4, pw, meas, pm, sc.max_ray_len, sc.ior_env)
+    o = oracle_mod.bounce(S, o4, d4, pw, meas, pm, sc.max_ray_len, sc.ior_env)
+    _cmp_bounce(g, o, False)
+
+
+def test_dropin_device_kernels(engine, oracle_mod):
+    """lpc_intersect / lpc_intersect_postproc / lpc_reflect_refract_rays on device
+    buffers in the reference's (n,4) and [ray][mesh] layouts."""
+    torch = pytest.importorskip("torch")
+    sc = scenes.eye(n=500, seed=6)
+    engine.upload_meshes(sc.meshes)
+    S = oracle_mod.Scene(sc.meshes)
+    o4, d4, pw = rays_of(sc)
+    n, K = len(pw), S.mesh_count
+    ref = oracle_mod.bounce(S, o4, d4, pw, np.zeros(n, np.int32), np.full(n, -2, np.int32),
+                            sc.max_ray_len, sc.ior_env)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    to, td = T(o4), T(d4)
+    tmin = torch.full((n, K), float(sc.max_ray_len), dtype=torch.float32, device=dev)
+    cnt = torch.zeros((n, K), dtype=torch.int32, device=dev)
+    itmp = torch.zeros((n, K), dtype=torch.int32, device=dev)
+    L, h = engine.L, engine.h
+    P = lambda t: t.data_ptr()
+    torch.cuda.synchronize()
+    engine._c(L.lpc_intersect(h, n, P(to), P(td), np.float32(sc.max_ray_len), P(tmin), P(cnt), P(itmp)))
+    np.testing.assert_array_equal(tmin.cpu().numpy(), ref["isect_min_ray_len"])
+    np.testing.assert_array_equal(cnt.cpu().numpy(), ref["isects_count"])
+    np.testing.assert_array_equal(itmp.cpu().numpy(), ref["isect_idx_tmp"])
+    dest = torch.zeros((n, 4), dtype=torch.float32, device=dev)
+    I = lambda: torch.zeros(n, dtype=torch.int32, device=dev)
+    prev = T(np.full(n, -2, np.int32))
+    n1, n2, ent, imid, iidx = I(), I(), I(), I(), I()
+    engine._c(L.lpc_intersect_postproc(h, n, P(to), P(td), P(dest), P(prev), P(n1), P(n2), P(ent), P(imid),
+                                       P(iidx), P(tmin), P(cnt), P(itmp), np.float32(sc.max_ray_len)))
+    np.testing.assert_array_equal(dest.cpu().numpy()[:, :3], ref["dest"][:, :3])
+    np.testing.assert_array_equal(imid.cpu().numpy(), ref["isect_mid"])
+    tp, tm = T(pw.copy()), I()
+    F4 = lambda: torch.zeros((n, 4), dtype=torch.float32, device=dev)
+    ro, rd, to2, td2 = F4(), F4(), F4(), F4()
+    rp, tpw = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    rm, tmm = I(), I()
+    engine._c(L.lpc_reflect_refract_rays(h, n, P(to), P(dest), P(td), P(tp), P(tm), P(n1), P(n2), P(ro), P(rd),
+                                         P(rp), P(rm), P(to2), P(td2), P(tpw), P(tmm), P(imid), P(iidx),
+                                         np.float32(sc.ior_env)))
+    np.testing.assert_array_equal(rd.cpu().numpy()[:, :3], ref["r_dir"][:, :3])
+    np.testing.assert_array_equal(td2.cpu().numpy()[:, :3], ref["t_dir"][:, :3])
+    np.testing.assert_array_equal(rp.cpu().numpy(), ref["r_pow"])
+    np.testing.assert_array_equal(tm.cpu().numpy(), ref["meas"])
