@@ -69,11 +69,32 @@ _PROTOS = {
 EXPORTED = tuple(_PROTOS) + ("lpc_last_error",)
 
 
+def _preload_hip_runtime():
+    """Share ONE HIP runtime with PyTorch.  torch links its own copy
+    (torch/lib/libamdhip64.so, DT_NEEDED "libamdhip64.so"); liblpc.so links
+    "libamdhip64.so.7".  Loading liblpc first would bring in /opt/rocm's runtime
+    and torch would later load a second one (two HSA runtimes -> "No HIP GPUs are
+    available").  Preloading torch's copy RTLD_GLOBAL makes liblpc's SONAME match
+    it.  LPC_HIP_RUNTIME=system keeps /opt/rocm's runtime (no torch in-process)."""
+    if os.environ.get("LPC_HIP_RUNTIME", "torch") == "system":
+        return None
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return None
+    cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+        return cand
+    return None
+
+
 def load(path: str = LIB_PATH):
     """Load liblpc.so and declare every entry point of include/lpc.h."""
     global _lib
     if _lib is not None:
         return _lib
+    _preload_hip_runtime()
     if not os.path.exists(path):
         raise LpcError(f"liblpc.so not built ({path}); run lightpycl_amd.build.build() "
                        "(hipcc --offload-arch=gfx950)")

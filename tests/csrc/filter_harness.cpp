@@ -1,0 +1,32 @@
+// CPU harness for lpc_math.hpp (the header the HIP kernels include): evaluates the
+// bounding-sphere filter the way k_intersect does (fused multiply-adds in float)
+// and the exact Moller-Trumbore acceptance, for property tests of the filter margin.
+#include <cmath>
+#include "lpc_math.hpp"
+
+using namespace lpc;
+
+extern "C" void filt_eval(int n, const float *O, const float *D, const float *V, float eps, double dcap,
+                          float *d_out, int *hit_out, float *t_out)
+{
+    for (int i = 0; i < n; ++i) {
+        const float *o = O + 3 * i, *dd = D + 3 * i, *v = V + 9 * i;
+        float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
+        FiltRec r = filter_record(v0, v1, v2, 0, dcap);
+        // k_intersect: unit direction, w = c - O, ww, wd, tq = negA - wd^2, d = ww*onemB + tq
+        float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
+        float nx = dd[0] * s, ny = dd[1] * s, nz = dd[2] * s;
+        float wx = r.cx - o[0], wy = r.cy - o[1], wz = r.cz - o[2];
+        float ww = fmaf(wz, wz, fmaf(wy, wy, wx * wx));
+        float wd = fmaf(wz, nz, fmaf(wy, ny, wx * nx));
+        float tq = fmaf(-wd, wd, r.negA);
+        d_out[i] = fmaf(ww, r.onemB, tq);
+        f3 V0 = mk3(v[0], v[1], v[2]);
+        f3 E1 = mk3(v[3] - v[0], v[4] - v[1], v[5] - v[2]);
+        f3 E2 = mk3(v[6] - v[0], v[7] - v[1], v[8] - v[2]);
+        float t = 0.0f;
+        int h = mt_exact(mk3(o[0], o[1], o[2]), mk3(dd[0], dd[1], dd[2]), V0, E1, E2, &t);
+        hit_out[i] = h && t > eps;
+        t_out[i] = t;
+    }
+}

@@ -1,0 +1,149 @@
+"""CPU tests of the drop-in host API (light_source, geo_optical_elements,
+iterative_tracer helpers) and of the C-ABI library surface (loads and exports
+every symbol of include/lpc.h; no compute without a GPU)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from lightpycl_amd import geo_optical_elements as goe
+from lightpycl_amd import light_source as lsrc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# -- light_source.py -----------------------------------------------------------
+def test_random_rays_layout_and_rng_sequence():
+    np.random.seed(123)
+    ls = lsrc.light_source(center=np.array([1, 2, 3, 0], np.float32), direction=(0, 0, 1), power=5.0,
+                           ray_count=1000)
+    nxt = np.random.rand()
+    np.random.seed(123)
+    draws = np.random.rand(2001)
+    assert nxt == draws[2000]                       # constructor draws u then v, N each
+    assert np.asarray(ls.rays_origin).shape == (1000, 4) and np.asarray(ls.rays_origin).dtype == np.float32
+    d = np.asarray(ls.rays_dir)
+    assert d.shape == (1000, 4) and d.dtype == np.float32
+    np.testing.assert_allclose(np.linalg.norm(d[:, :3], axis=1), 1.0, rtol=1e-6)
+    assert np.all(d[:, 2] >= 0)                     # +z hemisphere
+    assert np.isclose(np.sum(np.asarray(ls.rays_power, np.float64)), 5.0, rtol=1e-5)
+    np.testing.assert_array_equal(np.asarray(ls.rays_origin)[0], np.float32([1, 2, 3, 0]))
+    # directions are arccos(u) elevation, 2 pi v azimuth
+    u, v = draws[:1000], draws[1000:2000]
+    np.testing.assert_allclose(d[:, 2], np.cos(np.arccos(u)), atol=1e-6)
+
+
+def test_direction_rotation():
+    np.random.seed(0)
+    ls = lsrc.light_source(direction=(0, 0, -1), ray_count=500)
+    assert np.all(np.asarray(ls.rays_dir)[:, 2] <= 1e-6)
+    np.random.seed(0)
+    ls = lsrc.light_source(direction=(1, 0, 0), ray_count=500)
+    # the reference rotates row vectors by Rx(elevation) then Rz(azimuth)
+    # (light_source.py:136-137): with azimuth 0 the +z beam axis lands on +y
+    assert np.all(np.asarray(ls.rays_dir)[:, 1] >= -1e-6)
+
+
+def test_collimated_rays():
+    np.random.seed(5)
+    ls = lsrc.light_source(center=np.array([0, 0, -10, 0], np.float32), direction=(0, 0.01, 1),
+                           directivity=lambda x, y: 1.0 + 0.0 * np.cos(y), power=1000., ray_count=400)
+    ls.random_collimated_rays(diameter=5.0)
+    o = np.asarray(ls.rays_origin)
+    d = np.asarray(ls.rays_dir)
+    assert o.shape == (400, 4) and o.dtype == np.float32 and d.dtype == np.float32
+    assert np.allclose(d, d[0])                     # parallel
+    assert np.ptp(o[:, 0]) <= 5.0 + 1e-4
+    assert np.asarray(ls.rays_power).shape == (400,)
+    assert np.isclose(np.sum(ls.rays_power, dtype=np.float64), 1000.0, rtol=1e-6)
+
+
+# -- geo_optical_elements.py ---------------------------------------------------
+def test_generators_triangle_counts_and_materials():
+    oe = goe.optical_elements()
+    h = oe.hemisphere(center=[0, 0, 0, 0], radius=10.0)
+    assert len(h.triangles) == 2 * 71 * 73
+    s = oe.sphere(center=[0, 0, 0, 0], radius=1.0)
+    assert len(s.triangles) == 2 * 71 * 73
+    c = oe.cube(center=(0, 0, 0, 0), size=[2, 2, 2, 0])
+    assert len(c.triangles) == 12
+    m = oe.parabolic_mirror(reflectivity=0.5)
+    assert m.getMaterialBuf() == {"type": 1, "IOR": 1.0, "R": 1.0, "dissipation": 0.0}   # reference quirk
+    c.setMaterial(mat_type="refractive", IOR=1.7, dissipation=0.5)
+    assert c.getMaterialBuf() == {"type": 0, "IOR": 1.7, "R": 1.0, "dissipation": 0.5}
+    c.setMaterial(mat_type="nonsense")
+    assert c.getMaterialBuf()["type"] == 0
+
+
+def test_tribuf_translate_rotate():
+    oe = goe.optical_elements()
+    c = oe.cube(center=(0, 0, 0, 0), size=[2, 2, 2, 0])
+    v0, v1, v2 = c.tribuf()
+    assert len(v0) == 12 and np.asarray(v0).shape == (12, 4)
+    c.translate([1, 0, 0, 0])
+    assert np.isclose(np.asarray(c.vertices)[:, 0].mean(), 1.0)
+    c.rotate(axis="z", angle=np.pi / 2, pivot=(0, 0, 0, 0))
+    vv = np.asarray(c.vertices)
+    assert vv.dtype == np.float64 or vv.dtype == np.float32
+    assert np.allclose(vv[:, 1].mean(), 1.0, atol=1e-6)         # x -> y
+    assert np.all(vv[:, 3] == 0)
+
+
+def test_flatten_matches_oracle_scene(oracle_mod):
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    sc = scenes.eye(n=8, seed=1)
+    v0, v1, v2, mid, mt, ior, refl, diss = flatten_meshes(sc.meshes)
+    S = oracle_mod.Scene(sc.meshes)
+    for a, b in ((v0, S.v0), (v1, S.v1), (v2, S.v2), (mid, S.mesh_id), (mt, S.mat_type), (ior, S.ior),
+                 (refl, S.refl), (diss, S.diss)):
+        np.testing.assert_array_equal(a, b)
+    with pytest.raises(ValueError):
+        flatten_meshes([])
+
+
+# -- iterative_tracer host helpers -------------------------------------------------
+def test_f32_sorted_sum_semantics():
+    from lightpycl_amd.iterative_tracer import f32_sorted_sum
+    rng = np.random.default_rng(0)
+    a = rng.random(1000).astype(np.float32) * np.float32(1e3)
+    ref = 0
+    for x in np.sort(a):                        # builtin sum(np.sort(a)), as :372
+        ref = ref + x
+    assert f32_sorted_sum(a) == ref and np.asarray(ref).dtype == np.float32
+    a2 = a.reshape(-1, 1)                        # (N,1): np.sort per row -> original order (:115)
+    ref2 = 0
+    for x in np.sort(a2):
+        ref2 = ref2 + x
+    assert f32_sorted_sum(a2) == ref2[0]
+    assert f32_sorted_sum(np.zeros(0, np.float32)) == 0
+
+
+# -- C ABI surface ---------------------------------------------------------------
+def test_c_abi_exports_every_header_symbol():
+    from lightpycl_amd import _lib
+    from lightpycl_amd.build import build
+    build(verbose=False)
+    hdr = open(os.path.join(ROOT, "include", "lpc.h")).read()
+    declared = set(re.findall(r"^(?:int|const char \*)\s*(lpc_\w+)\(", hdr, flags=re.M))
+    assert len(declared) >= 20
+    assert declared == set(_lib.EXPORTED)
+    L = _lib.load()
+    for name in declared:
+        assert getattr(L, name) is not None
+    assert L.lpc_abi_version() == 1
+
+
+def test_c_abi_errors_without_device():
+    import ctypes
+    from lightpycl_amd import _lib
+    L = _lib.load()
+    if _lib.device_count() > 0:
+        pytest.skip("a HIP device is present")
+    h = ctypes.c_void_p()
+    rc = L.lpc_open(0, ctypes.byref(h))
+    assert rc != 0 and not h.value
+    assert L.lpc_last_error(None)                 # message for the failed open
+    assert L.lpc_close(None) == 0
+    assert L.lpc_trace_reset(None) != 0

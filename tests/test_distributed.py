@@ -1,0 +1,72 @@
+"""Multi-process (world_size 2, gloo, CPU) run of the sharded trace driver
+(lightpycl_amd.distributed): each rank traces its contiguous shard of the rays
+and all ranks take the reference's global termination decision from all-reduced
+(live rays, power left).  The global per-iteration ray counts and the summed
+per-mesh measured power must equal a single-process trace of all rays."""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, n, out_path):
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lightpycl_amd import scenes
+    from lightpycl_amd.distributed import ShardedTrace, TorchComm, shard_bounds
+    from oracle_engine import OracleEngine
+    sc = scenes.BUILDERS[name](n=n, seed=2)
+    o = np.asarray(sc.sources[0].rays_origin, np.float32)
+    d = np.asarray(sc.sources[0].rays_dir, np.float32)
+    p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
+    lo, hi = shard_bounds(len(p), rank, world)
+    eng = OracleEngine(sc.meshes, o[lo:hi], d[lo:hi], p[lo:hi], sc.max_ray_len, sc.ior_env)
+    r = ShardedTrace(eng, TorchComm(dist)).run(sc.iterations, sc.tau, float(np.sum(p[lo:hi], dtype=np.float64)))
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(dict(counts=r["global_counts"], mesh_power=list(map(float, r["mesh_power"]))), f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,n", [("lens", 3000), ("parabolic", 2001)])
+def test_sharded_trace_matches_single_process(oracle_mod, tmp_path, name, n):
+    from lightpycl_amd import scenes
+    out = str(tmp_path / "r.json")
+    mp.spawn(_worker, args=(2, _free_port(), name, n, out), nprocs=2, join=True)
+    got = json.load(open(out))
+    sc = scenes.BUILDERS[name](n=n, seed=2)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                               keep_results=False)
+    assert got["counts"] == info["counts"]
+    np.testing.assert_allclose(got["mesh_power"], info["mesh_power"], rtol=1e-12, atol=1e-12)
+
+
+def test_shard_bounds_cover():
+    from lightpycl_amd.distributed import shard_bounds
+    for n in (0, 1, 7, 1000, 1001):
+        for w in (1, 2, 3, 8):
+            parts = [shard_bounds(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1

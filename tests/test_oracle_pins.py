@@ -1,0 +1,98 @@
+"""Pin the CPU oracle (and the drop-in light_source / geo_optical_elements it is fed
+with) to outputs of the reference itself that SURVEY.md records:
+
+* triangle counts of the reference scenes ("probed triangle counts");
+* per-iteration ray counts of reference traces run during the survey with
+  np.random.seed(1) (SURVEY.md sections 5-7: lens 10k rays = 98,654 bounces with
+  iteration 4 = 10,743 rays; eye 2k rays iteration 6 = 39,942; eye 10k rays
+  [10000, 20000, 20000, 40000, 59999, 119973, 199617, 377766, 653109, 1220218];
+  parabolic: every ray hits the mirror then the hemisphere, 2 iterations);
+* the known-answer Fresnel rows of SURVEY.md section 4.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from lightpycl_amd import scenes
+
+
+def test_triangle_counts(oracle_mod):
+    expect = {"parabolic": 39420, "lens": 19006, "eye": 67390, "synthetic": 103660}
+    for name, m in expect.items():
+        sc = scenes.BUILDERS[name](n=16, seed=1)
+        assert oracle_mod.Scene(sc.meshes).tri_count == m, name
+
+
+def test_parabolic_counts(oracle_mod):
+    sc = scenes.parabolic(n=10000, seed=1)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, 16, 0.99, sc.max_ray_len, sc.ior_env, keep_results=False)
+    assert info["counts"] == [10000, 10000]
+    assert abs(info["mesh_power"][0] - 1.0) < 1e-6     # mirror R = 1.0 (setMaterial quirk)
+
+
+def test_lens_counts(oracle_mod):
+    sc = scenes.lens(n=10000, seed=1)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, 16, 0.99, sc.max_ray_len, sc.ior_env, keep_results=False)
+    assert info["counts"][4] == 10743
+    assert len(info["counts"]) == 8 and sum(info["counts"]) == 98654
+
+
+def test_eye_2k_prefix(oracle_mod):
+    sc = scenes.eye(n=2000, seed=1)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, 7, 0.99, sc.max_ray_len, sc.ior_env, keep_results=False)
+    assert info["counts"][6] == 39942
+
+
+@pytest.mark.skipif(not os.environ.get("LPC_SLOW"), reason="~2 min on 8 cores; set LPC_SLOW=1")
+def test_eye_10k_full(oracle_mod):
+    sc = scenes.eye(n=10000, seed=1)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, 16, 0.99, sc.max_ray_len, sc.ior_env, keep_results=False)
+    assert info["counts"] == [10000, 20000, 20000, 40000, 59999, 119973, 199617, 377766, 653109, 1220218]
+
+
+# -- SURVEY.md section 4 known-answer rows (reflect_refract_rays called directly) -------
+def kat_case(oracle_mod, mat, ior, refl, diss, n1, n2, d, origin=(0.2, 0.2, -1.0), meas=0):
+    """One ray whose destination is (0.2,0.2,0) on a triangle in the z=0 plane."""
+    L = oracle_mod.lib()
+    v0 = np.array([[-5, -5, 0, 0]], np.float32)
+    v1 = np.array([[5, -5, 0, 0]], np.float32)
+    v2 = np.array([[0, 5, 0, 0]], np.float32)
+    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))
+    i = lambda a: np.ascontiguousarray(np.asarray(a, np.int32))
+    O = f([[*origin, 0]])
+    D = f([[*d, 0]])
+    dest = f([[0.2, 0.2, 0.0, 0]])
+    pw = f([1.0])
+    ms = i([meas])
+    z4 = lambda: np.zeros((1, 4), np.float32)
+    ro, rd, to, td = z4(), z4(), z4(), z4()
+    rp, tp = np.zeros(1, np.float32), np.zeros(1, np.float32)
+    rm, tm = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    L.orc_reflect_refract_rays(1, O, dest, D, pw, ms, i([n1]), i([n2]), ro, rd, rp, rm, to, td, tp, tm,
+                               i([0]), i([0]), v0, v1, v2, i(mat), f(ior), f(refl), f(diss), np.float32(1.0))
+    return dict(pow=pw[0], meas=ms[0], r_dir=rd[0, :3], r_pow=rp[0], r_meas=rm[0], t_dir=td[0, :3], t_pow=tp[0],
+                t_meas=tm[0], r_org=ro[0, :3])
+
+
+def test_kat_rows(oracle_mod):
+    s = 0.70710678
+    r = kat_case(oracle_mod, [0], [1.5], [1.0], [0.0], -1, 0, (0, 0, 1))          # air -> glass, normal
+    assert r["r_pow"] == np.float32(0.040000003) and r["t_pow"] == np.float32(0.96)
+    assert np.array_equal(r["r_dir"], [0, 0, -1]) and np.array_equal(r["t_dir"], [0, 0, 1])
+    r = kat_case(oracle_mod, [0], [1.5], [1.0], [0.0], 0, -1, (s, 0, s))          # TIR glass -> air at 45 deg
+    assert r["r_pow"] == np.float32(1.0) and r["t_meas"] == -1 and r["t_pow"] == 0
+    np.testing.assert_allclose(r["r_dir"], [0.7071068, 0, -0.7071068], rtol=0, atol=1e-7)
+    assert np.array_equal(r["t_dir"], [0, 0, 0])
+    r = kat_case(oracle_mod, [1], [1.0], [0.9], [0.0], -1, -1, (0, 0, 1))        # mirror R = 0.9
+    assert r["r_pow"] == np.float32(0.9) and r["t_meas"] == -1
+    r = kat_case(oracle_mod, [0], [1.5], [1.0], [1.0], 0, -1, (0, 0, 1))          # dissipation, path 1
+    assert r["pow"] == np.float32(0.36787945)
+    assert r["r_pow"] == np.float32(0.014715179) and r["t_pow"] == np.float32(0.3531643)
+    r = kat_case(oracle_mod, [3], [1.0], [1.0], [0.0], -1, -1, (0, 0, 1))         # measure surface
+    assert r["meas"] == 1 and r["r_meas"] == -1 and r["t_meas"] == -1 and r["r_pow"] == 0
+    assert np.array_equal(r["r_org"], np.float32([0.2, 0.2, 0.0]))
+    r = kat_case(oracle_mod, [2], [1.0], [1.0], [0.0], -1, -1, (0, 0, 1))         # terminator
+    assert r["meas"] == -1
+    r = kat_case(oracle_mod, [0], [-2.0], [1.0], [0.0], -1, 0, (0, 0, 1))         # negative index
+    assert r["r_pow"] == np.float32(9.0) and r["t_pow"] == np.float32(-8.0)

@@ -1,0 +1,44 @@
+"""Summarise a tools/profile.sh run into profiles/ (committed evidence).
+
+    python tools/pmc_summary.py gpurun_out/prof r01
+
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats), profiles/<tag>_pmc.json
+(per-kernel averages of every PMC pass) and profiles/pmc_intersect.json, which
+bench.py reads for roofline.traffic: HBM bytes per k_intersect launch =
+(2 * FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of
+MI355X_MICROARCH.md section HBM (FETCH_SIZE reads half of a wide streaming read).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+src, tag = sys.argv[1], sys.argv[2]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+out = os.path.join(root, "profiles")
+os.makedirs(out, exist_ok=True)
+shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+per = collections.defaultdict(lambda: collections.defaultdict(list))
+for d in sorted(os.listdir(src)):
+    f = os.path.join(src, d, "pmc_counter_collection.csv")
+    if d.startswith("pmc") and os.path.exists(f):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"].split("(")[0]
+            per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+summary = {k: {c: {"launches": len(v), "mean": sum(v) / len(v), "values": v} for c, v in cs.items()}
+           for k, cs in per.items()}
+json.dump(summary, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
+ki = summary.get("lpck::k_intersect", {})
+if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
+    fetch, write = ki["FETCH_SIZE"]["mean"], ki["WRITE_SIZE"]["mean"]
+    rec = {"source": f"profiles/{tag}_pmc.json", "kernel": "k_intersect",
+           "fetch_size_kb_mean": fetch, "write_size_kb_mean": write,
+           "hbm_bytes_per_launch": (2.0 * fetch + write) * 1024.0,
+           "note": "mean over the k_intersect launches of one bench step (all iterations)"}
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
+        if c in ki:
+            rec[c.lower() + "_mean"] = ki[c]["mean"]
+    json.dump(rec, open(os.path.join(out, "pmc_intersect.json"), "w"), indent=1)
+    print(json.dumps(rec, indent=1))
