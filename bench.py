@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-rays", type=int, default=1 << 16, help="CPU baseline sample (rays, one bounce)")
+    ap.add_argument("--cpu-rays", type=int, default=1 << 20, help="CPU baseline sample (rays, one bounce)")
     return ap.parse_args()
 
 

@@ -649,8 +649,8 @@ int lpc_intersect(lpc_handle *h, int64_t n, const float *dev_origin4, const floa
         RaysIn in;
         in.ox = s; in.oy = s + Cw; in.oz = s + 2 * Cw; in.dx = s + 3 * Cw; in.dy = s + 4 * Cw;
         in.dz = s + 5 * Cw; in.pw = nullptr; in.pmid = nullptr;
-        RETIF(run_intersect(h, in, nc, max_ray_len, dev_tmin + base * h->K, dev_cnt + base * h->K,
-                            dev_itmp + base * h->K));
+        RETIF(run_intersect(h, in, nc, max_ray_len, dev_tmin + base * h->K, dev_itmp + base * h->K,
+                            dev_cnt + base * h->K));
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (h->prof) prof_resolve(h);
