@@ -31,9 +31,33 @@ namespace lpck {
 
 // ---------------------------------------------------------------------------
 // k_intersect
-// grid = (ceil(n/512), pieces), block = 256; thread t handles rays
-// base+t and base+256+t (coalesced SoA loads, packed FP32 pairs).
-__global__ __launch_bounds__(256) void k_intersect(RaysIn R, int64_t n,
+// grid = (ceil(n/512), pieces), block = 256.  Thread t handles the rays at sorted
+// positions base+t and base+256+t (perm: coherence order, see k_raykey), two rays
+// per lane as packed FP32 pairs.  A piece is a range of cluster groups of one
+// mesh run; each cluster (<= 64 triangles) is tested first and its triangles only
+// when some lane's ray passes near it.
+static __device__ __forceinline__ void sphere_test4(const float *cx, const float *cy, const float *cz,
+                                                    const float *onemB, const float *negA, f2 ox, f2 oy,
+                                                    f2 oz, f2 nx, f2 ny, f2 nz, f2 (&d)[4])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const f2 wx = cx[k] - ox, wy = cy[k] - oy, wz = cz[k] - oz;
+        const f2 ww = wx * wx + wy * wy + wz * wz;
+        const f2 wd = wx * nx + wy * ny + wz * nz;
+        const f2 tq = negA[k] - wd * wd;          // one SGPR operand per packed FMA
+        d[k] = ww * onemB[k] + tq;
+    }
+}
+
+static __device__ __forceinline__ float min8(const f2 (&d)[4])
+{
+    return fminf(fminf(fminf(d[0].x, d[0].y), fminf(d[1].x, d[1].y)),
+                 fminf(fminf(d[2].x, d[2].y), fminf(d[3].x, d[3].y)));
+}
+
+__global__ __launch_bounds__(256) void k_intersect(RaysIn R, int64_t n, const int32_t *__restrict__ perm,
+                                                   const ClusterGroup *__restrict__ cgrp,
                                                    const FiltGroup *__restrict__ grp,
                                                    const ExactRec *__restrict__ xrec,
                                                    const Piece *__restrict__ pieces, float eps,
@@ -42,62 +66,112 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, int64_t n,
                                                    int32_t *__restrict__ pc)
 {
     const int p = blockIdx.y;
-    const int64_t r0 = (int64_t)blockIdx.x * 512 + threadIdx.x;
-    const int64_t r1 = r0 + 256;
-    const int64_t q0 = r0 < n ? r0 : n - 1;
-    const int64_t q1 = r1 < n ? r1 : n - 1;
+    const int64_t s0 = (int64_t)blockIdx.x * 512 + threadIdx.x;
+    const int64_t s1 = s0 + 256;
+    const int64_t q0s = s0 < n ? s0 : n - 1;
+    const int64_t q1s = s1 < n ? s1 : n - 1;
+    const int64_t q0 = perm ? perm[q0s] : q0s;
+    const int64_t q1 = perm ? perm[q1s] : q1s;
     const f3 O0 = mk3(R.ox[q0], R.oy[q0], R.oz[q0]);
     const f3 O1 = mk3(R.ox[q1], R.oy[q1], R.oz[q1]);
     const f3 D0 = mk3(R.dx[q0], R.dy[q0], R.dz[q0]);
     const f3 D1 = mk3(R.dx[q1], R.dy[q1], R.dz[q1]);
     // unit direction for the filter only (its rounding is inside the margin)
-    const float s0 = 1.0f / sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z);
-    const float s1 = 1.0f / sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z);
+    const float u0 = 1.0f / sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z);
+    const float u1 = 1.0f / sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z);
     const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
-    const f2 nx = {D0.x * s0, D1.x * s1}, ny = {D0.y * s0, D1.y * s1}, nz = {D0.z * s0, D1.z * s1};
+    const f2 nx = {D0.x * u0, D1.x * u1}, ny = {D0.y * u0, D1.y * u1}, nz = {D0.z * u0, D1.z * u1};
 
     float t0 = max_ray_len, t1 = max_ray_len;
     int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
     const Piece pc_ = pieces[p];
-    const int32_t g_lo = pc_.lo >> 2, g_hi = pc_.hi >> 2;
-    FiltGroup G = grp[g_lo];
-    for (int32_t g = g_lo; g < g_hi; ++g) {
-        const FiltGroup Gn = grp[g + 1];      // prefetch (the array has one spare group)
-        f2 d[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const f2 wx = G.cx[k] - ox, wy = G.cy[k] - oy, wz = G.cz[k] - oz;
-            const f2 ww = wx * wx + wy * wy + wz * wz;
-            const f2 wd = wx * nx + wy * ny + wz * nz;
-            const f2 tq = G.negA[k] - wd * wd;        // one SGPR operand per packed FMA
-            d[k] = ww * G.onemB[k] + tq;
-        }
-        const float m = fminf(fminf(fminf(d[0].x, d[0].y), fminf(d[1].x, d[1].y)),
-                              fminf(fminf(d[2].x, d[2].y), fminf(d[3].x, d[3].y)));
-        if (m <= 0.0f) {
+    ClusterGroup CG = cgrp[pc_.lo];
+    for (int32_t cg = pc_.lo; cg < pc_.hi; ++cg) {
+        const ClusterGroup CGn = cgrp[cg + 1];          // prefetch (one spare at the end)
+        f2 dc[4];
+        sphere_test4(CG.cx, CG.cy, CG.cz, CG.onemB, CG.negA, ox, oy, oz, nx, ny, nz, dc);
+        if (min8(dc) <= 0.0f) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (d[k].x <= 0.0f || d[k].y <= 0.0f) {
-                    const int32_t idx = G.idx[k];
-                    const ExactRec x = xrec[idx];
-                    const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
-                    const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
-                    const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
-                    if (d[k].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
-                    if (d[k].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+                if (dc[k].x <= 0.0f || dc[k].y <= 0.0f) {
+                    const int32_t g_lo = CG.g_lo[k], g_hi = g_lo + CG.g_cnt[k];
+                    FiltGroup G = grp[g_lo];
+                    for (int32_t g = g_lo; g < g_hi; ++g) {
+                        const FiltGroup Gn = grp[g + 1];   // prefetch (one spare at the end)
+                        f2 d[4];
+                        sphere_test4(G.cx, G.cy, G.cz, G.onemB, G.negA, ox, oy, oz, nx, ny, nz, d);
+                        if (min8(d) <= 0.0f) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                if (d[j].x <= 0.0f || d[j].y <= 0.0f) {
+                                    const int32_t idx = G.idx[j];
+                                    const ExactRec x = xrec[idx];
+                                    const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
+                                    const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
+                                    const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
+                                    if (d[j].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+                                    if (d[j].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+                                }
+                            }
+                        }
+                        G = Gn;
+                    }
                 }
             }
         }
-        G = Gn;
+        CG = CGn;
     }
     const int64_t o = (int64_t)p * n;
-    if (r0 < n) { pt[o + r0] = t0; pi[o + r0] = i0; pc[o + r0] = c0; }
-    if (r1 < n) { pt[o + r1] = t1; pi[o + r1] = i1; pc[o + r1] = c1; }
+    if (s0 < n) { pt[o + q0] = t0; pi[o + q0] = i0; pc[o + q0] = c0; }
+    if (s1 < n) { pt[o + q1] = t1; pi[o + q1] = i1; pc[o + q1] = c1; }
+}
+
+// Ray coherence key: 15-bit Morton code of the origin cell (32^3 grid over the
+// scene box) above a 16-bit Morton code of the octahedral-mapped direction.
+static __device__ __forceinline__ uint32_t spread2(uint32_t x)   // 8 bits -> even bits
+{
+    x &= 0xff;
+    x = (x | (x << 4)) & 0x0f0f;
+    x = (x | (x << 2)) & 0x3333;
+    x = (x | (x << 1)) & 0x5555;
+    return x;
+}
+static __device__ __forceinline__ uint32_t spread3(uint32_t x)   // 5 bits -> every third bit
+{
+    x &= 0x1f;
+    x = (x | (x << 8)) & 0x100f;
+    x = (x | (x << 4)) & 0x10c3;
+    x = (x | (x << 2)) & 0x1249;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
+                                                float sx, float sy, float sz, uint32_t *__restrict__ keys,
+                                                int32_t *__restrict__ vals)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
+    const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+    float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
+    if (dz < 0.0f) {
+        const float tx = (1.0f - fabsf(py)) * (px >= 0.0f ? 1.0f : -1.0f);
+        const float ty = (1.0f - fabsf(px)) * (py >= 0.0f ? 1.0f : -1.0f);
+        px = tx; py = ty;
+    }
+    const uint32_t du = (uint32_t)fminf(fmaxf((px * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
+    const uint32_t dv = (uint32_t)fminf(fmaxf((py * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
+    const uint32_t ox = (uint32_t)fminf(fmaxf((R.ox[i] - bx0) * sx, 0.0f), 31.0f);
+    const uint32_t oy = (uint32_t)fminf(fmaxf((R.oy[i] - by0) * sy, 0.0f), 31.0f);
+    const uint32_t oz = (uint32_t)fminf(fmaxf((R.oz[i] - bz0) * sz, 0.0f), 31.0f);
+    const uint32_t okey = spread3(ox) | (spread3(oy) << 1) | (spread3(oz) << 2);
+    keys[i] = (okey << 16) | spread2(du) | (spread2(dv) << 1);
+    vals[i] = (int32_t)i;
 }
 
 // ---------------------------------------------------------------------------
-// k_combine: slot j of ray r = ordered combination of the pieces of the run
-// that flushes into slot j (first minimum wins, counts add).  Slots no run
+// k_combine: slot j of ray r = combination of the pieces of the run that
+// flushes into slot j (lowest-index minimum wins, counts add).  Slots no run
 // writes keep the reference's initial state (max_ray_len, idx 0, count 0)
 // unless keep_unwritten (drop-in mode: caller's buffer is left untouched).
 __global__ __launch_bounds__(256) void k_combine(int64_t n, int32_t K,
@@ -124,7 +198,10 @@ __global__ __launch_bounds__(256) void k_combine(int64_t n, int32_t K,
         for (int32_t p = lo; p < hi; ++p) {
             const int64_t b = (int64_t)p * n + r;
             const float tp = pt[b];
-            if (tp < t) { t = tp; idx = pi[b]; }
+            const int32_t ip = pi[b];
+            // lowest triangle index among the minimal t (pieces hold spatially
+            // sorted triangles, so index order is not piece order)
+            if (tp < t || (tp == t && ip >= 0 && (idx < 0 || ip < idx))) { t = tp; idx = ip; }
             cnt += pc[b];
         }
         st[a] = t; si[a] = idx; sc[a] = cnt;

@@ -73,7 +73,9 @@ LPC_HD void mt_accumulate(f3 O, f3 D, f3 V0, f3 E1, f3 E2, int32_t idx, float ep
 {
     float t;
     if (mt_exact(O, D, V0, E1, E2, &t) && t > eps) {
-        if (t < tmin) { tmin = t; imin = idx; }
+        // first minimum in triangle-index order (the reference's strict `<` over
+        // increasing i) == lowest index among equal t, whatever order we visit in
+        if (t < tmin || (t == tmin && idx < imin)) { tmin = t; imin = idx; }
         cnt += 1;
     }
 }
@@ -293,6 +295,16 @@ struct FiltGroup {
     int32_t pad[8];
 };
 
+// Four clusters in SoA form.  A cluster is up to 16 filter groups (64 triangles of
+// one mesh run, spatially sorted); its sphere test has the same form as a
+// triangle's and is implied by every member's test (cluster_record()).
+struct ClusterGroup {
+    float cx[4], cy[4], cz[4], onemB[4], negA[4];
+    int32_t g_lo[4];    // first filter group of the cluster
+    int32_t g_cnt[4];   // filter groups in the cluster (0 for padding)
+    int32_t pad[4];
+};
+
 struct ExactRec {       // V0, E1 = V1-V0, E2 = V2-V0 (float, exactly as the reference)
     float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, pad0, pad1, pad2;
 };
@@ -371,6 +383,56 @@ static inline FiltRec filter_record(
     if ((double)Af < A) Af = nextafterf(Af, INFINITY);
     r.onemB = onemB; r.negA = -Af;
     return r;
+}
+
+// Host: round a sphere test (A, B) to the float record form (A up, 1-B down).
+static inline void round_test(double A, double B, float *onemB_out, float *negA_out)
+{
+    if (!(B < 0.5)) { *onemB_out = -1e30f; *negA_out = 0.0f; return; }   // always a candidate
+    float onemB = (float)(1.0 - B * (1.0 + 1e-6));
+    if ((double)onemB > 1.0 - B) onemB = nextafterf(onemB, -INFINITY);
+    float Af = (float)(A * (1.0 + 1e-6));
+    if ((double)Af < A) Af = nextafterf(Af, INFINITY);
+    *onemB_out = onemB; *negA_out = -Af;
+}
+
+// Host: cluster test implied by its members' tests.  If a member's float test
+// passes, the exact line distance to its centre obeys dist_i^2 <= A_i + Bp_i w_i^2
+// (Bp_i = B_i + 32 eps covers the float evaluation).  With delta_i = |c_i - C|:
+// dist_C <= delta_i + sqrt(A_i) + sqrt(Bp_i)(|w_C| + delta_i) <= R0 + b |w_C|, so
+// dist_C^2 <= (1+h) R0^2 + (1+1/h) b^2 w_C^2; +64 eps on B for the cluster's own
+// float evaluation.  `never` members are skipped; an `always` member makes the
+// cluster always a candidate.
+static inline void cluster_record(const FiltRec *m, int count, float *cx, float *cy, float *cz,
+                                  float *onemB, float *negA)
+{
+    const double eps = 1.0 / 16777216.0, h = 0.05;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int live = 0;
+    bool always = false;
+    for (int i = 0; i < count; ++i) {
+        if (m[i].negA == INFINITY) continue;                 // never
+        if (m[i].onemB < -1e29f) { always = true; continue; }
+        const float c[3] = {m[i].cx, m[i].cy, m[i].cz};
+        for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], c[k]); hi[k] = fmax(hi[k], c[k]); }
+        ++live;
+    }
+    *cx = *cy = *cz = 0.0f;
+    if (always) { *onemB = -1e30f; *negA = 0.0f; return; }
+    if (live == 0) { *onemB = 1.0f; *negA = INFINITY; return; }
+    const float C[3] = {(float)(0.5 * (lo[0] + hi[0])), (float)(0.5 * (lo[1] + hi[1])),
+                        (float)(0.5 * (lo[2] + hi[2]))};
+    double R0 = 0.0, b = 0.0;
+    for (int i = 0; i < count; ++i) {
+        if (m[i].negA == INFINITY) continue;
+        const double A = -(double)m[i].negA, B = 1.0 - (double)m[i].onemB + 32.0 * eps;
+        const double dx = (double)m[i].cx - C[0], dy = (double)m[i].cy - C[1], dz = (double)m[i].cz - C[2];
+        const double dl = sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 1e-9);
+        R0 = fmax(R0, dl + sqrt(A) + sqrt(B) * dl);
+        b = fmax(b, sqrt(B));
+    }
+    *cx = C[0]; *cy = C[1]; *cz = C[2];
+    round_test((1.0 + h) * R0 * R0 * (1.0 + 1e-6), (1.0 + 1.0 / h) * b * b + 64.0 * eps, onemB, negA);
 }
 
 }  // namespace lpc

@@ -6,6 +6,8 @@
 #include "lpc_kernels.hip"
 #include "lpc.h"
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -64,10 +66,13 @@ struct lpc_handle {
     // scene
     int32_t M = 0, K = 0, Mpad = 0;
     std::vector<float> hv0, hv1, hv2;               // host copies (record rebuilds)
-    std::vector<int32_t> run_lo, run_hi, run_flo, run_fhi;
+    std::vector<int32_t> run_lo, run_hi;
+    std::vector<int32_t> run_clo, run_chi;           // cluster-group range per run
+    float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
     std::vector<int32_t> slot_run;
     std::vector<int32_t> meas_meshes;
-    DBuf d_frec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
+    DBuf d_frec, d_crec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
+    int32_t n_cgroups = 0;
     double dcap = 16.0;
     std::map<int32_t, PieceTable> ptabs;
     // workspace
@@ -75,7 +80,9 @@ struct lpc_handle {
     int64_t ws_rays = 0;
     int64_t ws_part = 0;                            // partial-array elements
     DBuf w_pt, w_pi, w_pc, w_st, w_si, w_sc, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
-    DBuf w_soa, w_stage;
+    DBuf w_soa, w_stage, w_sort, w_sort_tmp;
+    size_t sort_tmp_bytes = 0;
+    bool sort_rays = true;
     // trace
     Pop A, B, T, I;
     int64_t n_cur = 0, n_init = 0;
@@ -153,40 +160,109 @@ static inline unsigned grid1(int64_t n, int bs = 256) { return (unsigned)((n + b
 
 // ---------------------------------------------------------------------------
 // scene records
+static inline uint64_t spread21(uint64_t x)
+{
+    x &= 0x1fffff;
+    x = (x | x << 32) & 0x1f00000000ffffull;
+    x = (x | x << 16) & 0x1f0000ff0000ffull;
+    x = (x | x << 8) & 0x100f00f00f00f00full;
+    x = (x | x << 4) & 0x10c30c30c30c30c3ull;
+    x = (x | x << 2) & 0x1249249249249249ull;
+    return x;
+}
+
+// Filter groups (4 triangles) and cluster groups (4 clusters of <= 64 triangles)
+// per mesh run.  Triangles of a run are visited in Morton order of their
+// centroids so clusters are spatially compact; results do not depend on the
+// order (ties resolved by triangle index).
 static int build_records(lpc_handle *h)
 {
-    const int32_t M = h->M;
-    std::vector<FiltRec> fr;
-    fr.reserve((size_t)M + 4 * h->run_lo.size());
-    h->run_flo.clear();
-    h->run_fhi.clear();
+    std::vector<FiltGroup> groups;
+    std::vector<ClusterGroup> cgroups;
+    h->run_clo.clear();
+    h->run_chi.clear();
+    FiltRec never;
+    never.cx = never.cy = never.cz = 0.0f; never.onemB = 1.0f; never.negA = INFINITY; never.idx = -1;
+    never.pad0 = never.pad1 = 0;
     for (size_t r = 0; r < h->run_lo.size(); ++r) {
-        h->run_flo.push_back((int32_t)fr.size());
-        for (int32_t i = h->run_lo[r]; i < h->run_hi[r]; ++i)
-            fr.push_back(filter_record(&h->hv0[4 * (size_t)i], &h->hv1[4 * (size_t)i],
-                                       &h->hv2[4 * (size_t)i], i, h->dcap));
-        while (fr.size() % 4) {   // pad the run with "never" records
-            FiltRec z;
-            z.cx = z.cy = z.cz = 0.0f; z.onemB = 1.0f; z.negA = INFINITY; z.idx = -1;
-            z.pad0 = z.pad1 = 0;
-            fr.push_back(z);
+        const int32_t lo = h->run_lo[r], cnt = h->run_hi[r] - lo;
+        std::vector<FiltRec> fr((size_t)cnt);
+        std::vector<double> cen((size_t)cnt * 3);
+        double bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int32_t i = 0; i < cnt; ++i) {
+            const size_t t = (size_t)(lo + i);
+            fr[(size_t)i] = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap);
+            for (int k = 0; k < 3; ++k) {
+                const double c = ((double)h->hv0[4 * t + k] + h->hv1[4 * t + k] + h->hv2[4 * t + k]) / 3.0;
+                cen[3 * (size_t)i + k] = c;
+                if (std::isfinite(c)) { bl[k] = std::min(bl[k], c); bh[k] = std::max(bh[k], c); }
+            }
         }
-        h->run_fhi.push_back((int32_t)fr.size());
+        std::vector<std::pair<uint64_t, int32_t>> key((size_t)cnt);
+        for (int32_t i = 0; i < cnt; ++i) {
+            uint64_t q[3];
+            for (int k = 0; k < 3; ++k) {
+                const double ext = bh[k] - bl[k];
+                const double v = ext > 0 ? (cen[3 * (size_t)i + k] - bl[k]) / ext : 0.0;
+                q[k] = (uint64_t)std::min(std::max(v * 2097151.0, 0.0), 2097151.0);
+            }
+            key[(size_t)i] = {spread21(q[0]) | spread21(q[1]) << 1 | spread21(q[2]) << 2, i};
+        }
+        std::sort(key.begin(), key.end());
+        std::vector<FiltRec> ord((size_t)cnt);
+        for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)key[(size_t)i].second];
+        // clusters of <= 64 records, each a run of filter groups
+        std::vector<ClusterGroup> cls;   // used as a flat list, one cluster per slot 0
+        h->run_clo.push_back((int32_t)cgroups.size());
+        ClusterGroup cur;
+        int fill = 0;
+        auto flush = [&](bool pad) {
+            if (fill == 0) return;
+            for (; pad && fill < 4; ++fill) {
+                cur.cx[fill] = cur.cy[fill] = cur.cz[fill] = 0.0f;
+                cur.onemB[fill] = 1.0f; cur.negA[fill] = INFINITY;
+                cur.g_lo[fill] = 0; cur.g_cnt[fill] = 0; cur.pad[fill] = 0;
+            }
+            cgroups.push_back(cur);
+            fill = 0;
+        };
+        for (int32_t a = 0; a < cnt; a += 64) {
+            const int32_t m = std::min(64, cnt - a);
+            const int32_t g_lo = (int32_t)groups.size();
+            for (int32_t b = a; b < a + m; b += 4) {
+                FiltGroup G;
+                memset(&G, 0, sizeof(G));
+                for (int k = 0; k < 4; ++k) {
+                    const FiltRec &f = (b + k < a + m) ? ord[(size_t)(b + k)] : never;
+                    G.cx[k] = f.cx; G.cy[k] = f.cy; G.cz[k] = f.cz;
+                    G.onemB[k] = f.onemB; G.negA[k] = f.negA; G.idx[k] = f.idx;
+                }
+                groups.push_back(G);
+            }
+            float cx, cy, cz, ob, na;
+            cluster_record(&ord[(size_t)a], m, &cx, &cy, &cz, &ob, &na);
+            cur.cx[fill] = cx; cur.cy[fill] = cy; cur.cz[fill] = cz; cur.onemB[fill] = ob; cur.negA[fill] = na;
+            cur.g_lo[fill] = g_lo; cur.g_cnt[fill] = (int32_t)groups.size() - g_lo; cur.pad[fill] = 0;
+            if (++fill == 4) flush(false);
+        }
+        flush(true);
+        h->run_chi.push_back((int32_t)cgroups.size());
     }
-    h->Mpad = (int32_t)fr.size();
-    // SoA groups of 4 records + one spare group for the loop's prefetch
-    const size_t ng = fr.size() / 4 + 1;
-    std::vector<FiltGroup> gs(ng);
-    memset(gs.data(), 0, ng * sizeof(FiltGroup));
-    for (size_t i = 0; i < fr.size(); ++i) {
-        FiltGroup &G = gs[i / 4];
-        const int k = (int)(i % 4);
-        G.cx[k] = fr[i].cx; G.cy[k] = fr[i].cy; G.cz[k] = fr[i].cz;
-        G.onemB[k] = fr[i].onemB; G.negA[k] = fr[i].negA; G.idx[k] = fr[i].idx;
-    }
-    for (int k = 0; k < 4; ++k) { gs[ng - 1].onemB[k] = 1.0f; gs[ng - 1].negA[k] = INFINITY; gs[ng - 1].idx[k] = -1; }
-    RETIF(dalloc(h, h->d_frec, ng * sizeof(FiltGroup)));
-    HIPCHK(h, hipMemcpy(h->d_frec.p, gs.data(), ng * sizeof(FiltGroup), hipMemcpyHostToDevice));
+    // spare group / cluster group for the loops' one-ahead prefetch
+    FiltGroup sg;
+    memset(&sg, 0, sizeof(sg));
+    for (int k = 0; k < 4; ++k) { sg.onemB[k] = 1.0f; sg.negA[k] = INFINITY; sg.idx[k] = -1; }
+    groups.push_back(sg);
+    ClusterGroup sc;
+    memset(&sc, 0, sizeof(sc));
+    for (int k = 0; k < 4; ++k) { sc.onemB[k] = 1.0f; sc.negA[k] = INFINITY; }
+    cgroups.push_back(sc);
+    h->n_cgroups = (int32_t)cgroups.size() - 1;
+    h->Mpad = (int32_t)(groups.size() - 1) * 4;
+    RETIF(dalloc(h, h->d_frec, groups.size() * sizeof(FiltGroup)));
+    RETIF(dalloc(h, h->d_crec, cgroups.size() * sizeof(ClusterGroup)));
+    HIPCHK(h, hipMemcpy(h->d_frec.p, groups.data(), groups.size() * sizeof(FiltGroup), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_crec.p, cgroups.data(), cgroups.size() * sizeof(ClusterGroup), hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -200,16 +276,16 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     g = std::min<int32_t>(g, 4096);
     auto it = h->ptabs.find(g);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
-    int64_t S = (h->Mpad + g - 1) / g;
-    S = std::max<int64_t>(256, (S + 3) / 4 * 4);
+    int64_t S = (h->n_cgroups + g - 1) / g;          // cluster groups per piece
+    S = std::max<int64_t>(1, S);
     std::vector<Piece> pcs;
     std::vector<int32_t> rplo, rphi;
-    for (size_t r = 0; r < h->run_flo.size(); ++r) {
+    for (size_t r = 0; r < h->run_clo.size(); ++r) {
         rplo.push_back((int32_t)pcs.size());
-        for (int64_t a = h->run_flo[r]; a < h->run_fhi[r]; a += S) {
+        for (int64_t a = h->run_clo[r]; a < h->run_chi[r]; a += S) {
             Piece p;
             p.lo = (int32_t)a;
-            p.hi = (int32_t)std::min<int64_t>(a + S, h->run_fhi[r]);
+            p.hi = (int32_t)std::min<int64_t>(a + S, h->run_chi[r]);
             pcs.push_back(p);
         }
         rphi.push_back((int32_t)pcs.size());
@@ -265,6 +341,13 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_blk_pow, (size_t)nb * 8));
         RETIF(dalloc(h, h->w_soa, (size_t)8 * C * 4));
         RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
+        RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
+        size_t tb = 0;
+        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                     (const int32_t *)nullptr, (int32_t *)nullptr, (int)C, 0, 31,
+                                                     h->stream));
+        RETIF(dalloc(h, h->w_sort_tmp, tb));
+        h->sort_tmp_bytes = tb;
         h->ws_rays = C;
     }
     return 0;
@@ -325,19 +408,32 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     PieceTable *pt;
     RETIF(piece_table(h, n, &pt));
     const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
+    const int32_t *perm = nullptr;
+    if (h->sort_rays && n >= 4096) {
+        // coherence order: rays of one wave share origin cell and direction
+        const size_t C = (size_t)h->ws_rays;
+        uint32_t *kin = (uint32_t *)h->w_sort.p, *kout = kin + C;
+        int32_t *vin = (int32_t *)(kout + C), *vout = vin + C;
+        hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
+                           h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin);
+        size_t tb = h->sort_tmp_bytes;
+        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (int)n, 0, 31,
+                                                     h->stream));
+        perm = vout;
+    }
     dim3 grid((unsigned)((n + 511) / 512), (unsigned)pt->npieces);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-    hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, n,
-                       (const FiltGroup *)h->d_frec.p, (const ExactRec *)h->d_xrec.p,
-                       (const Piece *)pt->pieces.p, eps, max_ray_len, (float *)h->w_pt.p,
-                       (int32_t *)h->w_pi.p, (int32_t *)h->w_pc.p);
+    hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, n, perm,
+                       (const ClusterGroup *)h->d_crec.p, (const FiltGroup *)h->d_frec.p,
+                       (const ExactRec *)h->d_xrec.p, (const Piece *)pt->pieces.p, eps, max_ray_len,
+                       (float *)h->w_pt.p, (int32_t *)h->w_pi.p, (int32_t *)h->w_pc.p);
     HIPCHK(h, hipGetLastError());
     if (h->prof) {
         (void)hipEventRecord(e1, h->stream);
         h->ev_isect.push_back({e0, e1});
         h->prof_launches += 1;
-        h->prof_pairs += n * (int64_t)h->Mpad;
+        h->prof_pairs += n * (int64_t)h->M;
     }
     if (st_user) {
         hipLaunchKernelGGL(k_combine, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
@@ -431,7 +527,7 @@ int lpc_close(lpc_handle *h)
     DBuf *bufs[] = {&h->d_frec, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
                     &h->d_diss, &h->w_pt, &h->w_pi, &h->w_pc, &h->w_st, &h->w_si, &h->w_sc,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
-                    &h->w_stage, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
+                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_crec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp};
     for (DBuf *b : bufs) dfree(*b);
     for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.slot_plo); dfree(kv.second.slot_phi); }
@@ -499,6 +595,20 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
         x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
         x.pad0 = x.pad1 = x.pad2 = 0.0f;
         for (int k = 0; k < 3; ++k) { vv[9 * (size_t)i + k] = a[k]; vv[9 * (size_t)i + 3 + k] = b[k]; vv[9 * (size_t)i + 6 + k] = c[k]; }
+    }
+    {   // scene box for the ray coherence key
+        float lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (const std::vector<float> *vs : {&h->hv0, &h->hv1, &h->hv2})
+            for (int32_t i = 0; i < M; ++i)
+                for (int k = 0; k < 3; ++k) {
+                    const float v = (*vs)[4 * (size_t)i + k];
+                    if (std::isfinite(v)) { lo3[k] = std::min(lo3[k], v); hi3[k] = std::max(hi3[k], v); }
+                }
+        for (int k = 0; k < 3; ++k) {
+            const float ext = hi3[k] - lo3[k];
+            h->box_lo[k] = std::isfinite(lo3[k]) ? lo3[k] : 0.0f;
+            h->box_scale[k] = (std::isfinite(ext) && ext > 0.0f) ? 32.0f / ext : 1.0f;
+        }
     }
     h->ptabs.clear();   // piece tables depend on the scene
     h->dcap = 16.0;

@@ -30,3 +30,36 @@ extern "C" void filt_eval(int n, const float *O, const float *D, const float *V,
         t_out[i] = t;
     }
 }
+
+// Cluster test vs member tests: rays (n) x one cluster of m triangles.  Writes
+// each member's float test value (n*m) and the cluster's (n).
+static inline float eval_test(const float *o, float nx, float ny, float nz, float cx, float cy, float cz,
+                              float onemB, float negA)
+{
+    float wx = cx - o[0], wy = cy - o[1], wz = cz - o[2];
+    float ww = fmaf(wz, wz, fmaf(wy, wy, wx * wx));
+    float wd = fmaf(wz, nz, fmaf(wy, ny, wx * nx));
+    float tq = fmaf(-wd, wd, negA);
+    return fmaf(ww, onemB, tq);
+}
+
+extern "C" void cluster_eval(int n, const float *O, const float *D, int m, const float *V, double dcap,
+                             float *d_tri, float *d_cl)
+{
+    FiltRec rec[64];
+    for (int j = 0; j < m; ++j) {
+        const float *v = V + 9 * j;
+        float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
+        rec[j] = filter_record(v0, v1, v2, j, dcap);
+    }
+    float cx, cy, cz, ob, na;
+    cluster_record(rec, m, &cx, &cy, &cz, &ob, &na);
+    for (int i = 0; i < n; ++i) {
+        const float *o = O + 3 * i, *dd = D + 3 * i;
+        float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
+        float nx = dd[0] * s, ny = dd[1] * s, nz = dd[2] * s;
+        for (int j = 0; j < m; ++j)
+            d_tri[(size_t)i * m + j] = eval_test(o, nx, ny, nz, rec[j].cx, rec[j].cy, rec[j].cz, rec[j].onemB, rec[j].negA);
+        d_cl[i] = eval_test(o, nx, ny, nz, cx, cy, cz, ob, na);
+    }
+}

@@ -104,3 +104,50 @@ def test_degenerate_triangles_never_candidates(harness):
     D = (p / np.linalg.norm(p, axis=1, keepdims=True)).astype(np.float32)
     d, hit, _ = harness(O, D, V, eps=1e-3)
     assert not hit.any() and (d > 0).all()
+
+
+@pytest.fixture(scope="module")
+def cluster_harness(harness):
+    L = ctypes.CDLL(SO)
+    P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    L.cluster_eval.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_double, P, P]
+    L.cluster_eval.restype = None
+
+    def run(O, D, V, dcap=16.0):
+        n, m = O.shape[0], V.shape[0]
+        dt = np.zeros(n * m, np.float32)
+        dc = np.zeros(n, np.float32)
+        L.cluster_eval(n, np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32), m,
+                       np.ascontiguousarray(V, np.float32), dcap, dt, dc)
+        return dt.reshape(n, m), dc
+    return run
+
+
+@pytest.mark.parametrize("name", ["lens", "eye", "synthetic", "parabolic"])
+def test_cluster_test_implied_by_member_tests(cluster_harness, name):
+    """Every ray whose test passes for some triangle of a 64-triangle cluster must
+    pass the cluster's test (k_intersect skips the cluster's triangles otherwise).
+    Clusters are consecutive triangles of the real scenes' meshes; rays are aimed
+    at those triangles from near and far origins."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    sc = scenes.BUILDERS[name](n=8, seed=1)
+    v0, v1, v2, mid, *_ = flatten_meshes(sc.meshes)
+    rng = np.random.default_rng(7)
+    checked = 0
+    for start in rng.choice(len(v0) - 64, 40, replace=False):
+        V = np.concatenate([v0[start:start + 64, :3], v1[start:start + 64, :3], v2[start:start + 64, :3]], 1)
+        j = rng.integers(0, 64, 2000)
+        bu, bv = rng.random(2000), rng.random(2000)
+        flip = bu + bv > 1
+        bu[flip], bv[flip] = 1 - bu[flip], 1 - bv[flip]
+        tgt = V[j, :3] + bu[:, None] * (V[j, 3:6] - V[j, :3]) + bv[:, None] * (V[j, 6:9] - V[j, :3])
+        tgt += rng.normal(size=tgt.shape) * np.abs(V).max() * 1e-3
+        O = (tgt + rng.normal(size=tgt.shape) * rng.choice([1e-2, 1.0, 1e2, 1e3], (2000, 1))).astype(np.float32)
+        D = (tgt - O)
+        D /= np.linalg.norm(D, axis=1, keepdims=True)
+        dt, dc = cluster_harness(O, D.astype(np.float32), V.astype(np.float32))
+        tri_pass = (dt <= 0).any(axis=1)
+        assert not (tri_pass & ~(dc <= 0)).any()
+        checked += int(tri_pass.sum())
+    assert checked > 10000
