@@ -163,9 +163,14 @@ typedef struct {
     double intersect_ms;     /* sum of k_intersect durations (HIP events)       */
     double shade_ms;         /* postproc+Fresnel+compaction kernels             */
     int64_t intersect_launches;
-    int64_t pairs;           /* ray-triangle pairs examined by k_intersect      */
+    int64_t pairs;           /* ray-triangle pairs of the brute-force algorithm */
+    int64_t node_visits;     /* hierarchy nodes visited (per wave)              */
+    int64_t group_tests;     /* 4-triangle filter groups tested (per wave)      */
+    int64_t wave_traversals; /* (wave, piece) traversals                        */
+    int64_t exact_tests;     /* exact Moller-Trumbore tests (per ray)           */
 } lpc_prof;
-/* Enable (1) / disable (0) per-launch HIP-event timing of the hot kernels. */
+/* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
+ * k_intersect traversal counters (2, diagnostic: adds atomics), or disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
 

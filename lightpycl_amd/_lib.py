@@ -29,7 +29,9 @@ class IterStats(ctypes.Structure):
 
 class Prof(ctypes.Structure):
     _fields_ = [("intersect_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
-                ("intersect_launches", ctypes.c_int64), ("pairs", ctypes.c_int64)]
+                ("intersect_launches", ctypes.c_int64), ("pairs", ctypes.c_int64),
+                ("node_visits", ctypes.c_int64), ("group_tests", ctypes.c_int64),
+                ("wave_traversals", ctypes.c_int64), ("exact_tests", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

@@ -5,7 +5,28 @@
 
 namespace lpck {
 
-struct Piece { int32_t lo, hi; };   // filter-record range [lo, hi), length % 4 == 0
+struct Piece {                       // one subtree of a mesh run's hierarchy
+    int32_t root;                     // root node (-1: none)
+    int32_t s_lo, s_hi;               // sliver groups tested by this piece
+    int32_t slot;                     // per-mesh scratch slot the run flushes into
+};
+
+// Per (slot, ray) nearest hit as one 64-bit key: order-preserving float bits of
+// t above the triangle index, so atomicMin gives the minimal t and, among equal
+// t, the lowest index (the reference's first-minimum rule, .cl:277-283).
+__host__ __device__ inline unsigned long long slot_key(float t, int32_t idx)
+{
+    uint32_t u = __builtin_bit_cast(uint32_t, t);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (uint32_t)idx;
+}
+__host__ __device__ inline float slot_key_t(unsigned long long k)
+{
+    uint32_t u = (uint32_t)(k >> 32);
+    u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+    return __builtin_bit_cast(float, u);
+}
+__host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (int32_t)(uint32_t)k; }
 
 struct RaysIn {                       // a ray population (SoA)
     const float *ox, *oy, *oz, *dx, *dy, *dz, *pw;
@@ -31,8 +52,8 @@ struct ShadeArgs {
     const int32_t *meas_in;           // NULL -> 0 (device loop population)
     int64_t n;
     int32_t K;
-    const float *st;                  // [K][n] per-slot min t
-    const int32_t *si, *sc;           // [K][n] argmin, hit count
+    const unsigned long long *skey;   // [K][n] per-slot nearest hit (slot_key)
+    const int32_t *sc;                // [K][n] hit count
     const int32_t *mat_type;
     const float *ior, *refl, *diss, *verts;
     float max_ray_len, ior_env;

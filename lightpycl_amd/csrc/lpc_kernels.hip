@@ -6,8 +6,11 @@
 //                    broadcast from SGPRs (s_load), exact Moller-Trumbore only
 //                    for filter candidates -> per-piece (t_min, argmin, count).
 //                    Replaces __kernel intersect (.cl:243-289).
-//   k_combine        pieces -> per-mesh slots with the reference's
-//                    first-minimum-wins rule and slot arithmetic (.cl:260-288).
+//   k_gather         rays into coherence order (after k_raykey + radix sort).
+//   k_slot_init/k_slot_export
+//                    per-mesh scratch slots (.cl:260-288): pieces flush their
+//                    nearest hit with 64-bit atomicMin (slot_key) and counts
+//                    with atomicAdd, so the result is order independent.
 //   k_shade          intersect_postproc (.cl:105-240) + reflect_refract_rays
 //                    (.cl:346-474) fused, one lane per ray, SoA in / SoA out.
 //   k_count/k_scan/k_scatter
@@ -31,11 +34,13 @@ namespace lpck {
 
 // ---------------------------------------------------------------------------
 // k_intersect
-// grid = (ceil(n/512), pieces), block = 256.  Thread t handles the rays at sorted
-// positions base+t and base+256+t (perm: coherence order, see k_raykey), two rays
-// per lane as packed FP32 pairs.  A piece is a range of cluster groups of one
-// mesh run; each cluster (<= 64 triangles) is tested first and its triangles only
-// when some lane's ray passes near it.
+// grid = (ceil(n/512), pieces), block = 256 = 4 waves; each wave traces 128
+// consecutive rays of the coherence order (perm, see k_raykey), two per lane as
+// packed FP32 pairs, through one piece = one subtree of a mesh run's 4-wide
+// sphere hierarchy.  The wave walks the hierarchy as a packet with a wave-uniform
+// stack in LDS: a child is visited when any of its 128 rays passes the child's
+// sphere test; leaves are filter groups of 4 triangles whose candidates get the
+// exact Moller-Trumbore test.
 static __device__ __forceinline__ void sphere_test4(const float *cx, const float *cy, const float *cz,
                                                     const float *onemB, const float *negA, f2 ox, f2 oy,
                                                     f2 oz, f2 nx, f2 ny, f2 nz, f2 (&d)[4])
@@ -56,26 +61,46 @@ static __device__ __forceinline__ float min8(const f2 (&d)[4])
                  fminf(fminf(d[2].x, d[2].y), fminf(d[3].x, d[3].y)));
 }
 
-__global__ __launch_bounds__(256) void k_intersect(RaysIn R, int64_t n, const int32_t *__restrict__ perm,
-                                                   const ClusterGroup *__restrict__ cgrp,
+// Stack depth per wave (node refs); the host checks every mesh's hierarchy fits.
+#define LPC_STACK 64
+
+static __device__ __forceinline__ bool any_lane(bool b)
+{
+    return __builtin_amdgcn_ballot_w64(b) != 0;
+}
+
+__global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                   const int32_t *__restrict__ perm,
+                                                   const Node4 *__restrict__ nodes,
                                                    const FiltGroup *__restrict__ grp,
                                                    const ExactRec *__restrict__ xrec,
+                                                   const SliverGroup *__restrict__ srec,
                                                    const Piece *__restrict__ pieces, float eps,
-                                                   float max_ray_len, float *__restrict__ pt,
-                                                   int32_t *__restrict__ pi,
-                                                   int32_t *__restrict__ pc)
+                                                   float max_ray_len,
+                                                   unsigned long long *__restrict__ skey,
+                                                   int32_t *__restrict__ scnt,
+                                                   unsigned long long *__restrict__ stats)
 {
+    __shared__ int32_t stack[4][LPC_STACK];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int p = blockIdx.y;
-    const int64_t s0 = (int64_t)blockIdx.x * 512 + threadIdx.x;
-    const int64_t s1 = s0 + 256;
+    // 128 consecutive rays (in coherence order) per wave, two per lane
+    const int64_t s0 = (int64_t)blockIdx.x * 512 + wv * 128 + lane;
+    const int64_t s1 = s0 + 64;
     const int64_t q0s = s0 < n ? s0 : n - 1;
     const int64_t q1s = s1 < n ? s1 : n - 1;
-    const int64_t q0 = perm ? perm[q0s] : q0s;
-    const int64_t q1 = perm ? perm[q1s] : q1s;
-    const f3 O0 = mk3(R.ox[q0], R.oy[q0], R.oz[q0]);
-    const f3 O1 = mk3(R.ox[q1], R.oy[q1], R.oz[q1]);
-    const f3 D0 = mk3(R.dx[q0], R.dy[q0], R.dz[q0]);
-    const f3 D1 = mk3(R.dx[q1], R.dy[q1], R.dz[q1]);
+    f3 O0, O1, D0, D1;
+    if (rs) {            // rays already gathered into coherence order (k_gather)
+        O0 = mk3(rs[q0s], rs[n + q0s], rs[2 * n + q0s]);
+        O1 = mk3(rs[q1s], rs[n + q1s], rs[2 * n + q1s]);
+        D0 = mk3(rs[3 * n + q0s], rs[4 * n + q0s], rs[5 * n + q0s]);
+        D1 = mk3(rs[3 * n + q1s], rs[4 * n + q1s], rs[5 * n + q1s]);
+    } else {
+        O0 = mk3(R.ox[q0s], R.oy[q0s], R.oz[q0s]);
+        O1 = mk3(R.ox[q1s], R.oy[q1s], R.oz[q1s]);
+        D0 = mk3(R.dx[q0s], R.dy[q0s], R.dz[q0s]);
+        D1 = mk3(R.dx[q1s], R.dy[q1s], R.dz[q1s]);
+    }
     // unit direction for the filter only (its rounding is inside the margin)
     const float u0 = 1.0f / sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z);
     const float u1 = 1.0f / sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z);
@@ -84,46 +109,149 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, int64_t n, const in
 
     float t0 = max_ray_len, t1 = max_ray_len;
     int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
-    const Piece pc_ = pieces[p];
-    ClusterGroup CG = cgrp[pc_.lo];
-    for (int32_t cg = pc_.lo; cg < pc_.hi; ++cg) {
-        const ClusterGroup CGn = cgrp[cg + 1];          // prefetch (one spare at the end)
-        f2 dc[4];
-        sphere_test4(CG.cx, CG.cy, CG.cz, CG.onemB, CG.negA, ox, oy, oz, nx, ny, nz, dc);
-        if (min8(dc) <= 0.0f) {
+    int32_t *stk = stack[wv];
+    int32_t top = 0;
+    uint32_t n_nodes = 0, n_groups = 0, n_exact = 0;   // profiling counters (stats != NULL)
+    const Piece P = pieces[p];
+    if (P.root >= 0) stk[top++] = P.root;          // the piece's subtree
+    while (top > 0) {
+        const int32_t node = __builtin_amdgcn_readfirstlane(stk[--top]);
+        const Node4 N = nodes[node];
+        ++n_nodes;
+        f2 dn[4];
+        sphere_test4(N.cx, N.cy, N.cz, N.onemB, N.negA, ox, oy, oz, nx, ny, nz, dn);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (dc[k].x <= 0.0f || dc[k].y <= 0.0f) {
-                    const int32_t g_lo = CG.g_lo[k], g_hi = g_lo + CG.g_cnt[k];
-                    FiltGroup G = grp[g_lo];
-                    for (int32_t g = g_lo; g < g_hi; ++g) {
-                        const FiltGroup Gn = grp[g + 1];   // prefetch (one spare at the end)
-                        f2 d[4];
-                        sphere_test4(G.cx, G.cy, G.cz, G.onemB, G.negA, ox, oy, oz, nx, ny, nz, d);
-                        if (min8(d) <= 0.0f) {
+        for (int k = 0; k < 4; ++k) {
+            if (!any_lane(dn[k].x <= 0.0f || dn[k].y <= 0.0f)) continue;
+            const int32_t ref = N.ref[k];
+            if (ref >= 0) { stk[top++] = ref; continue; }
+            const FiltGroup G = grp[~ref];
+            ++n_groups;
+            f2 d[4];
+            sphere_test4(G.cx, G.cy, G.cz, G.onemB, G.negA, ox, oy, oz, nx, ny, nz, d);
+            if (min8(d) <= 0.0f) {
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                if (d[j].x <= 0.0f || d[j].y <= 0.0f) {
-                                    const int32_t idx = G.idx[j];
-                                    const ExactRec x = xrec[idx];
-                                    const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
-                                    const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
-                                    const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
-                                    if (d[j].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
-                                    if (d[j].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
-                                }
-                            }
-                        }
-                        G = Gn;
+                for (int j = 0; j < 4; ++j) {
+                    if (d[j].x <= 0.0f || d[j].y <= 0.0f) {
+                        const int32_t idx = G.idx[j];
+                        const ExactRec x = xrec[idx];
+                        const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
+                        const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
+                        const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
+                        if (d[j].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+                        if (d[j].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+                        n_exact += (d[j].x <= 0.0f) + (d[j].y <= 0.0f);
                     }
                 }
             }
         }
-        CG = CGn;
     }
-    const int64_t o = (int64_t)p * n;
-    if (s0 < n) { pt[o + q0] = t0; pi[o + q0] = i0; pc[o + q0] = c0; }
-    if (s1 < n) { pt[o + q1] = t1; pi[o + q1] = i1; pc[o + q1] = c1; }
+    // Slivers (line filter, see sliver_params): candidate iff
+    // (D.(E2 x T))^2 <= (|D| (a + b max|T_i|))^2; padding entries have a = NaN.
+    if (P.s_lo < P.s_hi) {
+        const f2 dx = {D0.x, D1.x}, dy = {D0.y, D1.y}, dz = {D0.z, D1.z};
+        const f2 dl = {sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z),
+                       sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z)};
+        for (int32_t sg = P.s_lo; sg < P.s_hi; ++sg) {
+            const SliverGroup G = srec[sg];
+            ++n_groups;
+            f2 d[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f2 tx = ox - G.v0x[k], ty = oy - G.v0y[k], tz = oz - G.v0z[k];
+                const f2 cx = G.e2y[k] * tz - G.e2z[k] * ty;
+                const f2 cy = G.e2z[k] * tx - G.e2x[k] * tz;
+                const f2 cz = G.e2x[k] * ty - G.e2y[k] * tx;
+                const f2 x = dx * cx + dy * cy + dz * cz;
+                const f2 tm = {fmaxf(fmaxf(fabsf(tx.x), fabsf(ty.x)), fabsf(tz.x)),
+                               fmaxf(fmaxf(fabsf(tx.y), fabsf(ty.y)), fabsf(tz.y))};
+                const f2 rhs = dl * (G.a[k] + G.b[k] * tm);
+                d[k] = x * x - rhs * rhs;
+            }
+            if (min8(d) <= 0.0f) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int32_t idx = G.idx[j];
+                    if (idx >= 0 && (d[j].x <= 0.0f || d[j].y <= 0.0f)) {
+                        const ExactRec xr = xrec[idx];
+                        const f3 V0 = mk3(xr.v0x, xr.v0y, xr.v0z);
+                        const f3 E1 = mk3(xr.e1x, xr.e1y, xr.e1z);
+                        const f3 E2 = mk3(xr.e2x, xr.e2y, xr.e2z);
+                        if (d[j].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+                        if (d[j].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+                        n_exact += (d[j].x <= 0.0f) + (d[j].y <= 0.0f);
+                    }
+                }
+            }
+        }
+    }
+    if (stats) {
+        for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
+        if (lane == 0) {
+            atomicAdd(&stats[0], (unsigned long long)n_nodes);
+            atomicAdd(&stats[1], (unsigned long long)n_groups);
+            atomicAdd(&stats[2], 1ull);
+            atomicAdd(&stats[3], (unsigned long long)n_exact);
+        }
+    }
+    // flush into the run's slot (original ray index): only pieces with hits write
+    const int64_t o = (int64_t)P.slot * n;
+    if (s0 < n) {
+        const int64_t q0 = perm ? perm[s0] : s0;
+        if (c0) atomicAdd(&scnt[o + q0], c0);
+        if (i0 >= 0) atomicMin(&skey[o + q0], slot_key(t0, i0));
+    }
+    if (s1 < n) {
+        const int64_t q1 = perm ? perm[s1] : s1;
+        if (c1) atomicAdd(&scnt[o + q1], c1);
+        if (i1 >= 0) atomicMin(&skey[o + q1], slot_key(t1, i1));
+    }
+}
+
+// Rays in coherence order, SoA [6][n] (ox oy oz dx dy dz), read coalesced by
+// every piece of k_intersect.
+__global__ __launch_bounds__(256) void k_gather(RaysIn R, int64_t n, const int32_t *__restrict__ perm,
+                                                float *__restrict__ rs)
+{
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int64_t q = perm[s];
+    rs[s] = R.ox[q]; rs[n + s] = R.oy[q]; rs[2 * n + s] = R.oz[q];
+    rs[3 * n + s] = R.dx[q]; rs[4 * n + s] = R.dy[q]; rs[5 * n + s] = R.dz[q];
+}
+
+// Slot initial state: slots a run flushes into start at (max_ray_len, idx -1,
+// count 0); slots no run writes keep the reference's initial scratch
+// (max_ray_len, idx 0, count 0).
+__global__ __launch_bounds__(256) void k_slot_init(int64_t n, int32_t K, const int32_t *__restrict__ live,
+                                                   float max_ray_len, unsigned long long *__restrict__ skey,
+                                                   int32_t *__restrict__ scnt)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    for (int32_t j = 0; j < K; ++j) {
+        skey[(int64_t)j * n + r] = slot_key(max_ray_len, live[j] ? -1 : 0);
+        scnt[(int64_t)j * n + r] = 0;
+    }
+}
+
+// Drop-in export of the slots to the reference's scratch buffers
+// (isect_min_ray_len / ray_isect_mesh_idx_tmp / isects_count, [ray][mesh]).
+// keep_unwritten: slots no run writes are left as the caller had them.
+__global__ __launch_bounds__(256) void k_slot_export(int64_t n, int32_t K, const int32_t *__restrict__ live,
+                                                     const unsigned long long *__restrict__ skey,
+                                                     const int32_t *__restrict__ scnt, float *__restrict__ st,
+                                                     int32_t *__restrict__ si, int32_t *__restrict__ sc,
+                                                     int keep_unwritten)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    for (int32_t j = 0; j < K; ++j) {
+        if (!live[j] && keep_unwritten) continue;
+        const unsigned long long k = skey[(int64_t)j * n + r];
+        const int64_t a = r * K + j;
+        st[a] = slot_key_t(k); si[a] = slot_key_idx(k); sc[a] = scnt[(int64_t)j * n + r];
+    }
 }
 
 // Ray coherence key: 15-bit Morton code of the origin cell (32^3 grid over the
@@ -170,45 +298,6 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
 }
 
 // ---------------------------------------------------------------------------
-// k_combine: slot j of ray r = combination of the pieces of the run that
-// flushes into slot j (lowest-index minimum wins, counts add).  Slots no run
-// writes keep the reference's initial state (max_ray_len, idx 0, count 0)
-// unless keep_unwritten (drop-in mode: caller's buffer is left untouched).
-__global__ __launch_bounds__(256) void k_combine(int64_t n, int32_t K,
-                                                 const int32_t *__restrict__ slot_plo,
-                                                 const int32_t *__restrict__ slot_phi,
-                                                 const float *__restrict__ pt,
-                                                 const int32_t *__restrict__ pi,
-                                                 const int32_t *__restrict__ pc,
-                                                 float max_ray_len, float *__restrict__ st,
-                                                 int32_t *__restrict__ si, int32_t *__restrict__ sc,
-                                                 int64_t sj, int64_t sr, int keep_unwritten)
-{
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    for (int32_t j = 0; j < K; ++j) {
-        const int32_t lo = slot_plo[j], hi = slot_phi[j];
-        const int64_t a = (int64_t)j * sj + r * sr;
-        if (lo >= hi) {
-            if (!keep_unwritten) { st[a] = max_ray_len; si[a] = 0; sc[a] = 0; }
-            continue;
-        }
-        float t = max_ray_len;
-        int32_t idx = -1, cnt = 0;
-        for (int32_t p = lo; p < hi; ++p) {
-            const int64_t b = (int64_t)p * n + r;
-            const float tp = pt[b];
-            const int32_t ip = pi[b];
-            // lowest triangle index among the minimal t (pieces hold spatially
-            // sorted triangles, so index order is not piece order)
-            if (tp < t || (tp == t && ip >= 0 && (idx < 0 || ip < idx))) { t = tp; idx = ip; }
-            cnt += pc[b];
-        }
-        st[a] = t; si[a] = idx; sc[a] = cnt;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
 __global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
 {
@@ -220,7 +309,8 @@ __global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
     const int64_t n = A.n;
     auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
         const int64_t a = (int64_t)j * n + r;
-        t = A.st[a]; c = A.sc[a]; i = A.si[a];
+        const unsigned long long k = A.skey[a];
+        t = slot_key_t(k); i = slot_key_idx(k); c = A.sc[a];
     };
     const PostOut po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
     const f3 dest = ray_dest(O, D, po.t_min);

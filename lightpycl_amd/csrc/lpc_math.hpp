@@ -295,13 +295,23 @@ struct FiltGroup {
     int32_t pad[8];
 };
 
-// Four clusters in SoA form.  A cluster is up to 16 filter groups (64 triangles of
-// one mesh run, spatially sorted); its sphere test has the same form as a
-// triangle's and is implied by every member's test (cluster_record()).
-struct ClusterGroup {
+// One node of the per-mesh sphere hierarchy: four child tests in SoA form.
+// ref[k] >= 0: child node index; ref[k] < 0: filter group ~ref[k] (4 triangles).
+// A child's test is implied by every test below it (cluster_record()), so a ray
+// that is a candidate for some triangle passes every node on the way down.
+struct Node4 {
     float cx[4], cy[4], cz[4], onemB[4], negA[4];
-    int32_t g_lo[4];    // first filter group of the cluster
-    int32_t g_cnt[4];   // filter groups in the cluster (0 for padding)
+    int32_t ref[4];
+    int32_t pad[8];
+};
+
+// Four "slivers" in SoA form: triangles whose sphere test degenerates (B >= 0.5,
+// e.g. revolve_curve's pole triangles with two vertices 1e-11 apart).  For them
+// Moller-Trumbore is rounding noise that can accept rays anywhere along the line
+// through V0 with direction E2, so they get a line filter instead (sliver_params).
+struct SliverGroup {
+    float v0x[4], v0y[4], v0z[4], e2x[4], e2y[4], e2z[4], a[4], b[4];
+    int32_t idx[4];
     int32_t pad[4];
 };
 
@@ -385,6 +395,33 @@ static inline FiltRec filter_record(
     return r;
 }
 
+// Host: line-filter constants of a sliver.  Moller-Trumbore accepts only if
+// |u| <= 1, i.e. |fl(P.T)| <= |fl(DEN)| (1+2eps) with P = D x E2, DEN = P.E1.
+// With |fl(P.T) - (D x E2).T| <= 10 eps |D||E2||T| and
+// |fl(DEN)| <= |D||E2 x E1| + 10 eps |D||E2||E1|, acceptance implies
+//     |D.(E2 x T)| <= |D| (|E2 x E1|(1+3eps) + 11 eps |E2||E1| + 10 eps |E2||T|).
+// The kernel tests x^2 <= (|D|(a + b tmax))^2 with x = D.(E2 x T) in float and
+// tmax = max|T_i| (|T| <= sqrt(3) tmax); a, b carry a factor 2 of slack for the
+// float evaluation of the test itself.
+static inline void sliver_params(const float *V0, const float *V1, const float *V2, float *a_out,
+                                 float *b_out)
+{
+    const double eps = 1.0 / 16777216.0;
+    double e1[3], e2[3];
+    for (int k = 0; k < 3; ++k) { e1[k] = (double)(V1[k] - V0[k]); e2[k] = (double)(V2[k] - V0[k]); }
+    const double c[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                         e2[0] * e1[1] - e2[1] * e1[0]};
+    const double nc = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    const double n2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+    double a = 2.0 * (nc * (1.0 + 4.0 * eps) + 16.0 * eps * n2 * n1);
+    double b = 2.0 * sqrt(3.0) * 32.0 * eps * n2;
+    float af = (float)a, bf = (float)b;
+    if ((double)af < a) af = nextafterf(af, INFINITY);
+    if ((double)bf < b) bf = nextafterf(bf, INFINITY);
+    *a_out = af; *b_out = bf;
+}
+
 // Host: round a sphere test (A, B) to the float record form (A up, 1-B down).
 static inline void round_test(double A, double B, float *onemB_out, float *negA_out)
 {
@@ -396,9 +433,10 @@ static inline void round_test(double A, double B, float *onemB_out, float *negA_
     *onemB_out = onemB; *negA_out = -Af;
 }
 
-// Host: cluster test implied by its members' tests.  If a member's float test
-// passes, the exact line distance to its centre obeys dist_i^2 <= A_i + Bp_i w_i^2
-// (Bp_i = B_i + 32 eps covers the float evaluation).  With delta_i = |c_i - C|:
+// Host: test of a cluster of TRIANGLES (any subtree of the hierarchy) implied by
+// the member triangles' tests.  If a member's float test passes, the exact line
+// distance to its centre obeys dist_i^2 <= A_i + Bp_i w_i^2 (Bp_i = B_i + 32 eps
+// covers the float evaluation).  With delta_i = |c_i - C|:
 // dist_C <= delta_i + sqrt(A_i) + sqrt(Bp_i)(|w_C| + delta_i) <= R0 + b |w_C|, so
 // dist_C^2 <= (1+h) R0^2 + (1+1/h) b^2 w_C^2; +64 eps on B for the cluster's own
 // float evaluation.  `never` members are skipped; an `always` member makes the

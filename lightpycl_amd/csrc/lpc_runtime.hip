@@ -48,7 +48,7 @@ struct Pop {
 };
 
 struct PieceTable {
-    DBuf pieces, slot_plo, slot_phi;
+    DBuf pieces;
     int32_t npieces = 0;
 };
 
@@ -67,20 +67,23 @@ struct lpc_handle {
     int32_t M = 0, K = 0, Mpad = 0;
     std::vector<float> hv0, hv1, hv2;               // host copies (record rebuilds)
     std::vector<int32_t> run_lo, run_hi;
-    std::vector<int32_t> run_clo, run_chi;           // cluster-group range per run
+    std::vector<int32_t> run_root;                   // hierarchy root node per run (-1: none)
+    std::vector<std::vector<int32_t>> run_frontier;  // node lists by depth (piece split)
+    std::vector<int32_t> run_slo, run_shi;           // sliver groups per run
+    int64_t n_slivers = 0;
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
     std::vector<int32_t> slot_run;
     std::vector<int32_t> meas_meshes;
-    DBuf d_frec, d_crec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
-    int32_t n_cgroups = 0;
+    DBuf d_frec, d_crec, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
+    std::vector<Node4> hnodes;                       // host copy of the hierarchy
     double dcap = 16.0;
     std::map<int32_t, PieceTable> ptabs;
     // workspace
     int64_t chunk = 0;                              // rays per chunk (0 -> default)
     int64_t ws_rays = 0;
-    int64_t ws_part = 0;                            // partial-array elements
-    DBuf w_pt, w_pi, w_pc, w_st, w_si, w_sc, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
+    DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
+    DBuf d_live;                                    // [K] slot written by some run
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
     // trace
@@ -92,8 +95,9 @@ struct lpc_handle {
     int64_t m_cap = 0, m_total = 0;
     DBuf d_acc;
     DBuf d_tmp;                                     // misc small device scratch
+    DBuf d_stats;                                   // k_intersect counters (profiling)
     // profiling
-    bool prof = false;
+    bool prof = false, prof_stats = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest;
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0;
@@ -171,33 +175,78 @@ static inline uint64_t spread21(uint64_t x)
     return x;
 }
 
-// Filter groups (4 triangles) and cluster groups (4 clusters of <= 64 triangles)
-// per mesh run.  Triangles of a run are visited in Morton order of their
-// centroids so clusters are spatially compact; results do not depend on the
-// order (ties resolved by triangle index).
+// Per mesh run: filter groups of 4 triangles in Morton order of the centroids,
+// and a 4-wide hierarchy built bottom-up over them (every entry's test is a
+// cluster_record() of the triangles below it).  Triangles whose sphere test is
+// degenerate ("always", B >= 0.5) go to the run's sliver list (line filter,
+// sliver_params) instead; triangles that can never be hit are dropped.  Results
+// do not depend on the order (ties are resolved by triangle index).
+static FiltRec test_rec(float cx, float cy, float cz, float onemB, float negA)
+{
+    FiltRec r;
+    r.cx = cx; r.cy = cy; r.cz = cz; r.onemB = onemB; r.negA = negA; r.idx = -1; r.pad0 = r.pad1 = 0;
+    return r;
+}
+
+static void drop_piece_tables(lpc_handle *h)
+{
+    for (auto &kv : h->ptabs) dfree(kv.second.pieces);
+    h->ptabs.clear();
+}
+
 static int build_records(lpc_handle *h)
 {
+    drop_piece_tables(h);   // pieces are subtrees of the hierarchy built here
     std::vector<FiltGroup> groups;
-    std::vector<ClusterGroup> cgroups;
-    h->run_clo.clear();
-    h->run_chi.clear();
-    FiltRec never;
-    never.cx = never.cy = never.cz = 0.0f; never.onemB = 1.0f; never.negA = INFINITY; never.idx = -1;
-    never.pad0 = never.pad1 = 0;
+    std::vector<SliverGroup> slivers;
+    std::vector<Node4> &nodes = h->hnodes;
+    nodes.clear();
+    h->run_root.clear();
+    h->run_frontier.clear();
+    h->run_slo.clear();
+    h->run_shi.clear();
+    h->n_slivers = 0;
+    const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 1.0f, INFINITY);
     for (size_t r = 0; r < h->run_lo.size(); ++r) {
-        const int32_t lo = h->run_lo[r], cnt = h->run_hi[r] - lo;
-        std::vector<FiltRec> fr((size_t)cnt);
-        std::vector<double> cen((size_t)cnt * 3);
+        const int32_t lo = h->run_lo[r], cnt_all = h->run_hi[r] - lo;
+        std::vector<FiltRec> fr;
+        std::vector<double> cen;
+        std::vector<int32_t> sl;
         double bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (int32_t i = 0; i < cnt; ++i) {
+        for (int32_t i = 0; i < cnt_all; ++i) {
             const size_t t = (size_t)(lo + i);
-            fr[(size_t)i] = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap);
+            const FiltRec f = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap);
+            if (f.negA == INFINITY) continue;                     // never a candidate
+            if (f.onemB < -1e29f) { sl.push_back(lo + i); continue; }
+            fr.push_back(f);
             for (int k = 0; k < 3; ++k) {
                 const double c = ((double)h->hv0[4 * t + k] + h->hv1[4 * t + k] + h->hv2[4 * t + k]) / 3.0;
-                cen[3 * (size_t)i + k] = c;
+                cen.push_back(c);
                 if (std::isfinite(c)) { bl[k] = std::min(bl[k], c); bh[k] = std::max(bh[k], c); }
             }
         }
+        // slivers: SoA groups of 4 (padding entries never pass: a = NaN)
+        h->run_slo.push_back((int32_t)slivers.size());
+        for (size_t a = 0; a < sl.size(); a += 4) {
+            SliverGroup G;
+            memset(&G, 0, sizeof(G));
+            for (int k = 0; k < 4; ++k) {
+                G.idx[k] = -1; G.a[k] = NAN; G.b[k] = 0.0f;
+                if (a + k >= sl.size()) continue;
+                const size_t t = (size_t)sl[a + k];
+                const float *V0 = &h->hv0[4 * t], *V1 = &h->hv1[4 * t], *V2 = &h->hv2[4 * t];
+                G.v0x[k] = V0[0]; G.v0y[k] = V0[1]; G.v0z[k] = V0[2];
+                G.e2x[k] = V2[0] - V0[0]; G.e2y[k] = V2[1] - V0[1]; G.e2z[k] = V2[2] - V0[2];
+                sliver_params(V0, V1, V2, &G.a[k], &G.b[k]);
+                G.idx[k] = (int32_t)t;
+            }
+            slivers.push_back(G);
+        }
+        h->run_shi.push_back((int32_t)slivers.size());
+        h->n_slivers += (int64_t)sl.size();
+        h->run_frontier.push_back(std::vector<int32_t>());
+        const int32_t cnt = (int32_t)fr.size();
+        if (cnt == 0) { h->run_root.push_back(-1); continue; }
         std::vector<std::pair<uint64_t, int32_t>> key((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) {
             uint64_t q[3];
@@ -211,100 +260,128 @@ static int build_records(lpc_handle *h)
         std::sort(key.begin(), key.end());
         std::vector<FiltRec> ord((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)key[(size_t)i].second];
-        // clusters of <= 64 records, each a run of filter groups
-        std::vector<ClusterGroup> cls;   // used as a flat list, one cluster per slot 0
-        h->run_clo.push_back((int32_t)cgroups.size());
-        ClusterGroup cur;
-        int fill = 0;
-        auto flush = [&](bool pad) {
-            if (fill == 0) return;
-            for (; pad && fill < 4; ++fill) {
-                cur.cx[fill] = cur.cy[fill] = cur.cz[fill] = 0.0f;
-                cur.onemB[fill] = 1.0f; cur.negA[fill] = INFINITY;
-                cur.g_lo[fill] = 0; cur.g_cnt[fill] = 0; cur.pad[fill] = 0;
-            }
-            cgroups.push_back(cur);
-            fill = 0;
+        // Every entry (a filter group or a node) covers a contiguous range of `ord`;
+        // its test is cluster_record() of the TRIANGLES in that range (not of the
+        // child tests), so the slack does not compound from level to level.
+        auto range_test = [&](int32_t a, int32_t b) {
+            FiltRec t = never;
+            cluster_record(&ord[(size_t)a], b - a, &t.cx, &t.cy, &t.cz, &t.onemB, &t.negA);
+            return t;
         };
-        for (int32_t a = 0; a < cnt; a += 64) {
-            const int32_t m = std::min(64, cnt - a);
-            const int32_t g_lo = (int32_t)groups.size();
-            for (int32_t b = a; b < a + m; b += 4) {
-                FiltGroup G;
-                memset(&G, 0, sizeof(G));
-                for (int k = 0; k < 4; ++k) {
-                    const FiltRec &f = (b + k < a + m) ? ord[(size_t)(b + k)] : never;
-                    G.cx[k] = f.cx; G.cy[k] = f.cy; G.cz[k] = f.cz;
-                    G.onemB[k] = f.onemB; G.negA[k] = f.negA; G.idx[k] = f.idx;
-                }
-                groups.push_back(G);
+        struct Ent { FiltRec t; int32_t ref, a, b; };
+        std::vector<Ent> ent;
+        for (int32_t a = 0; a < cnt; a += 4) {
+            FiltGroup G;
+            memset(&G, 0, sizeof(G));
+            const int32_t b = std::min(a + 4, cnt);
+            for (int k = 0; k < 4; ++k) {
+                const FiltRec &m = (a + k < cnt) ? ord[(size_t)(a + k)] : never;
+                G.cx[k] = m.cx; G.cy[k] = m.cy; G.cz[k] = m.cz;
+                G.onemB[k] = m.onemB; G.negA[k] = m.negA; G.idx[k] = m.idx;
             }
-            float cx, cy, cz, ob, na;
-            cluster_record(&ord[(size_t)a], m, &cx, &cy, &cz, &ob, &na);
-            cur.cx[fill] = cx; cur.cy[fill] = cy; cur.cz[fill] = cz; cur.onemB[fill] = ob; cur.negA[fill] = na;
-            cur.g_lo[fill] = g_lo; cur.g_cnt[fill] = (int32_t)groups.size() - g_lo; cur.pad[fill] = 0;
-            if (++fill == 4) flush(false);
+            ent.push_back({range_test(a, b), ~(int32_t)groups.size(), a, b});
+            groups.push_back(G);
         }
-        flush(true);
-        h->run_chi.push_back((int32_t)cgroups.size());
+        // internal levels, fan-out 4, until one node remains
+        std::vector<std::vector<int32_t>> levels;
+        for (;;) {
+            std::vector<Ent> up;
+            std::vector<int32_t> lvl;
+            for (size_t i = 0; i < ent.size(); i += 4) {
+                Node4 N;
+                memset(&N, 0, sizeof(N));
+                for (int k = 0; k < 4; ++k) {
+                    const bool live = i + k < ent.size();
+                    const FiltRec &m = live ? ent[i + k].t : never;
+                    N.cx[k] = m.cx; N.cy[k] = m.cy; N.cz[k] = m.cz;
+                    N.onemB[k] = m.onemB; N.negA[k] = m.negA;
+                    N.ref[k] = live ? ent[i + k].ref : ~0;
+                }
+                const int32_t a = ent[i].a, b = ent[std::min(i + 3, ent.size() - 1)].b;
+                up.push_back({range_test(a, b), (int32_t)nodes.size(), a, b});
+                lvl.push_back((int32_t)nodes.size());
+                nodes.push_back(N);
+            }
+            levels.push_back(lvl);
+            ent.swap(up);
+            if (ent.size() == 1) break;
+        }
+        if (levels.size() > 20) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
+        h->run_root.push_back(ent[0].ref);
+        // frontier lists from the root down (for splitting a run into pieces)
+        for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
+            h->run_frontier.back().push_back((int32_t)it->front());   // first node index of the level
+            h->run_frontier.back().push_back((int32_t)it->size());     // node count of the level
+        }
     }
-    // spare group / cluster group for the loops' one-ahead prefetch
+    // spare records so no buffer is empty
     FiltGroup sg;
     memset(&sg, 0, sizeof(sg));
     for (int k = 0; k < 4; ++k) { sg.onemB[k] = 1.0f; sg.negA[k] = INFINITY; sg.idx[k] = -1; }
     groups.push_back(sg);
-    ClusterGroup sc;
-    memset(&sc, 0, sizeof(sc));
-    for (int k = 0; k < 4; ++k) { sc.onemB[k] = 1.0f; sc.negA[k] = INFINITY; }
-    cgroups.push_back(sc);
-    h->n_cgroups = (int32_t)cgroups.size() - 1;
+    SliverGroup ss;
+    memset(&ss, 0, sizeof(ss));
+    for (int k = 0; k < 4; ++k) { ss.a[k] = NAN; ss.idx[k] = -1; }
+    slivers.push_back(ss);
+    if (nodes.empty()) { Node4 N; memset(&N, 0, sizeof(N)); nodes.push_back(N); }
     h->Mpad = (int32_t)(groups.size() - 1) * 4;
     RETIF(dalloc(h, h->d_frec, groups.size() * sizeof(FiltGroup)));
-    RETIF(dalloc(h, h->d_crec, cgroups.size() * sizeof(ClusterGroup)));
+    RETIF(dalloc(h, h->d_crec, nodes.size() * sizeof(Node4)));
+    RETIF(dalloc(h, h->d_srec, slivers.size() * sizeof(SliverGroup)));
     HIPCHK(h, hipMemcpy(h->d_frec.p, groups.data(), groups.size() * sizeof(FiltGroup), hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->d_crec.p, cgroups.data(), cgroups.size() * sizeof(ClusterGroup), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_crec.p, nodes.data(), nodes.size() * sizeof(Node4), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_srec.p, slivers.data(), slivers.size() * sizeof(SliverGroup),
+                        hipMemcpyHostToDevice));
     return 0;
 }
 
-// Piece table for a launch of n rays: each run split into slices of S records
-// so that blocks_x * pieces fills the GPU.
+// Piece table for a launch of n rays: pieces = subtrees of the runs that own a
+// slot (a run whose slot a later run overwrites is skipped, as its results are),
+// each run split at the shallowest hierarchy level with >= g nodes so that
+// blocks_x * pieces fills the GPU.
 static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
 {
     const int64_t bx = std::max<int64_t>(1, (n + 511) / 512);
-    const int64_t target_blocks = 4096;
-    int32_t g = (int32_t)std::max<int64_t>(1, (target_blocks + bx - 1) / bx);
+    std::vector<int32_t> run_slot(h->run_root.size(), -1);
+    for (int32_t j = 0; j < h->K; ++j)
+        if (h->slot_run[(size_t)j] >= 0) run_slot[(size_t)h->slot_run[(size_t)j]] = j;
+    int64_t live_runs = 0;
+    for (int32_t v : run_slot) live_runs += v >= 0;
+    const int64_t target_blocks = 8192;
+    int32_t g = (int32_t)std::max<int64_t>(1, (target_blocks + bx * std::max<int64_t>(live_runs, 1) - 1) /
+                                                  (bx * std::max<int64_t>(live_runs, 1)));
     g = std::min<int32_t>(g, 4096);
     auto it = h->ptabs.find(g);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
-    int64_t S = (h->n_cgroups + g - 1) / g;          // cluster groups per piece
-    S = std::max<int64_t>(1, S);
     std::vector<Piece> pcs;
-    std::vector<int32_t> rplo, rphi;
-    for (size_t r = 0; r < h->run_clo.size(); ++r) {
-        rplo.push_back((int32_t)pcs.size());
-        for (int64_t a = h->run_clo[r]; a < h->run_chi[r]; a += S) {
+    for (size_t r = 0; r < h->run_root.size(); ++r) {
+        if (run_slot[r] < 0) continue;
+        const std::vector<int32_t> &L = h->run_frontier[r];   // (first, count) per level, root first
+        std::vector<int32_t> roots;
+        if (!L.empty()) {
+            size_t lv = 0;
+            while (lv + 1 < L.size() / 2 && L[2 * lv + 1] < g) ++lv;
+            for (int32_t i = 0; i < L[2 * lv + 1]; ++i) roots.push_back(L[2 * lv] + i);
+        }
+        // the run's sliver groups are shared out over its pieces
+        const int32_t slo = h->run_slo[r], ns = h->run_shi[r] - slo;
+        const int32_t np = std::max<int32_t>((int32_t)roots.size(), std::min<int32_t>(ns, std::max(g, 1)));
+        for (int32_t i = 0; i < np; ++i) {
             Piece p;
-            p.lo = (int32_t)a;
-            p.hi = (int32_t)std::min<int64_t>(a + S, h->run_chi[r]);
+            p.root = i < (int32_t)roots.size() ? roots[(size_t)i] : -1;
+            p.s_lo = slo + (int32_t)((int64_t)ns * i / np);
+            p.s_hi = slo + (int32_t)((int64_t)ns * (i + 1) / np);
+            p.slot = run_slot[r];
             pcs.push_back(p);
         }
-        rphi.push_back((int32_t)pcs.size());
     }
     if (pcs.size() > 65535) return set_err(h, LPC_E_ARG, "too many triangle pieces");
-    std::vector<int32_t> splo(h->K), sphi(h->K);
-    for (int32_t j = 0; j < h->K; ++j) {
-        int32_t r = h->slot_run[j];
-        splo[j] = r >= 0 ? rplo[r] : 0;
-        sphi[j] = r >= 0 ? rphi[r] : 0;
-    }
     PieceTable &t = h->ptabs[g];
-    RETIF(dalloc(h, t.pieces, pcs.size() * sizeof(Piece)));
-    RETIF(dalloc(h, t.slot_plo, splo.size() * 4));
-    RETIF(dalloc(h, t.slot_phi, sphi.size() * 4));
-    HIPCHK(h, hipMemcpy(t.pieces.p, pcs.data(), pcs.size() * sizeof(Piece), hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(t.slot_plo.p, splo.data(), splo.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(t.slot_phi.p, sphi.data(), sphi.size() * 4, hipMemcpyHostToDevice));
     t.npieces = (int32_t)pcs.size();
+    if (!pcs.empty()) {
+        RETIF(dalloc(h, t.pieces, pcs.size() * sizeof(Piece)));
+        HIPCHK(h, hipMemcpy(t.pieces.p, pcs.data(), pcs.size() * sizeof(Piece), hipMemcpyHostToDevice));
+    }
     *out = &t;
     return 0;
 }
@@ -314,25 +391,15 @@ static int64_t chunk_rays(const lpc_handle *h)
     return h->chunk > 0 ? h->chunk : (int64_t)8 << 20;
 }
 
-// Workspace for a chunk of `n` rays (partials sized pieces(n) * n).
+// Workspace for a chunk of `n` rays.
 static int ensure_ws(lpc_handle *h, int64_t n)
 {
-    PieceTable *pt;
-    RETIF(piece_table(h, n, &pt));
-    const int64_t pe = (int64_t)pt->npieces * n;
-    if (n <= h->ws_rays && pe <= h->ws_part) return 0;
-    if (pe > h->ws_part) {
-        const int64_t PE = std::max(pe, h->ws_part);
-        RETIF(dalloc(h, h->w_pt, (size_t)PE * 4));
-        RETIF(dalloc(h, h->w_pi, (size_t)PE * 4));
-        RETIF(dalloc(h, h->w_pc, (size_t)PE * 4));
-        h->ws_part = PE;
-    }
-    if (n > h->ws_rays) {
+    if (n <= h->ws_rays) return 0;
+    {
         const int64_t C = n;
-        RETIF(dalloc(h, h->w_st, (size_t)h->K * C * 4));
-        RETIF(dalloc(h, h->w_si, (size_t)h->K * C * 4));
+        RETIF(dalloc(h, h->w_key, (size_t)h->K * C * 8));
         RETIF(dalloc(h, h->w_sc, (size_t)h->K * C * 4));
+        RETIF(dalloc(h, h->w_rs, (size_t)6 * C * 4));
         RETIF(dalloc(h, h->w_shf, (size_t)kShadeF * C * 4));
         RETIF(dalloc(h, h->w_shi, (size_t)kShadeI * C * 4));
         const int64_t nb = (C + 1023) / 1024;
@@ -399,8 +466,8 @@ static void prof_resolve(lpc_handle *h)
     h->ev_rest.clear();
 }
 
-// intersect + combine for n rays of `in` into the slot arrays (or a caller's
-// [ray][mesh] buffers when st_user != NULL).
+// intersect for n rays of `in` into the slot arrays, and optionally into a
+// caller's [ray][mesh] buffers (st_user != NULL, the reference's scratch layout).
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
                          float *st_user, int32_t *si_user, int32_t *sc_user)
 {
@@ -408,7 +475,12 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     PieceTable *pt;
     RETIF(piece_table(h, n, &pt));
     const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
+    unsigned long long *skey = (unsigned long long *)h->w_key.p;
+    int32_t *scnt = (int32_t *)h->w_sc.p;
+    hipLaunchKernelGGL(k_slot_init, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
+                       (const int32_t *)h->d_live.p, max_ray_len, skey, scnt);
     const int32_t *perm = nullptr;
+    const float *rs = nullptr;
     if (h->sort_rays && n >= 4096) {
         // coherence order: rays of one wave share origin cell and direction
         const size_t C = (size_t)h->ws_rays;
@@ -420,33 +492,30 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (int)n, 0, 31,
                                                      h->stream));
         perm = vout;
+        hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
+        rs = (const float *)h->w_rs.p;
     }
-    dim3 grid((unsigned)((n + 511) / 512), (unsigned)pt->npieces);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-    hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, n, perm,
-                       (const ClusterGroup *)h->d_crec.p, (const FiltGroup *)h->d_frec.p,
-                       (const ExactRec *)h->d_xrec.p, (const Piece *)pt->pieces.p, eps, max_ray_len,
-                       (float *)h->w_pt.p, (int32_t *)h->w_pi.p, (int32_t *)h->w_pc.p);
-    HIPCHK(h, hipGetLastError());
-    if (h->prof) {
-        (void)hipEventRecord(e1, h->stream);
-        h->ev_isect.push_back({e0, e1});
-        h->prof_launches += 1;
-        h->prof_pairs += n * (int64_t)h->M;
+    if (pt->npieces > 0) {
+        dim3 grid((unsigned)((n + 511) / 512), (unsigned)pt->npieces);
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+        hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, rs, n, perm,
+                           (const Node4 *)h->d_crec.p, (const FiltGroup *)h->d_frec.p,
+                           (const ExactRec *)h->d_xrec.p, (const SliverGroup *)h->d_srec.p,
+                           (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt,
+                           h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr);
+        HIPCHK(h, hipGetLastError());
+        if (h->prof) {
+            (void)hipEventRecord(e1, h->stream);
+            h->ev_isect.push_back({e0, e1});
+            h->prof_launches += 1;
+            h->prof_pairs += n * (int64_t)h->M;
+        }
     }
     if (st_user) {
-        hipLaunchKernelGGL(k_combine, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
-                           (const int32_t *)pt->slot_plo.p, (const int32_t *)pt->slot_phi.p,
-                           (const float *)h->w_pt.p, (const int32_t *)h->w_pi.p,
-                           (const int32_t *)h->w_pc.p, max_ray_len, st_user, si_user, sc_user,
-                           (int64_t)1, (int64_t)h->K, 1);
-    } else {
-        hipLaunchKernelGGL(k_combine, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
-                           (const int32_t *)pt->slot_plo.p, (const int32_t *)pt->slot_phi.p,
-                           (const float *)h->w_pt.p, (const int32_t *)h->w_pi.p,
-                           (const int32_t *)h->w_pc.p, max_ray_len, (float *)h->w_st.p,
-                           (int32_t *)h->w_si.p, (int32_t *)h->w_sc.p, (int64_t)n, (int64_t)1, 0);
+        hipLaunchKernelGGL(k_slot_export, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
+                           (const int32_t *)h->d_live.p, (const unsigned long long *)skey,
+                           (const int32_t *)scnt, st_user, si_user, sc_user, 1);
     }
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -457,7 +526,7 @@ static int run_shade(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, in
 {
     ShadeArgs A;
     A.in = in; A.meas_in = meas_in; A.n = n; A.K = h->K;
-    A.st = (const float *)h->w_st.p; A.si = (const int32_t *)h->w_si.p; A.sc = (const int32_t *)h->w_sc.p;
+    A.skey = (const unsigned long long *)h->w_key.p; A.sc = (const int32_t *)h->w_sc.p;
     A.mat_type = (const int32_t *)h->d_mat.p; A.ior = (const float *)h->d_ior.p;
     A.refl = (const float *)h->d_refl.p; A.diss = (const float *)h->d_diss.p;
     A.verts = (const float *)h->d_verts.p;
@@ -525,12 +594,12 @@ int lpc_close(lpc_handle *h)
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     DBuf *bufs[] = {&h->d_frec, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
-                    &h->d_diss, &h->w_pt, &h->w_pi, &h->w_pc, &h->w_st, &h->w_si, &h->w_sc,
+                    &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
-                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_crec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp};
+                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_crec, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
+                    &h->d_acc, &h->d_tmp, &h->d_stats};
     for (DBuf *b : bufs) dfree(*b);
-    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.slot_plo); dfree(kv.second.slot_phi); }
+    for (auto &kv : h->ptabs) dfree(kv.second.pieces);
     prof_resolve(h);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -582,6 +651,12 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
                                          "corrupt another ray's scratch); mesh ids must not decrease to 0");
         h->slot_run[slot] = (int32_t)r;   // a later run overwrites, as the sequential loop does
     }
+    {
+        std::vector<int32_t> live((size_t)K);
+        for (int32_t j = 0; j < K; ++j) live[(size_t)j] = h->slot_run[(size_t)j] >= 0;
+        RETIF(dalloc(h, h->d_live, (size_t)K * 4));
+        HIPCHK(h, hipMemcpy(h->d_live.p, live.data(), (size_t)K * 4, hipMemcpyHostToDevice));
+    }
     h->meas_meshes.clear();
     for (int32_t j = 0; j < K; ++j) if (mat_type[j] == 3) h->meas_meshes.push_back(j);
     // exact records and vertices
@@ -610,7 +685,6 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
             h->box_scale[k] = (std::isfinite(ext) && ext > 0.0f) ? 32.0f / ext : 1.0f;
         }
     }
-    h->ptabs.clear();   // piece tables depend on the scene
     h->dcap = 16.0;
     RETIF(build_records(h));
     RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
@@ -625,7 +699,7 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     HIPCHK(h, hipMemcpy(h->d_ior.p, ior, (size_t)K * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_refl.p, refl, (size_t)K * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_diss.p, diss, (size_t)K * 4, hipMemcpyHostToDevice));
-    h->ws_rays = 0; h->ws_part = 0;   // K may have changed
+    h->ws_rays = 0;   // K may have changed
     h->traced_ready = false;
     return 0;
 }
@@ -1102,6 +1176,11 @@ int lpc_prof_enable(lpc_handle *h, int on)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     h->prof = on != 0;
+    h->prof_stats = on >= 2;
+    if (h->prof_stats && !h->d_stats.p) {
+        RETIF(dalloc(h, h->d_stats, 64));
+        HIPCHK(h, hipMemset(h->d_stats.p, 0, 64));
+    }
     return 0;
 }
 
@@ -1114,7 +1193,16 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     out->shade_ms = h->prof_rest_ms;
     out->intersect_launches = h->prof_launches;
     out->pairs = h->prof_pairs;
-    if (reset) { h->prof_isect_ms = h->prof_rest_ms = 0.0; h->prof_launches = h->prof_pairs = 0; }
+    unsigned long long st[8] = {0};
+    if (h->d_stats.p) HIPCHK(h, hipMemcpy(st, h->d_stats.p, 64, hipMemcpyDeviceToHost));
+    out->node_visits = (int64_t)st[0];
+    out->group_tests = (int64_t)st[1];
+    out->wave_traversals = (int64_t)st[2];
+    out->exact_tests = (int64_t)st[3];
+    if (reset) {
+        h->prof_isect_ms = h->prof_rest_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
+        if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, 64));
+    }
     return 0;
 }
 

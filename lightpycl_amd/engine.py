@@ -214,11 +214,12 @@ class Engine:
         return (H, xe, ye) if not want_xy else (H, xe, ye, x, y, pc)
 
     # -- profiling -------------------------------------------------------------
-    def prof_enable(self, on=True):
-        self._c(self.L.lpc_prof_enable(self.h, 1 if on else 0))
+    def prof_enable(self, on=True, counters=False):
+        self._c(self.L.lpc_prof_enable(self.h, (2 if counters else 1) if on else 0))
 
     def prof_read(self, reset=True):
         p = _lib.Prof()
         self._c(self.L.lpc_prof_read(self.h, ctypes.byref(p), 1 if reset else 0))
         return dict(intersect_ms=p.intersect_ms, shade_ms=p.shade_ms,
-                    intersect_launches=p.intersect_launches, pairs=p.pairs)
+                    intersect_launches=p.intersect_launches, pairs=p.pairs, node_visits=p.node_visits,
+                    group_tests=p.group_tests, wave_traversals=p.wave_traversals, exact_tests=p.exact_tests)

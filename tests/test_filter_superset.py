@@ -151,3 +151,104 @@ def test_cluster_test_implied_by_member_tests(cluster_harness, name):
         assert not (tri_pass & ~(dc <= 0)).any()
         checked += int(tri_pass.sum())
     assert checked > 10000
+
+
+@pytest.fixture(scope="module")
+def sliver_harness(harness):
+    L = ctypes.CDLL(SO)
+    P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+    L.sliver_eval.argtypes = [ctypes.c_int, P, P, P, ctypes.c_float, ctypes.c_int, P, I, P]
+    L.sliver_eval.restype = None
+    L.filt_class.argtypes = [ctypes.c_int, P, ctypes.c_double, I]
+    L.filt_class.restype = None
+
+    def run(O, D, V, eps, fused):
+        n = O.shape[0]
+        d = np.zeros(n, np.float32)
+        h = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        L.sliver_eval(n, np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32),
+                      np.ascontiguousarray(V, np.float32), np.float32(eps), int(fused), d, h, t)
+        return d, h.astype(bool), t
+
+    def classify(V, dcap=16.0):
+        c = np.zeros(V.shape[0], np.int32)
+        L.filt_class(V.shape[0], np.ascontiguousarray(V, np.float32), dcap, c)
+        return c
+    run.classify = classify
+    return run
+
+
+def _scene_slivers(sliver_harness, name):
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    sc = scenes.BUILDERS[name](n=8, seed=1)
+    v0, v1, v2, *_ = flatten_meshes(sc.meshes)
+    V = np.concatenate([v0[:, :3], v1[:, :3], v2[:, :3]], 1).astype(np.float32)
+    return V[sliver_harness.classify(V) == 2]
+
+
+def _rays_at_lines(rng, V, n, dist):
+    """Rays aimed at points on (or 1e-7 relative off) the infinite line through V0
+    along E2 -- where Moller-Trumbore's rounding noise accepts pairs of a sliver."""
+    j = rng.integers(0, V.shape[0], n)
+    v0 = V[j, :3].astype(np.float64)
+    e2 = V[j, 6:9].astype(np.float64) - v0
+    s = rng.uniform(-3, 3, (n, 1))
+    tgt = v0 + s * e2 + rng.normal(size=(n, 3)) * 1e-7 * np.abs(V[j]).max(1, keepdims=True)
+    o = tgt + rng.normal(size=(n, 3)) * dist[:, None]
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o.astype(np.float32), d.astype(np.float32), V[j]
+
+
+@pytest.mark.parametrize("name", ["synthetic", "eye", "lens"])
+@pytest.mark.parametrize("fused", [0, 1])
+def test_sliver_line_filter_is_superset(sliver_harness, name, fused):
+    """Triangles whose sphere test degenerates (revolve_curve's pole slivers: two
+    vertices ~1e-11 apart) are tested with the line filter; every pair the exact test
+    accepts -- including rounding-noise accepts anywhere along the sliver's line --
+    must pass it."""
+    V = _scene_slivers(sliver_harness, name)
+    if V.shape[0] == 0:
+        pytest.skip("scene has no slivers")
+    rng = np.random.default_rng(11 + fused)
+    n = 400_000
+    dist = rng.choice([1e-2, 1.0, 30.0, 1e3], n)
+    O, D, Vj = _rays_at_lines(rng, V, n, dist)
+    d, hit, _ = sliver_harness(O, D, Vj, 1e-3, fused)
+    if name == "synthetic":
+        assert hit.sum() > 20                   # noise accepts do occur (r = 1000 pole slivers)
+    assert not (hit & ~(d <= 0)).any()
+    # random directions from the same origins: the line filter rejects nearly all
+    Dr = rng.normal(size=D.shape).astype(np.float32)
+    d2, hit2, _ = sliver_harness(O, Dr, Vj, 1e-3, fused)
+    assert not (hit2 & ~(d2 <= 0)).any()
+    assert (d2 <= 0).mean() < 0.05                # and the filter still rejects pairs
+
+
+def test_sliver_line_filter_synthetic_thin(sliver_harness):
+    """Random thin triangles (aspect 1e4 .. 1e12) that filter_record routes to the
+    sliver list; rays aimed along their lines and at their interiors."""
+    rng = np.random.default_rng(5)
+    m = 5000
+    v0 = rng.normal(size=(m, 3)) * 100
+    e = rng.normal(size=(m, 3))
+    e /= np.linalg.norm(e, axis=1, keepdims=True)
+    perp = np.cross(e, rng.normal(size=(m, 3)))
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True)
+    L = rng.uniform(0.1, 100, (m, 1))
+    h = L * 10.0 ** rng.uniform(-12, -4, (m, 1))
+    v1 = v0 + L * e
+    v2 = v0 + L * e * rng.uniform(0, 1, (m, 1)) + h * perp
+    V = np.concatenate([v0, v1, v2], 1).astype(np.float32)
+    V = V[sliver_harness.classify(V) == 2]
+    assert V.shape[0] > 1000
+    n = 400_000
+    dist = rng.choice([1e-1, 10.0, 1e3], n)
+    O, D, Vj = _rays_at_lines(rng, V, n, dist)
+    for fused in (0, 1):
+        d, hit, _ = sliver_harness(O, D, Vj, 1e-3, fused)
+        assert hit.sum() > 100
+        assert not (hit & ~(d <= 0)).any()

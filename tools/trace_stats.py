@@ -1,0 +1,38 @@
+"""GPU box: traversal statistics of k_intersect per bench iteration (diagnostic)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from lightpycl_amd import scenes  # noqa: E402
+from lightpycl_amd.engine import Engine  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "synthetic"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
+sc = scenes.BUILDERS[name](n=n, seed=7)
+e = Engine(0)
+e.upload_meshes(sc.meshes)
+o = np.asarray(sc.sources[0].rays_origin, np.float32)
+d = np.asarray(sc.sources[0].rays_dir, np.float32)
+p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
+e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+for counters in (False, True):
+    e.reset()
+    e.prof_enable(True, counters=counters)
+    e.prof_read(reset=True)
+    for it in range(sc.iterations):
+        nin = e.population()
+        t = time.perf_counter()
+        st, _ = e.iterate()
+        dt = time.perf_counter() - t
+        pr = e.prof_read(reset=True)
+        waves = max(pr["wave_traversals"], 1)
+        print(f"{name} it{it} rays {nin:8d} wall {dt*1e3:7.3f} ms  isect {pr['intersect_ms']:7.3f} ms "
+              f"rest {pr['shade_ms']:6.3f} ms  nodes/wave {pr['node_visits']/waves:7.1f} "
+              f"groups/wave {pr['group_tests']/waves:7.1f} exact/ray {pr['exact_tests']/max(nin,1):6.2f} "
+              f"traversals {pr['wave_traversals']}", flush=True)
+        if st.n_reflect + st.n_refract == 0:
+            break
+    print("counters" if counters else "timing only")
