@@ -168,6 +168,11 @@ typedef struct {
     int64_t group_tests;     /* 4-triangle filter groups tested (per wave)      */
     int64_t wave_traversals; /* (wave, piece) traversals                        */
     int64_t exact_tests;     /* exact Moller-Trumbore tests (per ray)           */
+    int64_t wave_hist[24];   /* k_intersect wave durations: bin b counts waves that
+                                ran [2^b, 2^(b+1)) wall-clock ticks (100 MHz)       */
+    int64_t heavy_piece;     /* piece with the largest summed wave time (last launch) */
+    int64_t heavy_piece_ticks;
+    int64_t piece_ticks;     /* summed wave ticks over all pieces (last launch)  */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * k_intersect traversal counters (2, diagnostic: adds atomics), or disable (0). */

@@ -31,7 +31,9 @@ class Prof(ctypes.Structure):
     _fields_ = [("intersect_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
                 ("intersect_launches", ctypes.c_int64), ("pairs", ctypes.c_int64),
                 ("node_visits", ctypes.c_int64), ("group_tests", ctypes.c_int64),
-                ("wave_traversals", ctypes.c_int64), ("exact_tests", ctypes.c_int64)]
+                ("wave_traversals", ctypes.c_int64), ("exact_tests", ctypes.c_int64),
+                ("wave_hist", ctypes.c_int64 * 24), ("heavy_piece", ctypes.c_int64),
+                ("heavy_piece_ticks", ctypes.c_int64), ("piece_ticks", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

@@ -5,10 +5,12 @@
 
 namespace lpck {
 
-struct Piece {                       // one subtree of a mesh run's hierarchy
-    int32_t root;                     // root node (-1: none)
-    int32_t s_lo, s_hi;               // sliver groups tested by this piece
+struct Piece {                       // part of one mesh run
+    int32_t root;                     // subtree root node (k_intersect)
+    int32_t s_lo, s_hi;               // sliver records [s_lo, s_hi) (k_slivers)
     int32_t slot;                     // per-mesh scratch slot the run flushes into
+    float cx, cy, cz, onemB, negA;    // the root's own test
+    int32_t pad[3];
 };
 
 // Per (slot, ray) nearest hit as one 64-bit key: order-preserving float bits of
@@ -27,6 +29,14 @@ __host__ __device__ inline float slot_key_t(unsigned long long k)
     return __builtin_bit_cast(float, u);
 }
 __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (int32_t)(uint32_t)k; }
+
+// Profiling counters (lpc_prof_enable(h, 2)): [0..3] traversal counters,
+// [HIST..HIST+24) k_intersect wave-duration histogram (log2 of 100 MHz ticks),
+// [PIECE..PIECE+PIECES) summed wave ticks per piece.
+#define LPC_STATS_HIST 8
+#define LPC_STATS_PIECE 32
+#define LPC_STATS_PIECES 4096
+#define LPC_STATS_WORDS (LPC_STATS_PIECE + LPC_STATS_PIECES)
 
 struct RaysIn {                       // a ray population (SoA)
     const float *ox, *oy, *oz, *dx, *dy, *dz, *pw;

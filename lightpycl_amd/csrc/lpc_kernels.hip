@@ -1,11 +1,11 @@
 // lpc_kernels.hip -- gfx950 kernels of the LightPyCL per-bounce path.
 //
-//   k_intersect      the hot loop: every ray against every triangle of one
-//                    "piece" (a slice of one mesh run).  Two rays per lane,
-//                    packed-FP32 bounding-sphere filter with the triangle record
-//                    broadcast from SGPRs (s_load), exact Moller-Trumbore only
-//                    for filter candidates -> per-piece (t_min, argmin, count).
-//                    Replaces __kernel intersect (.cl:243-289).
+//   k_packet         per-wave bound (origin ball + direction cone) of 128 rays.
+//   k_intersect      the hot loop (replaces __kernel intersect, .cl:243-289):
+//                    packet-culled cluster -> triangle traversal of one "piece"
+//                    (part of one mesh run), per-ray conservative sphere tests,
+//                    exact Moller-Trumbore only for candidates -> per-slot
+//                    nearest hit (64-bit atomicMin) and hit count.
 //   k_gather         rays into coherence order (after k_raykey + radix sort).
 //   k_slot_init/k_slot_export
 //                    per-mesh scratch slots (.cl:260-288): pieces flush their
@@ -34,47 +34,143 @@ namespace lpck {
 
 // ---------------------------------------------------------------------------
 // k_intersect
-// grid = (ceil(n/512), pieces), block = 256 = 4 waves; each wave traces 128
-// consecutive rays of the coherence order (perm, see k_raykey), two per lane as
-// packed FP32 pairs, through one piece = one subtree of a mesh run's 4-wide
-// sphere hierarchy.  The wave walks the hierarchy as a packet with a wave-uniform
-// stack in LDS: a child is visited when any of its 128 rays passes the child's
-// sphere test; leaves are filter groups of 4 triangles whose candidates get the
-// exact Moller-Trumbore test.
+// grid = (ceil(n/512), pieces), block = 256 = 4 waves; each wave traces a packet
+// of 128 consecutive rays of the coherence order (k_raykey + sort + k_gather), two
+// per lane as packed FP32 pairs, through one piece = a range of 64-triangle
+// clusters (and a share of the slivers) of one mesh run:
+//   1. lane-parallel packet tests (packet_sphere_test against the wave's
+//      PacketRec) of 64 cluster records at a time -> ballot;
+//   2. per passing cluster: per-ray cluster test (record broadcast by readlane),
+//      then lane-parallel packet tests of its 64 triangle records -> ballot;
+//   3. per passing triangle: per-ray sphere test, exact Moller-Trumbore for the
+//      candidates (mt_accumulate).
+// Slivers: lane-parallel packet_sliver_test, then the per-ray line filter.
+// Every level is implied by the one below it (tests/test_filter_superset.py), so
+// the exact test sees every pair it would accept: results are bit-exact.
+static __device__ __forceinline__ bool any_lane(bool b)
+{
+    return __builtin_amdgcn_ballot_w64(b) != 0;
+}
+static __device__ __forceinline__ float bcast(float v, int l)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+static __device__ __forceinline__ int bcasti(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+static __device__ __forceinline__ f2 sphere_test1(float cx, float cy, float cz, float onemB, float negA, f2 ox,
+                                                  f2 oy, f2 oz, f2 nx, f2 ny, f2 nz)
+{
+    const f2 wx = cx - ox, wy = cy - oy, wz = cz - oz;
+    const f2 ww = wx * wx + wy * wy + wz * wz;
+    const f2 wd = wx * nx + wy * ny + wz * nz;
+    const f2 tq = negA - wd * wd;
+    return ww * onemB + tq;
+}
+
+template <class T>
+static __device__ __forceinline__ T wave_red(T v, int op)   // 0 min, 1 max, 2 sum
+{
+    for (int o = 32; o >= 1; o >>= 1) {
+        const T u = __shfl_xor(v, o, 64);
+        v = op == 0 ? (u < v ? u : v) : op == 1 ? (u > v ? u : v) : v + u;
+    }
+    return v;
+}
+
+// Packet bound of each 128-ray wave (one wave per packet, same ray->lane map as
+// k_intersect).
+__global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                PacketRec *__restrict__ pk)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w * 128 >= n) return;
+    const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
+    const int64_t q[2] = {s0 < n ? s0 : n - 1, s1 < n ? s1 : n - 1};
+    float o[2][3], d[2][3];
+    for (int r = 0; r < 2; ++r) {
+        if (rs) {
+            for (int k = 0; k < 3; ++k) { o[r][k] = rs[k * n + q[r]]; d[r][k] = rs[(3 + k) * n + q[r]]; }
+        } else {
+            o[r][0] = R.ox[q[r]]; o[r][1] = R.oy[q[r]]; o[r][2] = R.oz[q[r]];
+            d[r][0] = R.dx[q[r]]; d[r][1] = R.dy[q[r]]; d[r][2] = R.dz[q[r]];
+        }
+    }
+    float mn[3], mx[3], nrm[2][3];
+    int fin = 1;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+    for (int k = 0; k < 3; ++k) { mn[k] = fminf(o[0][k], o[1][k]); mx[k] = fmaxf(o[0][k], o[1][k]); }
+    for (int r = 0; r < 2; ++r) {
+        const float l = sqrtf(d[r][0] * d[r][0] + d[r][1] * d[r][1] + d[r][2] * d[r][2]);
+        fin &= (l > 0.0f && l < INFINITY && fabsf(o[r][0] + o[r][1] + o[r][2]) < INFINITY) ? 1 : 0;
+        for (int k = 0; k < 3; ++k) nrm[r][k] = d[r][k] / l;
+        sx += nrm[r][0]; sy += nrm[r][1]; sz += nrm[r][2];
+    }
+    for (int k = 0; k < 3; ++k) { mn[k] = wave_red(mn[k], 0); mx[k] = wave_red(mx[k], 1); }
+    fin = wave_red(fin, 0);
+    sx = wave_red(sx, 2); sy = wave_red(sy, 2); sz = wave_red(sz, 2);
+    PacketRec Q;
+    packet_centre(mn, mx, Q);
+    float rr = 0.0f;
+    for (int r = 0; r < 2; ++r) {
+        const float x = o[r][0] - Q.ox, y = o[r][1] - Q.oy, z = o[r][2] - Q.oz;
+        rr = fmaxf(rr, sqrtf(x * x + y * y + z * z));
+    }
+    rr = wave_red(rr, 1);
+    packet_finish(rr, sx, sy, sz, Q);
+    float ang = fmaxf(packet_angle(nrm[0][0], nrm[0][1], nrm[0][2], Q.ax, Q.ay, Q.az),
+                      packet_angle(nrm[1][0], nrm[1][1], nrm[1][2], Q.ax, Q.ay, Q.az));
+    if (!(ang == ang)) ang = INFINITY;
+    ang = wave_red(ang, 1);
+    packet_angle_finish(ang, fin != 0, Q);
+    for (int k = 0; k < 5; ++k) Q.pad[k] = 0;
+    if (lane == 0) pk[w] = Q;
+}
+
+// Per-ray nearest-hit state and its flush into the run's slot (original ray
+// index q): only pieces with hits write; atomicMin on slot_key keeps the minimal
+// t and, among equal t, the lowest triangle index, so the flush order is free.
+static __device__ __forceinline__ void slot_flush(unsigned long long *skey, int32_t *scnt, int64_t o, int64_t q,
+                                                  float t, int32_t i, int32_t c)
+{
+    if (c) atomicAdd(&scnt[o + q], c);
+    if (i >= 0) atomicMin(&skey[o + q], slot_key(t, i));
+}
+
+static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__restrict__ rs, int64_t n, int64_t q,
+                                                f3 &O, f3 &D)
+{
+    if (rs) {
+        O = mk3(rs[q], rs[n + q], rs[2 * n + q]);
+        D = mk3(rs[3 * n + q], rs[4 * n + q], rs[5 * n + q]);
+    } else {
+        O = mk3(R.ox[q], R.oy[q], R.oz[q]);
+        D = mk3(R.dx[q], R.dy[q], R.dz[q]);
+    }
+}
+
+// Stack depth per wave (node refs); the host checks every hierarchy fits.
+#define LPC_STACK 32
+
 static __device__ __forceinline__ void sphere_test4(const float *cx, const float *cy, const float *cz,
                                                     const float *onemB, const float *negA, f2 ox, f2 oy,
                                                     f2 oz, f2 nx, f2 ny, f2 nz, f2 (&d)[4])
 {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const f2 wx = cx[k] - ox, wy = cy[k] - oy, wz = cz[k] - oz;
-        const f2 ww = wx * wx + wy * wy + wz * wz;
-        const f2 wd = wx * nx + wy * ny + wz * nz;
-        const f2 tq = negA[k] - wd * wd;          // one SGPR operand per packed FMA
-        d[k] = ww * onemB[k] + tq;
-    }
+    for (int k = 0; k < 4; ++k) d[k] = sphere_test1(cx[k], cy[k], cz[k], onemB[k], negA[k], ox, oy, oz, nx, ny, nz);
 }
 
-static __device__ __forceinline__ float min8(const f2 (&d)[4])
-{
-    return fminf(fminf(fminf(d[0].x, d[0].y), fminf(d[1].x, d[1].y)),
-                 fminf(fminf(d[2].x, d[2].y), fminf(d[3].x, d[3].y)));
-}
-
-// Stack depth per wave (node refs); the host checks every mesh's hierarchy fits.
-#define LPC_STACK 64
-
-static __device__ __forceinline__ bool any_lane(bool b)
-{
-    return __builtin_amdgcn_ballot_w64(b) != 0;
-}
-
+// k_intersect: packets of 128 rays of the coherence order (two per lane, packed
+// FP32 pairs), grid = (ceil(n/512), pieces), block = 4 waves.  A wave walks the
+// piece's subtree with a wave-uniform stack in LDS: a node's four children are
+// tested against all 128 rays (filter form d <= 0, see filter_record; node data
+// wave-uniform through the scalar cache); a child node is pushed when any ray
+// passes it, a child triangle gets the exact Moller-Trumbore test for the rays
+// that pass its own test.
 __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                    const int32_t *__restrict__ perm,
                                                    const Node4 *__restrict__ nodes,
-                                                   const FiltGroup *__restrict__ grp,
                                                    const ExactRec *__restrict__ xrec,
-                                                   const SliverGroup *__restrict__ srec,
                                                    const Piece *__restrict__ pieces, float eps,
                                                    float max_ray_len,
                                                    unsigned long long *__restrict__ skey,
@@ -83,129 +179,138 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
 {
     __shared__ int32_t stack[4][LPC_STACK];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int p = blockIdx.y;
-    // 128 consecutive rays (in coherence order) per wave, two per lane
-    const int64_t s0 = (int64_t)blockIdx.x * 512 + wv * 128 + lane;
-    const int64_t s1 = s0 + 64;
-    const int64_t q0s = s0 < n ? s0 : n - 1;
-    const int64_t q1s = s1 < n ? s1 : n - 1;
+    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+    if (w * 128 >= n) return;                      // whole wave past the end
+    const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
     f3 O0, O1, D0, D1;
-    if (rs) {            // rays already gathered into coherence order (k_gather)
-        O0 = mk3(rs[q0s], rs[n + q0s], rs[2 * n + q0s]);
-        O1 = mk3(rs[q1s], rs[n + q1s], rs[2 * n + q1s]);
-        D0 = mk3(rs[3 * n + q0s], rs[4 * n + q0s], rs[5 * n + q0s]);
-        D1 = mk3(rs[3 * n + q1s], rs[4 * n + q1s], rs[5 * n + q1s]);
-    } else {
-        O0 = mk3(R.ox[q0s], R.oy[q0s], R.oz[q0s]);
-        O1 = mk3(R.ox[q1s], R.oy[q1s], R.oz[q1s]);
-        D0 = mk3(R.dx[q0s], R.dy[q0s], R.dz[q0s]);
-        D1 = mk3(R.dx[q1s], R.dy[q1s], R.dz[q1s]);
-    }
+    load_ray(R, rs, n, s0 < n ? s0 : n - 1, O0, D0);
+    load_ray(R, rs, n, s1 < n ? s1 : n - 1, O1, D1);
     // unit direction for the filter only (its rounding is inside the margin)
     const float u0 = 1.0f / sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z);
     const float u1 = 1.0f / sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z);
     const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
     const f2 nx = {D0.x * u0, D1.x * u1}, ny = {D0.y * u0, D1.y * u1}, nz = {D0.z * u0, D1.z * u1};
+    const Piece P = pieces[blockIdx.y];
 
+    const uint64_t clk0 = stats ? wall_clock64() : 0;
     float t0 = max_ray_len, t1 = max_ray_len;
     int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
     int32_t *stk = stack[wv];
     int32_t top = 0;
-    uint32_t n_nodes = 0, n_groups = 0, n_exact = 0;   // profiling counters (stats != NULL)
-    const Piece P = pieces[p];
-    if (P.root >= 0) stk[top++] = P.root;          // the piece's subtree
+    uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
+    if (P.root >= 0) {
+        const f2 d = sphere_test1(P.cx, P.cy, P.cz, P.onemB, P.negA, ox, oy, oz, nx, ny, nz);
+        if (any_lane(d.x <= 0.0f || d.y <= 0.0f)) stk[top++] = P.root;
+    }
     while (top > 0) {
         const int32_t node = __builtin_amdgcn_readfirstlane(stk[--top]);
         const Node4 N = nodes[node];
         ++n_nodes;
-        f2 dn[4];
-        sphere_test4(N.cx, N.cy, N.cz, N.onemB, N.negA, ox, oy, oz, nx, ny, nz, dn);
+        f2 d[4];
+        sphere_test4(N.cx, N.cy, N.cz, N.onemB, N.negA, ox, oy, oz, nx, ny, nz, d);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (!any_lane(dn[k].x <= 0.0f || dn[k].y <= 0.0f)) continue;
+            const bool r0 = d[k].x <= 0.0f, r1 = d[k].y <= 0.0f;
+            if (!any_lane(r0 || r1)) continue;
             const int32_t ref = N.ref[k];
             if (ref >= 0) { stk[top++] = ref; continue; }
-            const FiltGroup G = grp[~ref];
-            ++n_groups;
-            f2 d[4];
-            sphere_test4(G.cx, G.cy, G.cz, G.onemB, G.negA, ox, oy, oz, nx, ny, nz, d);
-            if (min8(d) <= 0.0f) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (d[j].x <= 0.0f || d[j].y <= 0.0f) {
-                        const int32_t idx = G.idx[j];
-                        const ExactRec x = xrec[idx];
-                        const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
-                        const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
-                        const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
-                        if (d[j].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
-                        if (d[j].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
-                        n_exact += (d[j].x <= 0.0f) + (d[j].y <= 0.0f);
-                    }
-                }
-            }
-        }
-    }
-    // Slivers (line filter, see sliver_params): candidate iff
-    // (D.(E2 x T))^2 <= (|D| (a + b max|T_i|))^2; padding entries have a = NaN.
-    if (P.s_lo < P.s_hi) {
-        const f2 dx = {D0.x, D1.x}, dy = {D0.y, D1.y}, dz = {D0.z, D1.z};
-        const f2 dl = {sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z),
-                       sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z)};
-        for (int32_t sg = P.s_lo; sg < P.s_hi; ++sg) {
-            const SliverGroup G = srec[sg];
-            ++n_groups;
-            f2 d[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const f2 tx = ox - G.v0x[k], ty = oy - G.v0y[k], tz = oz - G.v0z[k];
-                const f2 cx = G.e2y[k] * tz - G.e2z[k] * ty;
-                const f2 cy = G.e2z[k] * tx - G.e2x[k] * tz;
-                const f2 cz = G.e2x[k] * ty - G.e2y[k] * tx;
-                const f2 x = dx * cx + dy * cy + dz * cz;
-                const f2 tm = {fmaxf(fmaxf(fabsf(tx.x), fabsf(ty.x)), fabsf(tz.x)),
-                               fmaxf(fmaxf(fabsf(tx.y), fabsf(ty.y)), fabsf(tz.y))};
-                const f2 rhs = dl * (G.a[k] + G.b[k] * tm);
-                d[k] = x * x - rhs * rhs;
-            }
-            if (min8(d) <= 0.0f) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int32_t idx = G.idx[j];
-                    if (idx >= 0 && (d[j].x <= 0.0f || d[j].y <= 0.0f)) {
-                        const ExactRec xr = xrec[idx];
-                        const f3 V0 = mk3(xr.v0x, xr.v0y, xr.v0z);
-                        const f3 E1 = mk3(xr.e1x, xr.e1y, xr.e1z);
-                        const f3 E2 = mk3(xr.e2x, xr.e2y, xr.e2z);
-                        if (d[j].x <= 0.0f) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
-                        if (d[j].y <= 0.0f) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
-                        n_exact += (d[j].x <= 0.0f) + (d[j].y <= 0.0f);
-                    }
-                }
-            }
+            const int32_t idx = ~ref;
+            const ExactRec x = xrec[idx];
+            const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
+            const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
+            const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
+            if (r0) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+            if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+            n_exact += (uint32_t)r0 + (uint32_t)r1;
         }
     }
     if (stats) {
         for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
         if (lane == 0) {
+            const uint64_t dt = wall_clock64() - clk0;
+            const int b = dt ? min(23, 63 - __builtin_clzll(dt)) : 0;
             atomicAdd(&stats[0], (unsigned long long)n_nodes);
-            atomicAdd(&stats[1], (unsigned long long)n_groups);
             atomicAdd(&stats[2], 1ull);
+            atomicAdd(&stats[3], (unsigned long long)n_exact);
+            atomicAdd(&stats[LPC_STATS_HIST + b], 1ull);
+            if (blockIdx.y < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + blockIdx.y], (unsigned long long)dt);
+        }
+    }
+    const int64_t o = (int64_t)P.slot * n;
+    if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
+    if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1);
+}
+
+// k_slivers: the run's slivers (line filter) for packets of 128 rays (two per
+// lane), grid = (ceil(n/512), sliver pieces of <= 64 slivers): lane-parallel
+// packet_sliver_test against the wave's PacketRec, then the per-ray line filter
+// and the exact test for the candidates.
+__global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                 const int32_t *__restrict__ perm,
+                                                 const PacketRec *__restrict__ pk,
+                                                 const SliverRec *__restrict__ srec,
+                                                 const Piece *__restrict__ pieces, float eps, float max_ray_len,
+                                                 unsigned long long *__restrict__ skey,
+                                                 int32_t *__restrict__ scnt,
+                                                 unsigned long long *__restrict__ stats)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w * 128 >= n) return;
+    const Piece P = pieces[blockIdx.y];
+    const PacketRec Q = pk[w];
+    const int32_t j = P.s_lo + lane;
+    SliverRec S;
+    if (j < P.s_hi) S = srec[j];
+    else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
+    uint64_t m = __builtin_amdgcn_ballot_w64(packet_sliver_test(Q, S));
+    if (!m) return;
+    const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
+    f3 O0, O1, D0, D1;
+    load_ray(R, rs, n, s0 < n ? s0 : n - 1, O0, D0);
+    load_ray(R, rs, n, s1 < n ? s1 : n - 1, O1, D1);
+    const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
+    const f2 dx = {D0.x, D1.x}, dy = {D0.y, D1.y}, dz = {D0.z, D1.z};
+    const f2 dl = {sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z), sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z)};
+    float t0 = max_ray_len, t1 = max_ray_len;
+    int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
+    uint32_t n_tests = 0, n_exact = 0;
+    while (m) {
+        const int k = __builtin_ctzll(m);
+        m &= m - 1;
+        const float v0x = bcast(S.v0x, k), v0y = bcast(S.v0y, k), v0z = bcast(S.v0z, k);
+        const float e2x = bcast(S.e2x, k), e2y = bcast(S.e2y, k), e2z = bcast(S.e2z, k);
+        const float sa = bcast(S.a, k), sbb = bcast(S.b, k);
+        const f2 tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
+        const f2 cx = e2y * tz - e2z * ty;
+        const f2 cy = e2z * tx - e2x * tz;
+        const f2 cz = e2x * ty - e2y * tx;
+        const f2 x = dx * cx + dy * cy + dz * cz;
+        const f2 tm = {fmaxf(fmaxf(fabsf(tx.x), fabsf(ty.x)), fabsf(tz.x)),
+                       fmaxf(fmaxf(fabsf(tx.y), fabsf(ty.y)), fabsf(tz.y))};
+        const f2 rhs = dl * (sa + sbb * tm);
+        const f2 d = x * x - rhs * rhs;
+        ++n_tests;
+        const bool r0 = d.x <= 0.0f, r1 = d.y <= 0.0f;
+        if (!any_lane(r0 || r1)) continue;
+        const int32_t idx = bcasti(S.idx, k);
+        const f3 V0 = mk3(v0x, v0y, v0z);
+        const f3 E1 = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
+        const f3 E2 = mk3(e2x, e2y, e2z);
+        if (r0) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+        if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+        n_exact += (uint32_t)r0 + (uint32_t)r1;
+    }
+    if (stats) {
+        for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
+        if (lane == 0) {
+            atomicAdd(&stats[1], (unsigned long long)n_tests);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
         }
     }
-    // flush into the run's slot (original ray index): only pieces with hits write
     const int64_t o = (int64_t)P.slot * n;
-    if (s0 < n) {
-        const int64_t q0 = perm ? perm[s0] : s0;
-        if (c0) atomicAdd(&scnt[o + q0], c0);
-        if (i0 >= 0) atomicMin(&skey[o + q0], slot_key(t0, i0));
-    }
-    if (s1 < n) {
-        const int64_t q1 = perm ? perm[s1] : s1;
-        if (c1) atomicAdd(&scnt[o + q1], c1);
-        if (i1 >= 0) atomicMin(&skey[o + q1], slot_key(t1, i1));
-    }
+    if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
+    if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1);
 }
 
 // Rays in coherence order, SoA [6][n] (ox oy oz dx dy dz), read coalesced by
@@ -612,14 +717,16 @@ __global__ __launch_bounds__(256) void k_project_hist(ProjArgs A)
 
 // Per-measure-mesh power of the measured record, one block per 64K records,
 // fixed-order sums (the host adds the block partials in order).
+// Deterministic float64 per-mesh power: fixed tiles, fixed reduction tree.
+#define LPC_MSUM_TILE 2048
 __global__ __launch_bounds__(256) void k_mesh_sum(int64_t n, const float *__restrict__ mp,
                                                   const int32_t *__restrict__ mm, int32_t mesh,
                                                   double *__restrict__ out)
 {
     __shared__ double s[4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t lo = (int64_t)blockIdx.x * 65536;
-    const int64_t hi = lo + 65536 < n ? lo + 65536 : n;
+    const int64_t lo = (int64_t)blockIdx.x * LPC_MSUM_TILE;
+    const int64_t hi = lo + LPC_MSUM_TILE < n ? lo + LPC_MSUM_TILE : n;
     double acc = 0.0;
     for (int64_t i = lo + threadIdx.x; i < hi; i += 256)
         if (mm[i] == mesh) acc += (double)mp[i];

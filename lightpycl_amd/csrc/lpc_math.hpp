@@ -287,33 +287,120 @@ struct FiltRec {
     int32_t pad0, pad1;
 };
 
-// Four filter records in SoA form: what one iteration of the hot loop reads
-// with a single 128-byte scalar load.
-struct FiltGroup {
-    float cx[4], cy[4], cz[4], onemB[4], negA[4];
-    int32_t idx[4];
-    int32_t pad[8];
-};
-
-// One node of the per-mesh sphere hierarchy: four child tests in SoA form.
-// ref[k] >= 0: child node index; ref[k] < 0: filter group ~ref[k] (4 triangles).
-// A child's test is implied by every test below it (cluster_record()), so a ray
-// that is a candidate for some triangle passes every node on the way down.
+// One node of a mesh run's 4-wide sphere hierarchy, children in SoA form.
+// ref[k] >= 0: child node; ref[k] < 0: triangle ~ref[k], whose test is the
+// triangle's own filter record.  A node's test (in its parent) is
+// cluster_record() of ALL triangles below it, so a ray that is a candidate for
+// some triangle passes every test on the way down.  Unused children: never.
 struct Node4 {
     float cx[4], cy[4], cz[4], onemB[4], negA[4];
     int32_t ref[4];
     int32_t pad[8];
 };
 
-// Four "slivers" in SoA form: triangles whose sphere test degenerates (B >= 0.5,
-// e.g. revolve_curve's pole triangles with two vertices 1e-11 apart).  For them
+// A "sliver": a triangle whose sphere test degenerates (B >= 0.5, e.g.
+// revolve_curve's pole triangles with two vertices 1e-11 apart).  For it
 // Moller-Trumbore is rounding noise that can accept rays anywhere along the line
-// through V0 with direction E2, so they get a line filter instead (sliver_params).
-struct SliverGroup {
-    float v0x[4], v0y[4], v0z[4], e2x[4], e2y[4], e2z[4], a[4], b[4];
-    int32_t idx[4];
-    int32_t pad[4];
+// through V0 with direction E2, so it gets a line filter instead (sliver_params).
+// Padding records have a = NaN (never pass).
+struct SliverRec {
+    float v0x, v0y, v0z, e2x, e2y, e2z, a, b;
+    int32_t idx;
+    float e1x, e1y, e1z;    // with v0, e2: the exact record (Moller-Trumbore input)
 };
+
+// Bound of one wave's packet of rays (k_packet): every origin lies within ro of
+// (ox,oy,oz) and every direction within angle th of the unit axis a.  all = 1
+// (incoherent packet, non-finite input) makes every packet test pass.
+struct PacketRec {
+    float ox, oy, oz, ro;
+    float ax, ay, az;
+    float th, sth, cth;
+    int32_t all;
+    int32_t pad[5];
+};
+
+// Packet test of a sphere record: false only if NO ray of the packet can pass the
+// per-ray float test d = ww (1-B) - A - wd^2 <= 0.  A passing ray satisfies
+// (exactly) dist(c, line)^2 <= A + (B + 32 eps) |w|^2 (see cluster_record), so the
+// angle psi between w = c - O and its line obeys sin^2 psi <= B' + A / |w|^2 =: sin^2 beta.
+// With W = c - o_c, L = |W|, |w| >= L - ro, angle(W, w) <= gamma = asin(ro / L) and
+// angle(line n, line a) <= th, the angle phi between W and the axis line obeys
+//     phi <= th + gamma + beta =: Sigma,
+// tested as |W x a| <= L sin(Sigma) (all angles in [0, pi/2]).  Float evaluation
+// error is covered by 1e-3 relative + 1e-6 absolute on sin(Sigma) and by passing
+// outright when a cosine would be computed with cancellation (sin > 0.99).
+LPC_HD bool packet_sphere_test(const PacketRec &Q, float cx, float cy, float cz, float onemB, float negA)
+{
+    if (Q.all) return true;
+    if (!(negA < INFINITY)) return false;                  // never record
+    const float A = -negA * 1.00001f;
+    const float B = (1.0f - onemB) + 4e-6f;
+    const float wx = cx - Q.ox, wy = cy - Q.oy, wz = cz - Q.oz;
+    const float L2 = wx * wx + wy * wy + wz * wz;
+    const float L = sqrtf(L2);
+    const float Lw = (L * 0.999999f - Q.ro * 1.000001f) * 0.999999f;   // <= |w| for every origin
+    if (!(Lw > 0.0f)) return true;
+    const float sg = (Q.ro / L) * 1.000002f;
+    if (!(sg < 0.99f)) return true;
+    const float s2 = B + A / (Lw * Lw);
+    if (!(s2 < 0.98f)) return true;
+    const float cg = sqrtf(1.0f - sg * sg), sb = sqrtf(s2), cb = sqrtf(1.0f - s2);
+    const float s1 = Q.sth * cg + Q.cth * sg, c1 = Q.cth * cg - Q.sth * sg;   // th + gamma
+    if (!(c1 > 0.15f)) return true;
+    const float sS = s1 * cb + c1 * sb, cS = c1 * cb - s1 * sb;               // + beta
+    if (!(cS > 0.15f)) return true;
+    const float px = wy * Q.az - wz * Q.ay, py = wz * Q.ax - wx * Q.az, pz = wx * Q.ay - wy * Q.ax;
+    const float cr2 = px * px + py * py + pz * pz;
+    const float sm = sS * 1.001f + 1e-6f;
+    return cr2 <= L2 * (sm * sm);
+}
+
+// Packet test of a sliver: a ray (origin O = o_c + delta, unit direction
+// n = a + nu, |delta| <= ro, |nu| <= th) passing the line filter has
+// |n.(E2 x T)| <= a_s + b_s |T| with T = O - V0 = Tc + delta, so
+//     |a.(E2 x Tc)| <= a_s + b_s (|Tc| + ro) + |E2| (ro + th (|Tc| + ro)).
+LPC_HD bool packet_sliver_test(const PacketRec &Q, const SliverRec &S)
+{
+    if (Q.all) return true;
+    if (!(S.a == S.a)) return false;                       // padding
+    const float tx = Q.ox - S.v0x, ty = Q.oy - S.v0y, tz = Q.oz - S.v0z;
+    const float tn = sqrtf(tx * tx + ty * ty + tz * tz);
+    const float e2n = sqrtf(S.e2x * S.e2x + S.e2y * S.e2y + S.e2z * S.e2z);
+    const float cx = S.e2y * tz - S.e2z * ty, cy = S.e2z * tx - S.e2x * tz, cz = S.e2x * ty - S.e2y * tx;
+    const float f = fabsf(Q.ax * cx + Q.ay * cy + Q.az * cz);
+    const float tr = (tn + Q.ro) * 1.000001f;
+    const float rhs = (S.a + S.b * tr) + e2n * (Q.ro + Q.th * tr);
+    return f <= rhs * 1.001f + 1e-6f * e2n * tn;
+}
+
+// Packet bound from its reductions (shared by k_packet and the tests): centre =
+// bbox centre of the origins; ro = max distance of an origin from it; axis =
+// normalised sum of the unit directions; th = max angle of a direction from it.
+LPC_HD void packet_centre(const float *mn, const float *mx, PacketRec &Q)
+{
+    Q.ox = 0.5f * (mn[0] + mx[0]);
+    Q.oy = 0.5f * (mn[1] + mx[1]);
+    Q.oz = 0.5f * (mn[2] + mx[2]);
+}
+LPC_HD float packet_angle(float nx, float ny, float nz, float ax, float ay, float az)
+{
+    const float px = ny * az - nz * ay, py = nz * ax - nx * az, pz = nx * ay - ny * ax;
+    return atan2f(sqrtf(px * px + py * py + pz * pz), nx * ax + ny * ay + nz * az);
+}
+LPC_HD void packet_finish(float rmax, float sx, float sy, float sz, PacketRec &Q)
+{
+    Q.ro = rmax * 1.00001f;
+    const float sl = sqrtf(sx * sx + sy * sy + sz * sz);
+    Q.ax = sx / sl; Q.ay = sy / sl; Q.az = sz / sl;
+}
+LPC_HD void packet_angle_finish(float angmax, bool finite, PacketRec &Q)
+{
+    Q.th = angmax * 1.00001f + 1e-6f;
+    Q.all = (!finite || !(Q.th < 1.2f) || !(Q.ro < INFINITY) || !(Q.ax == Q.ax)) ? 1 : 0;
+    Q.sth = sinf(Q.th);
+    Q.cth = cosf(Q.th);
+}
 
 struct ExactRec {       // V0, E1 = V1-V0, E2 = V2-V0 (float, exactly as the reference)
     float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, pad0, pad1, pad2;

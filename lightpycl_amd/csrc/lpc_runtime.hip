@@ -48,8 +48,8 @@ struct Pop {
 };
 
 struct PieceTable {
-    DBuf pieces;
-    int32_t npieces = 0;
+    DBuf pieces, spieces;              // hierarchy pieces (k_intersect), sliver pieces (k_slivers)
+    int32_t npieces = 0, nspieces = 0;
 };
 
 const int kShadeF = 12;   // float arrays of the shade outputs
@@ -67,15 +67,14 @@ struct lpc_handle {
     int32_t M = 0, K = 0, Mpad = 0;
     std::vector<float> hv0, hv1, hv2;               // host copies (record rebuilds)
     std::vector<int32_t> run_lo, run_hi;
-    std::vector<int32_t> run_root;                   // hierarchy root node per run (-1: none)
-    std::vector<std::vector<int32_t>> run_frontier;  // node lists by depth (piece split)
-    std::vector<int32_t> run_slo, run_shi;           // sliver groups per run
+    std::vector<std::vector<int32_t>> run_levels;    // per run: (first node, count) per level, root first
+    std::vector<FiltRec> node_self;                  // each node's own test (piece roots)
+    std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
     std::vector<int32_t> slot_run;
     std::vector<int32_t> meas_meshes;
-    DBuf d_frec, d_crec, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
-    std::vector<Node4> hnodes;                       // host copy of the hierarchy
+    DBuf d_nodes, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
     double dcap = 16.0;
     std::map<int32_t, PieceTable> ptabs;
     // workspace
@@ -84,6 +83,7 @@ struct lpc_handle {
     DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf d_live;                                    // [K] slot written by some run
+    DBuf w_pk;                                      // PacketRec per 128-ray wave
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
     // trace
@@ -175,12 +175,13 @@ static inline uint64_t spread21(uint64_t x)
     return x;
 }
 
-// Per mesh run: filter groups of 4 triangles in Morton order of the centroids,
-// and a 4-wide hierarchy built bottom-up over them (every entry's test is a
-// cluster_record() of the triangles below it).  Triangles whose sphere test is
-// degenerate ("always", B >= 0.5) go to the run's sliver list (line filter,
-// sliver_params) instead; triangles that can never be hit are dropped.  Results
-// do not depend on the order (ties are resolved by triangle index).
+// Per mesh run: a 4-wide sphere hierarchy built bottom-up over its triangles in
+// Morton order of the centroids (bottom nodes hold up to 4 triangles); every
+// node's test is cluster_record() of ALL triangles below it, so the slack does
+// not compound from level to level.  Triangles whose sphere test is degenerate
+// ("always", B >= 0.5) go to the run's sliver list (line filter, sliver_params)
+// instead; triangles that can never be hit are dropped.  Results do not depend
+// on the order (ties are resolved by triangle index).
 static FiltRec test_rec(float cx, float cy, float cz, float onemB, float negA)
 {
     FiltRec r;
@@ -190,21 +191,18 @@ static FiltRec test_rec(float cx, float cy, float cz, float onemB, float negA)
 
 static void drop_piece_tables(lpc_handle *h)
 {
-    for (auto &kv : h->ptabs) dfree(kv.second.pieces);
+    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
     h->ptabs.clear();
 }
 
 static int build_records(lpc_handle *h)
 {
-    drop_piece_tables(h);   // pieces are subtrees of the hierarchy built here
-    std::vector<FiltGroup> groups;
-    std::vector<SliverGroup> slivers;
-    std::vector<Node4> &nodes = h->hnodes;
-    nodes.clear();
-    h->run_root.clear();
-    h->run_frontier.clear();
-    h->run_slo.clear();
-    h->run_shi.clear();
+    drop_piece_tables(h);   // pieces index the records built here
+    std::vector<Node4> nodes;
+    std::vector<SliverRec> slivers;
+    h->run_levels.clear();
+    h->node_self.clear();
+    h->run_slo.clear(); h->run_shi.clear();
     h->n_slivers = 0;
     const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 1.0f, INFINITY);
     for (size_t r = 0; r < h->run_lo.size(); ++r) {
@@ -225,28 +223,24 @@ static int build_records(lpc_handle *h)
                 if (std::isfinite(c)) { bl[k] = std::min(bl[k], c); bh[k] = std::max(bh[k], c); }
             }
         }
-        // slivers: SoA groups of 4 (padding entries never pass: a = NaN)
         h->run_slo.push_back((int32_t)slivers.size());
-        for (size_t a = 0; a < sl.size(); a += 4) {
-            SliverGroup G;
-            memset(&G, 0, sizeof(G));
-            for (int k = 0; k < 4; ++k) {
-                G.idx[k] = -1; G.a[k] = NAN; G.b[k] = 0.0f;
-                if (a + k >= sl.size()) continue;
-                const size_t t = (size_t)sl[a + k];
-                const float *V0 = &h->hv0[4 * t], *V1 = &h->hv1[4 * t], *V2 = &h->hv2[4 * t];
-                G.v0x[k] = V0[0]; G.v0y[k] = V0[1]; G.v0z[k] = V0[2];
-                G.e2x[k] = V2[0] - V0[0]; G.e2y[k] = V2[1] - V0[1]; G.e2z[k] = V2[2] - V0[2];
-                sliver_params(V0, V1, V2, &G.a[k], &G.b[k]);
-                G.idx[k] = (int32_t)t;
-            }
-            slivers.push_back(G);
+        for (int32_t t32 : sl) {
+            const size_t t = (size_t)t32;
+            const float *V0 = &h->hv0[4 * t], *V1 = &h->hv1[4 * t], *V2 = &h->hv2[4 * t];
+            SliverRec S;
+            memset(&S, 0, sizeof(S));
+            S.v0x = V0[0]; S.v0y = V0[1]; S.v0z = V0[2];
+            S.e2x = V2[0] - V0[0]; S.e2y = V2[1] - V0[1]; S.e2z = V2[2] - V0[2];
+            sliver_params(V0, V1, V2, &S.a, &S.b);
+            S.e1x = V1[0] - V0[0]; S.e1y = V1[1] - V0[1]; S.e1z = V1[2] - V0[2];
+            S.idx = t32;
+            slivers.push_back(S);
         }
         h->run_shi.push_back((int32_t)slivers.size());
         h->n_slivers += (int64_t)sl.size();
-        h->run_frontier.push_back(std::vector<int32_t>());
+        h->run_levels.push_back(std::vector<int32_t>());
         const int32_t cnt = (int32_t)fr.size();
-        if (cnt == 0) { h->run_root.push_back(-1); continue; }
+        if (cnt == 0) continue;
         std::vector<std::pair<uint64_t, int32_t>> key((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) {
             uint64_t q[3];
@@ -260,127 +254,123 @@ static int build_records(lpc_handle *h)
         std::sort(key.begin(), key.end());
         std::vector<FiltRec> ord((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)key[(size_t)i].second];
-        // Every entry (a filter group or a node) covers a contiguous range of `ord`;
-        // its test is cluster_record() of the TRIANGLES in that range (not of the
-        // child tests), so the slack does not compound from level to level.
+        // every entry covers a contiguous range of `ord`; its test is
+        // cluster_record() of the triangles in that range
         auto range_test = [&](int32_t a, int32_t b) {
             FiltRec t = never;
             cluster_record(&ord[(size_t)a], b - a, &t.cx, &t.cy, &t.cz, &t.onemB, &t.negA);
             return t;
         };
         struct Ent { FiltRec t; int32_t ref, a, b; };
-        std::vector<Ent> ent;
-        for (int32_t a = 0; a < cnt; a += 4) {
-            FiltGroup G;
-            memset(&G, 0, sizeof(G));
-            const int32_t b = std::min(a + 4, cnt);
-            for (int k = 0; k < 4; ++k) {
-                const FiltRec &m = (a + k < cnt) ? ord[(size_t)(a + k)] : never;
-                G.cx[k] = m.cx; G.cy[k] = m.cy; G.cz[k] = m.cz;
-                G.onemB[k] = m.onemB; G.negA[k] = m.negA; G.idx[k] = m.idx;
-            }
-            ent.push_back({range_test(a, b), ~(int32_t)groups.size(), a, b});
-            groups.push_back(G);
-        }
-        // internal levels, fan-out 4, until one node remains
-        std::vector<std::vector<int32_t>> levels;
-        for (;;) {
+        std::vector<Ent> ent((size_t)cnt);
+        for (int32_t a = 0; a < cnt; ++a) ent[(size_t)a] = {ord[(size_t)a], ~ord[(size_t)a].idx, a, a + 1};
+        std::vector<std::pair<int32_t, int32_t>> levels;   // (first node, count), bottom up
+        do {
             std::vector<Ent> up;
-            std::vector<int32_t> lvl;
+            const int32_t first = (int32_t)nodes.size();
             for (size_t i = 0; i < ent.size(); i += 4) {
                 Node4 N;
                 memset(&N, 0, sizeof(N));
                 for (int k = 0; k < 4; ++k) {
-                    const bool live = i + k < ent.size();
-                    const FiltRec &m = live ? ent[i + k].t : never;
+                    const bool use = i + k < ent.size();
+                    const FiltRec &m = use ? ent[i + k].t : never;
                     N.cx[k] = m.cx; N.cy[k] = m.cy; N.cz[k] = m.cz;
                     N.onemB[k] = m.onemB; N.negA[k] = m.negA;
-                    N.ref[k] = live ? ent[i + k].ref : ~0;
+                    N.ref[k] = use ? ent[i + k].ref : ~0;
                 }
                 const int32_t a = ent[i].a, b = ent[std::min(i + 3, ent.size() - 1)].b;
-                up.push_back({range_test(a, b), (int32_t)nodes.size(), a, b});
-                lvl.push_back((int32_t)nodes.size());
+                const FiltRec self = range_test(a, b);
+                up.push_back({self, (int32_t)nodes.size(), a, b});
                 nodes.push_back(N);
+                h->node_self.push_back(self);
             }
-            levels.push_back(lvl);
+            levels.push_back({first, (int32_t)up.size()});
             ent.swap(up);
-            if (ent.size() == 1) break;
-        }
-        if (levels.size() > 20) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
-        h->run_root.push_back(ent[0].ref);
-        // frontier lists from the root down (for splitting a run into pieces)
+        } while (ent.size() > 1);
+        // 4-wide: at most 3 siblings wait per level on a wave's stack
+        if (3 * (int)levels.size() + 1 > LPC_STACK) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
         for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
-            h->run_frontier.back().push_back((int32_t)it->front());   // first node index of the level
-            h->run_frontier.back().push_back((int32_t)it->size());     // node count of the level
+            h->run_levels.back().push_back(it->first);
+            h->run_levels.back().push_back(it->second);
         }
     }
+    if ((int64_t)nodes.size() > INT32_MAX / 2) return set_err(h, LPC_E_ARG, "too many triangles");
     // spare records so no buffer is empty
-    FiltGroup sg;
-    memset(&sg, 0, sizeof(sg));
-    for (int k = 0; k < 4; ++k) { sg.onemB[k] = 1.0f; sg.negA[k] = INFINITY; sg.idx[k] = -1; }
-    groups.push_back(sg);
-    SliverGroup ss;
-    memset(&ss, 0, sizeof(ss));
-    for (int k = 0; k < 4; ++k) { ss.a[k] = NAN; ss.idx[k] = -1; }
-    slivers.push_back(ss);
     if (nodes.empty()) { Node4 N; memset(&N, 0, sizeof(N)); nodes.push_back(N); }
-    h->Mpad = (int32_t)(groups.size() - 1) * 4;
-    RETIF(dalloc(h, h->d_frec, groups.size() * sizeof(FiltGroup)));
-    RETIF(dalloc(h, h->d_crec, nodes.size() * sizeof(Node4)));
-    RETIF(dalloc(h, h->d_srec, slivers.size() * sizeof(SliverGroup)));
-    HIPCHK(h, hipMemcpy(h->d_frec.p, groups.data(), groups.size() * sizeof(FiltGroup), hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->d_crec.p, nodes.data(), nodes.size() * sizeof(Node4), hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->d_srec.p, slivers.data(), slivers.size() * sizeof(SliverGroup),
+    if (slivers.empty()) {
+        SliverRec ss;
+        memset(&ss, 0, sizeof(ss));
+        ss.a = NAN; ss.idx = -1;
+        slivers.push_back(ss);
+    }
+    h->Mpad = (int32_t)nodes.size();
+    RETIF(dalloc(h, h->d_nodes, nodes.size() * sizeof(Node4)));
+    RETIF(dalloc(h, h->d_srec, slivers.size() * sizeof(SliverRec)));
+    HIPCHK(h, hipMemcpy(h->d_nodes.p, nodes.data(), nodes.size() * sizeof(Node4), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_srec.p, slivers.data(), slivers.size() * sizeof(SliverRec),
                         hipMemcpyHostToDevice));
     return 0;
 }
 
-// Piece table for a launch of n rays: pieces = subtrees of the runs that own a
-// slot (a run whose slot a later run overwrites is skipped, as its results are),
-// each run split at the shallowest hierarchy level with >= g nodes so that
-// blocks_x * pieces fills the GPU.
+// Piece table for a launch of n rays.  Hierarchy pieces = subtrees of the runs
+// that own a slot (a run whose slot a later run overwrites is skipped, as its
+// results are): each run's root, or all nodes of the shallowest level with >= g
+// nodes, g chosen so that blocks_x * pieces fills the GPU.  Sliver pieces = the
+// runs' slivers in blocks of <= 64 (one lane each).
 static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
 {
     const int64_t bx = std::max<int64_t>(1, (n + 511) / 512);
-    std::vector<int32_t> run_slot(h->run_root.size(), -1);
+    const size_t nr = h->run_levels.size();
+    std::vector<int32_t> run_slot(nr, -1);
     for (int32_t j = 0; j < h->K; ++j)
         if (h->slot_run[(size_t)j] >= 0) run_slot[(size_t)h->slot_run[(size_t)j]] = j;
     int64_t live_runs = 0;
     for (int32_t v : run_slot) live_runs += v >= 0;
+    live_runs = std::max<int64_t>(live_runs, 1);
     const int64_t target_blocks = 8192;
-    int32_t g = (int32_t)std::max<int64_t>(1, (target_blocks + bx * std::max<int64_t>(live_runs, 1) - 1) /
-                                                  (bx * std::max<int64_t>(live_runs, 1)));
-    g = std::min<int32_t>(g, 4096);
+    int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (target_blocks + bx * live_runs - 1) /
+                                                                          (bx * live_runs)));
     auto it = h->ptabs.find(g);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
-    std::vector<Piece> pcs;
-    for (size_t r = 0; r < h->run_root.size(); ++r) {
+    std::vector<Piece> pcs, spc;
+    for (size_t r = 0; r < nr; ++r) {
         if (run_slot[r] < 0) continue;
-        const std::vector<int32_t> &L = h->run_frontier[r];   // (first, count) per level, root first
-        std::vector<int32_t> roots;
+        const std::vector<int32_t> &L = h->run_levels[r];
         if (!L.empty()) {
             size_t lv = 0;
             while (lv + 1 < L.size() / 2 && L[2 * lv + 1] < g) ++lv;
-            for (int32_t i = 0; i < L[2 * lv + 1]; ++i) roots.push_back(L[2 * lv] + i);
+            for (int32_t i = 0; i < L[2 * lv + 1]; ++i) {
+                Piece p;
+                memset(&p, 0, sizeof(p));
+                p.root = L[2 * lv] + i;
+                const FiltRec &t = h->node_self[(size_t)p.root];
+                p.cx = t.cx; p.cy = t.cy; p.cz = t.cz; p.onemB = t.onemB; p.negA = t.negA;
+                p.s_lo = p.s_hi = 0;
+                p.slot = run_slot[r];
+                pcs.push_back(p);
+            }
         }
-        // the run's sliver groups are shared out over its pieces
-        const int32_t slo = h->run_slo[r], ns = h->run_shi[r] - slo;
-        const int32_t np = std::max<int32_t>((int32_t)roots.size(), std::min<int32_t>(ns, std::max(g, 1)));
-        for (int32_t i = 0; i < np; ++i) {
+        for (int32_t a = h->run_slo[r]; a < h->run_shi[r]; a += 64) {
             Piece p;
-            p.root = i < (int32_t)roots.size() ? roots[(size_t)i] : -1;
-            p.s_lo = slo + (int32_t)((int64_t)ns * i / np);
-            p.s_hi = slo + (int32_t)((int64_t)ns * (i + 1) / np);
+            memset(&p, 0, sizeof(p));
+            p.root = -1;
+            p.s_lo = a;
+            p.s_hi = std::min(a + 64, h->run_shi[r]);
             p.slot = run_slot[r];
-            pcs.push_back(p);
+            spc.push_back(p);
         }
     }
-    if (pcs.size() > 65535) return set_err(h, LPC_E_ARG, "too many triangle pieces");
+    if (pcs.size() > 65535 || spc.size() > 65535) return set_err(h, LPC_E_ARG, "too many triangle pieces");
     PieceTable &t = h->ptabs[g];
     t.npieces = (int32_t)pcs.size();
+    t.nspieces = (int32_t)spc.size();
     if (!pcs.empty()) {
         RETIF(dalloc(h, t.pieces, pcs.size() * sizeof(Piece)));
         HIPCHK(h, hipMemcpy(t.pieces.p, pcs.data(), pcs.size() * sizeof(Piece), hipMemcpyHostToDevice));
+    }
+    if (!spc.empty()) {
+        RETIF(dalloc(h, t.spieces, spc.size() * sizeof(Piece)));
+        HIPCHK(h, hipMemcpy(t.spieces.p, spc.data(), spc.size() * sizeof(Piece), hipMemcpyHostToDevice));
     }
     *out = &t;
     return 0;
@@ -400,6 +390,7 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_key, (size_t)h->K * C * 8));
         RETIF(dalloc(h, h->w_sc, (size_t)h->K * C * 4));
         RETIF(dalloc(h, h->w_rs, (size_t)6 * C * 4));
+        RETIF(dalloc(h, h->w_pk, (size_t)((C + 127) / 128) * sizeof(PacketRec)));
         RETIF(dalloc(h, h->w_shf, (size_t)kShadeF * C * 4));
         RETIF(dalloc(h, h->w_shi, (size_t)kShadeI * C * 4));
         const int64_t nb = (C + 1023) / 1024;
@@ -495,22 +486,29 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
         rs = (const float *)h->w_rs.p;
     }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     if (pt->npieces > 0) {
-        dim3 grid((unsigned)((n + 511) / 512), (unsigned)pt->npieces);
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-        hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, rs, n, perm,
-                           (const Node4 *)h->d_crec.p, (const FiltGroup *)h->d_frec.p,
-                           (const ExactRec *)h->d_xrec.p, (const SliverGroup *)h->d_srec.p,
+        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + 511) / 512), (unsigned)pt->npieces), dim3(256), 0,
+                           h->stream, in, rs, n, perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
                            (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt,
                            h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr);
         HIPCHK(h, hipGetLastError());
-        if (h->prof) {
-            (void)hipEventRecord(e1, h->stream);
-            h->ev_isect.push_back({e0, e1});
-            h->prof_launches += 1;
-            h->prof_pairs += n * (int64_t)h->M;
-        }
+    }
+    if (pt->nspieces > 0) {
+        hipLaunchKernelGGL(k_packet, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, h->stream, in, rs, n,
+                           (PacketRec *)h->w_pk.p);
+        hipLaunchKernelGGL(k_slivers, dim3((unsigned)((n + 511) / 512), (unsigned)pt->nspieces), dim3(256), 0,
+                           h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p, (const SliverRec *)h->d_srec.p,
+                           (const Piece *)pt->spieces.p, eps, max_ray_len, skey, scnt,
+                           h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr);
+        HIPCHK(h, hipGetLastError());
+    }
+    if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
+        (void)hipEventRecord(e1, h->stream);
+        h->ev_isect.push_back({e0, e1});
+        h->prof_launches += 1;
+        h->prof_pairs += n * (int64_t)h->M;
     }
     if (st_user) {
         hipLaunchKernelGGL(k_slot_export, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
@@ -593,13 +591,13 @@ int lpc_close(lpc_handle *h)
     if (!h) return 0;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    DBuf *bufs[] = {&h->d_frec, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
+    DBuf *bufs[] = {&h->d_nodes, &h->w_pk, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
-                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_crec, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
+                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats};
     for (DBuf *b : bufs) dfree(*b);
-    for (auto &kv : h->ptabs) dfree(kv.second.pieces);
+    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
     prof_resolve(h);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1064,7 +1062,7 @@ static int mesh_power(lpc_handle *h, double *out)
 {
     for (int32_t j = 0; j < h->K; ++j) out[j] = 0.0;
     if (h->m_total == 0) return 0;
-    const int64_t nb = (h->m_total + 65535) / 65536;
+    const int64_t nb = (h->m_total + LPC_MSUM_TILE - 1) / LPC_MSUM_TILE;
     RETIF(dalloc(h, h->d_tmp, (size_t)nb * 8));
     std::vector<double> part((size_t)nb);
     const size_t mc = (size_t)h->m_cap;
@@ -1178,8 +1176,8 @@ int lpc_prof_enable(lpc_handle *h, int on)
     h->prof = on != 0;
     h->prof_stats = on >= 2;
     if (h->prof_stats && !h->d_stats.p) {
-        RETIF(dalloc(h, h->d_stats, 64));
-        HIPCHK(h, hipMemset(h->d_stats.p, 0, 64));
+        RETIF(dalloc(h, h->d_stats, LPC_STATS_WORDS * 8));
+        HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
     }
     return 0;
 }
@@ -1193,15 +1191,22 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     out->shade_ms = h->prof_rest_ms;
     out->intersect_launches = h->prof_launches;
     out->pairs = h->prof_pairs;
-    unsigned long long st[8] = {0};
-    if (h->d_stats.p) HIPCHK(h, hipMemcpy(st, h->d_stats.p, 64, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> st(LPC_STATS_WORDS, 0ull);
+    if (h->d_stats.p) HIPCHK(h, hipMemcpy(st.data(), h->d_stats.p, LPC_STATS_WORDS * 8, hipMemcpyDeviceToHost));
     out->node_visits = (int64_t)st[0];
     out->group_tests = (int64_t)st[1];
     out->wave_traversals = (int64_t)st[2];
     out->exact_tests = (int64_t)st[3];
+    for (int b = 0; b < 24; ++b) out->wave_hist[b] = (int64_t)st[LPC_STATS_HIST + b];
+    out->heavy_piece = -1; out->heavy_piece_ticks = 0; out->piece_ticks = 0;
+    for (int p = 0; p < LPC_STATS_PIECES; ++p) {
+        const int64_t v = (int64_t)st[LPC_STATS_PIECE + p];
+        out->piece_ticks += v;
+        if (v > out->heavy_piece_ticks) { out->heavy_piece_ticks = v; out->heavy_piece = p; }
+    }
     if (reset) {
         h->prof_isect_ms = h->prof_rest_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
-        if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, 64));
+        if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
     }
     return 0;
 }

@@ -222,4 +222,6 @@ class Engine:
         self._c(self.L.lpc_prof_read(self.h, ctypes.byref(p), 1 if reset else 0))
         return dict(intersect_ms=p.intersect_ms, shade_ms=p.shade_ms,
                     intersect_launches=p.intersect_launches, pairs=p.pairs, node_visits=p.node_visits,
-                    group_tests=p.group_tests, wave_traversals=p.wave_traversals, exact_tests=p.exact_tests)
+                    group_tests=p.group_tests, wave_traversals=p.wave_traversals, exact_tests=p.exact_tests,
+                    wave_hist=list(p.wave_hist), heavy_piece=p.heavy_piece, heavy_piece_ticks=p.heavy_piece_ticks,
+                    piece_ticks=p.piece_ticks)

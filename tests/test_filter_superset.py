@@ -252,3 +252,75 @@ def test_sliver_line_filter_synthetic_thin(sliver_harness):
         d, hit, _ = sliver_harness(O, D, Vj, 1e-3, fused)
         assert hit.sum() > 100
         assert not (hit & ~(d <= 0)).any()
+
+
+@pytest.fixture(scope="module")
+def packet_harness(harness):
+    L = ctypes.CDLL(SO)
+    P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    Q = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+    L.packet_eval.argtypes = [ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_double, Q]
+    L.packet_eval.restype = None
+
+    def run(O, D, V, kind, pk=128, dcap=16.0):
+        out = np.zeros(4, np.int64)
+        L.packet_eval(O.shape[0], np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32), pk,
+                      V.shape[0], np.ascontiguousarray(V, np.float32), kind, dcap, out)
+        return dict(violations=int(out[0]), packet_pass=int(out[1]), ray_pass=int(out[2]), incoherent=int(out[3]))
+    return run
+
+
+def _packets(rng, V, npk, ball, dist, spread, line=False):
+    """npk packets of 128 rays: origins in a ball of radius `ball` around a point at
+    ~`dist` from a target triangle (or sliver line), directions toward points on /
+    near it with angular jitter `spread`."""
+    O, D = [], []
+    for _ in range(npk):
+        j = rng.integers(0, V.shape[0])
+        v0, v1, v2 = (V[j, 3 * k:3 * k + 3].astype(np.float64) for k in range(3))
+        if line:
+            tgt = v0 + rng.uniform(-3, 3, (128, 1)) * (v2 - v0)
+        else:
+            bu, bv = rng.random((2, 128, 1))
+            f = bu + bv > 1
+            bu[f], bv[f] = 1 - bu[f], 1 - bv[f]
+            tgt = v0 + bu * (v1 - v0) + bv * (v2 - v0)
+        c = tgt.mean(0) + rng.normal(size=3) * dist
+        o = c + rng.normal(size=(128, 3)) * ball
+        d = tgt - o
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        d += rng.normal(size=d.shape) * spread
+        O.append(o)
+        D.append(d)
+    return np.concatenate(O).astype(np.float32), np.concatenate(D).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["lens", "synthetic", "eye"])
+@pytest.mark.parametrize("ball,dist,spread", [(0.0, 100.0, 1e-3), (1e-3, 30.0, 1e-2), (1.0, 10.0, 0.05),
+                                              (30.0, 500.0, 1e-4), (0.0, 1e3, 0.0), (5.0, 2.0, 0.3)])
+def test_packet_tests_are_sound(packet_harness, sliver_harness, name, ball, dist, spread):
+    """k_intersect skips a cluster / triangle / sliver for a whole wave when the
+    packet bound of its 128 rays (origin ball + direction cone, k_packet) fails the
+    record's packet test; that must never happen while some ray of the packet passes
+    the record's per-ray test."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    sc = scenes.BUILDERS[name](n=8, seed=1)
+    v0, v1, v2, *_ = flatten_meshes(sc.meshes)
+    V = np.concatenate([v0[:, :3], v1[:, :3], v2[:, :3]], 1).astype(np.float32)
+    cls = sliver_harness.classify(V)
+    rng = np.random.default_rng(int(ball * 7 + dist + spread * 1000))
+    start = rng.integers(0, max(1, V.shape[0] - 4096))
+    Vn = V[start:start + 4096][cls[start:start + 4096] == 0]
+    O, D = _packets(rng, Vn, 60, ball, dist, spread)
+    for kind in (0, 1):
+        r = packet_harness(O, D, Vn, kind)
+        assert r["violations"] == 0, r
+        assert r["ray_pass"] > 0
+        if kind == 0 and ball <= 1e-3:                 # the packet test does cull
+            assert r["packet_pass"] < max(2 * r["ray_pass"], 0.5 * len(Vn) * 60), r
+    Vs = V[cls == 2]
+    if len(Vs):
+        O, D = _packets(rng, Vs, 60, ball, dist, spread, line=True)
+        r = packet_harness(O, D, Vs, 2)
+        assert r["violations"] == 0, r

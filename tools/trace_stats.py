@@ -30,9 +30,16 @@ for counters in (False, True):
         pr = e.prof_read(reset=True)
         waves = max(pr["wave_traversals"], 1)
         print(f"{name} it{it} rays {nin:8d} wall {dt*1e3:7.3f} ms  isect {pr['intersect_ms']:7.3f} ms "
-              f"rest {pr['shade_ms']:6.3f} ms  nodes/wave {pr['node_visits']/waves:7.1f} "
-              f"groups/wave {pr['group_tests']/waves:7.1f} exact/ray {pr['exact_tests']/max(nin,1):6.2f} "
-              f"traversals {pr['wave_traversals']}", flush=True)
+              f"rest {pr['shade_ms']:6.3f} ms  nodes/traversal {pr['node_visits']/max(pr['wave_traversals'],1):7.1f} "
+              f"sliver tests/packet {pr['group_tests']/max(nin/128,1):7.1f} exact/ray {pr['exact_tests']/max(nin,1):6.2f} "
+              f"waves {pr['wave_traversals']}", flush=True)
+        if counters:
+            h = pr["wave_hist"]
+            nz = [(b, c) for b, c in enumerate(h) if c]
+            print("    wave time histogram (us >= : waves): " +
+                  ", ".join(f"{(1 << b) / 100:.2f}: {c}" for b, c in nz) +
+                  f"  | heaviest piece {pr['heavy_piece']} = "
+                  f"{100.0 * pr['heavy_piece_ticks'] / max(pr['piece_ticks'], 1):.1f}% of wave time", flush=True)
         if st.n_reflect + st.n_refract == 0:
             break
     print("counters" if counters else "timing only")
