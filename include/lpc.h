@@ -173,6 +173,10 @@ typedef struct {
     int64_t heavy_piece;     /* piece with the largest summed wave time (last launch) */
     int64_t heavy_piece_ticks;
     int64_t piece_ticks;     /* summed wave ticks over all pieces (last launch)  */
+    int64_t tail_waves;      /* k_intersect waves that ran >= 2^16 ticks (655 us) */
+    int64_t tail_nodes;      /* their node visits                               */
+    int64_t tail_spread_urad;/* their summed direction spread (micro-radians)   */
+    int64_t tail_exact;      /* their exact tests                               */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * k_intersect traversal counters (2, diagnostic: adds atomics), or disable (0). */

@@ -33,7 +33,9 @@ class Prof(ctypes.Structure):
                 ("node_visits", ctypes.c_int64), ("group_tests", ctypes.c_int64),
                 ("wave_traversals", ctypes.c_int64), ("exact_tests", ctypes.c_int64),
                 ("wave_hist", ctypes.c_int64 * 24), ("heavy_piece", ctypes.c_int64),
-                ("heavy_piece_ticks", ctypes.c_int64), ("piece_ticks", ctypes.c_int64)]
+                ("heavy_piece_ticks", ctypes.c_int64), ("piece_ticks", ctypes.c_int64),
+                ("tail_waves", ctypes.c_int64), ("tail_nodes", ctypes.c_int64),
+                ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

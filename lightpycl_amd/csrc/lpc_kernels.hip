@@ -152,18 +152,19 @@ static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__
 // Stack depth per wave (node refs); the host checks every hierarchy fits.
 #define LPC_STACK 32
 
-static __device__ __forceinline__ void sphere_test4(const float *cx, const float *cy, const float *cz,
-                                                    const float *onemB, const float *negA, f2 ox, f2 oy,
-                                                    f2 oz, f2 nx, f2 ny, f2 nz, f2 (&d)[4])
+static __device__ __forceinline__ float sphere_test(float cx, float cy, float cz, float onemB, float negA,
+                                                   const f3 &O, float nx, float ny, float nz)
 {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d[k] = sphere_test1(cx[k], cy[k], cz[k], onemB[k], negA[k], ox, oy, oz, nx, ny, nz);
+    const float wx = cx - O.x, wy = cy - O.y, wz = cz - O.z;
+    const float ww = wx * wx + wy * wy + wz * wz;
+    const float wd = wx * nx + wy * ny + wz * nz;
+    return ww * onemB + (negA - wd * wd);
 }
 
-// k_intersect: packets of 128 rays of the coherence order (two per lane, packed
-// FP32 pairs), grid = (ceil(n/512), pieces), block = 4 waves.  A wave walks the
-// piece's subtree with a wave-uniform stack in LDS: a node's four children are
-// tested against all 128 rays (filter form d <= 0, see filter_record; node data
+// k_intersect: packets of 64 rays of the coherence order (one per lane),
+// grid = (ceil(n/256), pieces), block = 4 waves.  A wave walks the piece's
+// subtree with a wave-uniform stack in LDS: a node's four children are tested
+// against all 64 rays (filter form d <= 0, see filter_record; node data
 // wave-uniform through the scalar cache); a child node is pushed when any ray
 // passes it, a child triangle gets the exact Moller-Trumbore test for the rays
 // that pass its own test.
@@ -178,57 +179,82 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
                                                    unsigned long long *__restrict__ stats)
 {
     __shared__ int32_t stack[4][LPC_STACK];
+    __shared__ int32_t qidx[4][64];
+    __shared__ uint64_t qmask[4][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
-    if (w * 128 >= n) return;                      // whole wave past the end
-    const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
-    f3 O0, O1, D0, D1;
-    load_ray(R, rs, n, s0 < n ? s0 : n - 1, O0, D0);
-    load_ray(R, rs, n, s1 < n ? s1 : n - 1, O1, D1);
+    if (w * 64 >= n) return;                       // whole wave past the end
+    const int64_t s = w * 64 + lane;
+    f3 O, D;
+    load_ray(R, rs, n, s < n ? s : n - 1, O, D);
     // unit direction for the filter only (its rounding is inside the margin)
-    const float u0 = 1.0f / sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z);
-    const float u1 = 1.0f / sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z);
-    const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
-    const f2 nx = {D0.x * u0, D1.x * u1}, ny = {D0.y * u0, D1.y * u1}, nz = {D0.z * u0, D1.z * u1};
+    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
+    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
     const Piece P = pieces[blockIdx.y];
 
     const uint64_t clk0 = stats ? wall_clock64() : 0;
-    float t0 = max_ray_len, t1 = max_ray_len;
-    int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
+    float t = max_ray_len;
+    int32_t i = -1, c = 0;
     int32_t *stk = stack[wv];
-    int32_t top = 0;
+    int32_t top = 0, nq = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
-    if (P.root >= 0) {
-        const f2 d = sphere_test1(P.cx, P.cy, P.cz, P.onemB, P.negA, ox, oy, oz, nx, ny, nz);
-        if (any_lane(d.x <= 0.0f || d.y <= 0.0f)) stk[top++] = P.root;
-    }
+    // Exact tests are deferred: candidate (triangle, lanes) pairs queue up in LDS;
+    // a drain gathers up to 64 exact records with one lane-parallel load and runs
+    // Moller-Trumbore per entry (record broadcast by readlane), so a wave pays one
+    // memory latency per 64 candidates instead of one per candidate.
+    auto drain = [&]() {
+        if (nq == 0) return;
+        const int32_t my = lane < nq ? qidx[wv][lane] : 0;
+        ExactRec X;
+        if (lane < nq) X = xrec[my];
+        for (int e = 0; e < nq; ++e) {
+            const uint64_t m = qmask[wv][e];
+            if ((m >> lane) & 1ull) {
+                mt_accumulate(O, D, mk3(bcast(X.v0x, e), bcast(X.v0y, e), bcast(X.v0z, e)),
+                              mk3(bcast(X.e1x, e), bcast(X.e1y, e), bcast(X.e1z, e)),
+                              mk3(bcast(X.e2x, e), bcast(X.e2y, e), bcast(X.e2z, e)), bcasti(my, e), eps, t, i, c);
+                ++n_exact;
+            }
+        }
+    };
+    if (P.root >= 0 && any_lane(sphere_test(P.cx, P.cy, P.cz, P.onemB, P.negA, O, nx, ny, nz) <= 0.0f))
+        stk[top++] = P.root;
     while (top > 0) {
         const int32_t node = __builtin_amdgcn_readfirstlane(stk[--top]);
         const Node4 N = nodes[node];
         ++n_nodes;
-        f2 d[4];
-        sphere_test4(N.cx, N.cy, N.cz, N.onemB, N.negA, ox, oy, oz, nx, ny, nz, d);
+        float d[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool r0 = d[k].x <= 0.0f, r1 = d[k].y <= 0.0f;
-            if (!any_lane(r0 || r1)) continue;
-            const int32_t ref = N.ref[k];
-            if (ref >= 0) { stk[top++] = ref; continue; }
-            const int32_t idx = ~ref;
-            const ExactRec x = xrec[idx];
-            const f3 V0 = mk3(x.v0x, x.v0y, x.v0z);
-            const f3 E1 = mk3(x.e1x, x.e1y, x.e1z);
-            const f3 E2 = mk3(x.e2x, x.e2y, x.e2z);
-            if (r0) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
-            if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
-            n_exact += (uint32_t)r0 + (uint32_t)r1;
+        for (int k = 0; k < 4; ++k) d[k] = sphere_test(N.cx[k], N.cy[k], N.cz[k], N.onemB[k], N.negA[k], O, nx, ny, nz);
+        if (N.ref[0] >= 0) {                       // internal node: children are nodes
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (any_lane(d[k] <= 0.0f)) stk[top++] = N.ref[k];
+        } else {                                   // leaf: children are triangles -> queue
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
+                if (!m) continue;
+                if (lane == 0) { qidx[wv][nq] = ~N.ref[k]; qmask[wv][nq] = m; }
+                if (++nq == 64) { drain(); nq = 0; }
+            }
         }
     }
+    drain();
     if (stats) {
         for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
+        // packet spread: max angle between a lane's direction and lane 0's
+        const float cs = nx * bcast(nx, 0) + ny * bcast(ny, 0) + nz * bcast(nz, 0);
+        const float cmin = wave_red(cs, 0);
         if (lane == 0) {
             const uint64_t dt = wall_clock64() - clk0;
             const int b = dt ? min(23, 63 - __builtin_clzll(dt)) : 0;
+            if (dt >= (1ull << 16)) {           // tail wave (>= 655 us)
+                atomicAdd(&stats[4], 1ull);
+                atomicAdd(&stats[5], (unsigned long long)n_nodes);
+                atomicAdd(&stats[6], (unsigned long long)(acosf(fminf(1.0f, fmaxf(-1.0f, cmin))) * 1e6f));
+                atomicAdd(&stats[7], (unsigned long long)n_exact);
+            }
             atomicAdd(&stats[0], (unsigned long long)n_nodes);
             atomicAdd(&stats[2], 1ull);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
@@ -236,9 +262,7 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
             if (blockIdx.y < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + blockIdx.y], (unsigned long long)dt);
         }
     }
-    const int64_t o = (int64_t)P.slot * n;
-    if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
-    if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1);
+    if (s < n) slot_flush(skey, scnt, (int64_t)P.slot * n, perm ? perm[s] : s, t, i, c);
 }
 
 // k_slivers: the run's slivers (line filter) for packets of 128 rays (two per

@@ -319,7 +319,7 @@ static int build_records(lpc_handle *h)
 // runs' slivers in blocks of <= 64 (one lane each).
 static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
 {
-    const int64_t bx = std::max<int64_t>(1, (n + 511) / 512);
+    const int64_t bx = std::max<int64_t>(1, (n + 255) / 256);
     const size_t nr = h->run_levels.size();
     std::vector<int32_t> run_slot(nr, -1);
     for (int32_t j = 0; j < h->K; ++j)
@@ -489,7 +489,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     if (pt->npieces > 0) {
-        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + 511) / 512), (unsigned)pt->npieces), dim3(256), 0,
+        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + 255) / 256), (unsigned)pt->npieces), dim3(256), 0,
                            h->stream, in, rs, n, perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
                            (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt,
                            h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr);
@@ -1198,6 +1198,8 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     out->wave_traversals = (int64_t)st[2];
     out->exact_tests = (int64_t)st[3];
     for (int b = 0; b < 24; ++b) out->wave_hist[b] = (int64_t)st[LPC_STATS_HIST + b];
+    out->tail_waves = (int64_t)st[4]; out->tail_nodes = (int64_t)st[5];
+    out->tail_spread_urad = (int64_t)st[6]; out->tail_exact = (int64_t)st[7];
     out->heavy_piece = -1; out->heavy_piece_ticks = 0; out->piece_ticks = 0;
     for (int p = 0; p < LPC_STATS_PIECES; ++p) {
         const int64_t v = (int64_t)st[LPC_STATS_PIECE + p];

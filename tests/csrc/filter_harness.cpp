@@ -221,3 +221,26 @@ extern "C" void packet_eval(int n, const float *O, const float *D, int pk, int m
         }
     }
 }
+
+// Per-ray filter candidate count over m triangles (kernel evaluation of the
+// sphere test; "always" records are skipped, they go to the sliver list).
+extern "C" void cand_count(int n, const float *O, const float *D, int m, const float *V, double dcap, int *cnt)
+{
+    std::vector<FiltRec> rec((size_t)m);
+    for (int j = 0; j < m; ++j) {
+        const float *v = V + 9 * j;
+        float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
+        rec[(size_t)j] = filter_record(v0, v1, v2, j, dcap);
+    }
+    for (int i = 0; i < n; ++i) {
+        const float *o = O + 3 * i, *dd = D + 3 * i;
+        float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
+        int c = 0;
+        for (int j = 0; j < m; ++j) {
+            const FiltRec &r = rec[(size_t)j];
+            if (r.onemB < -1e29f) continue;
+            c += eval_test(o, dd[0] * s, dd[1] * s, dd[2] * s, r.cx, r.cy, r.cz, r.onemB, r.negA) <= 0.0f;
+        }
+        cnt[i] = c;
+    }
+}

@@ -40,6 +40,10 @@ for counters in (False, True):
                   ", ".join(f"{(1 << b) / 100:.2f}: {c}" for b, c in nz) +
                   f"  | heaviest piece {pr['heavy_piece']} = "
                   f"{100.0 * pr['heavy_piece_ticks'] / max(pr['piece_ticks'], 1):.1f}% of wave time", flush=True)
+            tw = max(pr["tail_waves"], 1)
+            print(f"    tail waves {pr['tail_waves']}: nodes/wave {pr['tail_nodes']/tw:.0f} "
+                  f"spread {pr['tail_spread_urad']/tw/1e6:.4f} rad exact/wave {pr['tail_exact']/tw:.0f}; "
+                  f"all waves: nodes/wave {pr['node_visits']/max(pr['wave_traversals'],1):.1f}", flush=True)
         if st.n_reflect + st.n_refract == 0:
             break
     print("counters" if counters else "timing only")
