@@ -9,7 +9,7 @@ struct Piece {                       // part of one mesh run
     int32_t root;                     // subtree root node (k_intersect)
     int32_t s_lo, s_hi;               // sliver records [s_lo, s_hi) (k_slivers)
     int32_t slot;                     // per-mesh scratch slot the run flushes into
-    float cx, cy, cz, onemB, negA;    // the root's own test
+    float cx, cy, cz, negB, negA;     // the root's own test
     int32_t pad[3];
 };
 

@@ -33,20 +33,17 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 namespace lpck {
 
 // ---------------------------------------------------------------------------
-// k_intersect
-// grid = (ceil(n/512), pieces), block = 256 = 4 waves; each wave traces a packet
-// of 128 consecutive rays of the coherence order (k_raykey + sort + k_gather), two
-// per lane as packed FP32 pairs, through one piece = a range of 64-triangle
-// clusters (and a share of the slivers) of one mesh run:
-//   1. lane-parallel packet tests (packet_sphere_test against the wave's
-//      PacketRec) of 64 cluster records at a time -> ballot;
-//   2. per passing cluster: per-ray cluster test (record broadcast by readlane),
-//      then lane-parallel packet tests of its 64 triangle records -> ballot;
-//   3. per passing triangle: per-ray sphere test, exact Moller-Trumbore for the
-//      candidates (mt_accumulate).
-// Slivers: lane-parallel packet_sliver_test, then the per-ray line filter.
-// Every level is implied by the one below it (tests/test_filter_superset.py), so
-// the exact test sees every pair it would accept: results are bit-exact.
+// Intersection.  Rays are processed in the coherence order (k_raykey + radix
+// sort + k_gather); every kernel flushes its per-ray nearest hit and count into
+// the per-mesh slots with order-independent atomics (slot_flush), so the kernels
+// and their pieces may run in any order:
+//   k_intersect  a mesh run's sphere hierarchy (filter_test), 64-ray packets;
+//   k_packet     per-wave bound of 128 rays (origin ball + direction cone);
+//   k_slivers    the runs' slivers: lane-parallel packet_sliver_test, then the
+//                per-ray line filter.
+// Every filter level is implied by the one below it and the lowest one by the
+// exact test (tests/test_filter_superset.py), so the exact Moller-Trumbore test
+// sees every pair it would accept: results are bit-exact.
 static __device__ __forceinline__ bool any_lane(bool b)
 {
     return __builtin_amdgcn_ballot_w64(b) != 0;
@@ -57,15 +54,6 @@ static __device__ __forceinline__ float bcast(float v, int l)
 }
 static __device__ __forceinline__ int bcasti(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
-static __device__ __forceinline__ f2 sphere_test1(float cx, float cy, float cz, float onemB, float negA, f2 ox,
-                                                  f2 oy, f2 oz, f2 nx, f2 ny, f2 nz)
-{
-    const f2 wx = cx - ox, wy = cy - oy, wz = cz - oz;
-    const f2 ww = wx * wx + wy * wy + wz * wz;
-    const f2 wd = wx * nx + wy * ny + wz * nz;
-    const f2 tq = negA - wd * wd;
-    return ww * onemB + tq;
-}
 
 template <class T>
 static __device__ __forceinline__ T wave_red(T v, int op)   // 0 min, 1 max, 2 sum
@@ -152,15 +140,6 @@ static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__
 // Stack depth per wave (node refs); the host checks every hierarchy fits.
 #define LPC_STACK 32
 
-static __device__ __forceinline__ float sphere_test(float cx, float cy, float cz, float onemB, float negA,
-                                                   const f3 &O, float nx, float ny, float nz)
-{
-    const float wx = cx - O.x, wy = cy - O.y, wz = cz - O.z;
-    const float ww = wx * wx + wy * wy + wz * wz;
-    const float wd = wx * nx + wy * ny + wz * nz;
-    return ww * onemB + (negA - wd * wd);
-}
-
 // k_intersect: packets of 64 rays of the coherence order (one per lane),
 // grid = (ceil(n/256), pieces), block = 4 waves.  A wave walks the piece's
 // subtree with a wave-uniform stack in LDS: a node's four children are tested
@@ -168,6 +147,18 @@ static __device__ __forceinline__ float sphere_test(float cx, float cy, float cz
 // wave-uniform through the scalar cache); a child node is pushed when any ray
 // passes it, a child triangle gets the exact Moller-Trumbore test for the rays
 // that pass its own test.
+// k-th set bit (0-based) of m.
+static __device__ __forceinline__ int select_bit(uint64_t m, int k)
+{
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const int c = __builtin_popcountll((m >> pos) & ((1ull << w) - 1ull));
+        if (k >= c) { k -= c; pos += w; }
+    }
+    return pos;
+}
+
 __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                    const int32_t *__restrict__ perm,
                                                    const Node4 *__restrict__ nodes,
@@ -179,8 +170,11 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
                                                    unsigned long long *__restrict__ stats)
 {
     __shared__ int32_t stack[4][LPC_STACK];
-    __shared__ int32_t qidx[4][64];
+    __shared__ int32_t qidx[4][64], qscan[4][64];
     __shared__ uint64_t qmask[4][64];
+    __shared__ float ray[4][6][64];                // the wave's rays (O, D) for the drain
+    __shared__ unsigned long long lkey[4][64];     // per-ray nearest hit (slot_key)
+    __shared__ int32_t lcnt[4][64];                // per-ray hit count
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     if (w * 64 >= n) return;                       // whole wave past the end
@@ -191,33 +185,57 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
     const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
     const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
     const Piece P = pieces[blockIdx.y];
+    ray[wv][0][lane] = O.x; ray[wv][1][lane] = O.y; ray[wv][2][lane] = O.z;
+    ray[wv][3][lane] = D.x; ray[wv][4][lane] = D.y; ray[wv][5][lane] = D.z;
+    const unsigned long long key0 = slot_key(max_ray_len, -1);
+    lkey[wv][lane] = key0;
+    lcnt[wv][lane] = 0;
 
     const uint64_t clk0 = stats ? wall_clock64() : 0;
-    float t = max_ray_len;
-    int32_t i = -1, c = 0;
     int32_t *stk = stack[wv];
     int32_t top = 0, nq = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
-    // Exact tests are deferred: candidate (triangle, lanes) pairs queue up in LDS;
-    // a drain gathers up to 64 exact records with one lane-parallel load and runs
-    // Moller-Trumbore per entry (record broadcast by readlane), so a wave pays one
-    // memory latency per 64 candidates instead of one per candidate.
+    // Exact tests are deferred: candidate (triangle, ray lanes) entries queue up
+    // in LDS; a drain expands them into (triangle, ray) pairs, runs 64 pairs at a
+    // time one per lane (exact record gathered, ray read from LDS) and folds the
+    // results into the per-ray accumulators with LDS atomics: atomicMin on
+    // slot_key(t, idx) for t < max_ray_len and a count for every accepted t > eps,
+    // which is mt_accumulate's rule (minimal t, lowest index among equal t).
     auto drain = [&]() {
         if (nq == 0) return;
-        const int32_t my = lane < nq ? qidx[wv][lane] : 0;
-        ExactRec X;
-        if (lane < nq) X = xrec[my];
-        for (int e = 0; e < nq; ++e) {
-            const uint64_t m = qmask[wv][e];
-            if ((m >> lane) & 1ull) {
-                mt_accumulate(O, D, mk3(bcast(X.v0x, e), bcast(X.v0y, e), bcast(X.v0z, e)),
-                              mk3(bcast(X.e1x, e), bcast(X.e1y, e), bcast(X.e1z, e)),
-                              mk3(bcast(X.e2x, e), bcast(X.e2y, e), bcast(X.e2z, e)), bcasti(my, e), eps, t, i, c);
+        const int pc = lane < nq ? __builtin_popcountll(qmask[wv][lane]) : 0;
+        int incl = pc;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        qscan[wv][lane] = incl;
+        const int total = __shfl(incl, 63, 64);
+        for (int base = 0; base < total; base += 64) {
+            const int q = base + lane;
+            if (q < total) {
+                int e = 0;                         // first entry with qscan[e] > q
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (e + step <= 63 && qscan[wv][e + step - 1] <= q) e += step;
+                const int k = q - (e > 0 ? qscan[wv][e - 1] : 0);
+                const int r = select_bit(qmask[wv][e], k);
+                const int32_t idx = qidx[wv][e];
+                const ExactRec x = xrec[idx];
+                const f3 Or = mk3(ray[wv][0][r], ray[wv][1][r], ray[wv][2][r]);
+                const f3 Dr = mk3(ray[wv][3][r], ray[wv][4][r], ray[wv][5][r]);
+                float t;
+                if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
+                    t > eps) {
+                    atomicAdd(&lcnt[wv][r], 1);
+                    if (t < max_ray_len) atomicMin(&lkey[wv][r], slot_key(t, idx));
+                }
                 ++n_exact;
             }
         }
+        nq = 0;
     };
-    if (P.root >= 0 && any_lane(sphere_test(P.cx, P.cy, P.cz, P.onemB, P.negA, O, nx, ny, nz) <= 0.0f))
+    if (P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f))
         stk[top++] = P.root;
     while (top > 0) {
         const int32_t node = __builtin_amdgcn_readfirstlane(stk[--top]);
@@ -225,7 +243,8 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
         ++n_nodes;
         float d[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = sphere_test(N.cx[k], N.cy[k], N.cz[k], N.onemB[k], N.negA[k], O, nx, ny, nz);
+        for (int k = 0; k < 4; ++k)
+            d[k] = filter_test(N.cx[k], N.cy[k], N.cz[k], N.negB[k], N.negA[k], O.x, O.y, O.z, nx, ny, nz);
         if (N.ref[0] >= 0) {                       // internal node: children are nodes
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -236,7 +255,7 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
                 const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
                 if (!m) continue;
                 if (lane == 0) { qidx[wv][nq] = ~N.ref[k]; qmask[wv][nq] = m; }
-                if (++nq == 64) { drain(); nq = 0; }
+                if (++nq == 64) drain();
             }
         }
     }
@@ -262,7 +281,13 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
             if (blockIdx.y < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + blockIdx.y], (unsigned long long)dt);
         }
     }
-    if (s < n) slot_flush(skey, scnt, (int64_t)P.slot * n, perm ? perm[s] : s, t, i, c);
+    if (s < n) {
+        const unsigned long long k = lkey[wv][lane];
+        const int32_t c = lcnt[wv][lane];
+        const int64_t o = (int64_t)P.slot * n, q = perm ? perm[s] : s;
+        if (c) atomicAdd(&scnt[o + q], c);
+        if (k != key0) atomicMin(&skey[o + q], k);
+    }
 }
 
 // k_slivers: the run's slivers (line filter) for packets of 128 rays (two per

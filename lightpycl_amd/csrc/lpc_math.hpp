@@ -261,39 +261,57 @@ LPC_HD void stereograph_project(f3 p, f3 piv, f3 R0, f3 R1, f3 R2, float pwr, fl
 // ---------------------------------------------------------------------------
 // Conservative bounding-sphere filter.
 //
-// For a ray with origin O and unit direction n (computed in float) and a
-// triangle with bounding sphere (c, rho), the squared distance from c to the
-// ray's line is  ww - wd^2  with w = c - O, ww = w.w, wd = w.n.  The filter
-// accepts (candidate) when
-//       d = ww * (1 - B) - A - wd^2  <=  0
-// i.e. dist^2 <= A + B ww.  A and B inflate the sphere enough that every pair
-// the exact Moller-Trumbore test accepts is a candidate:
-//  * rounding of ww, wd, n in float: |error| <= ~16 eps ww  (term kB_round);
-//  * Moller-Trumbore's own error: an accepted pair's line passes within
-//    ~c eps |T| |E|^2/|E1 x E2| of the triangle (the barycentric error of a
-//    nearly-parallel ray times the ray's slope), |T| <= |w| + rho;  with
-//    (a+b)^2 <= (1+h) a^2 + (1+1/h) b^2 this gives the rho^2 and ww terms.
-// The constants are deliberately generous (see tests/test_filter_superset.py,
-// which measures the actual worst case on adversarial inputs).
+// Per (ray, record) the hot loop evaluates, in float (FMA contraction allowed),
+//     w = c - O,  p = w x n,  d = p.p + (negA + negB w.w)        (n = D/|D|)
+// and calls the pair a candidate when d <= 0, i.e. when dist(c, line)^2 <= A + B |w|^2
+// (p.p is the squared distance from c to the ray's line, computed without the
+// cancellation of |w|^2 - (w.n)^2).  For a triangle record A and B make the
+// candidate set a superset of the pairs the exact Moller-Trumbore test accepts:
+//  * an accepted pair's line passes within kappa |T| of the triangle, kappa =
+//    kmt eps |E|^2 / |E1 x E2| (Moller-Trumbore's error for a nearly parallel ray,
+//    kmt = 256 deliberately generous), |T| <= |w| + rho, so
+//        dist(c, line) <= rho (1 + kappa) + kappa |w|;
+//  * (a + b)^2 <= (1+h) a^2 + (1+1/h) b^2 for any h > 0 gives A + B |w|^2; h is
+//    chosen per record for the scene's scale S (h = kappa S / a);
+//  * store_test() adds the float evaluation of d: |p_f| <= dist (1 + 3 eps) + 7 eps |w|,
+//    so exact dist^2 <= A + B ww  ==>  d_float <= 0 for the stored (negA, negB);
+//    conversely d_float <= 0  ==>  exact dist^2 <= implied_test(negA, negB).
+// tests/test_filter_superset.py measures the actual worst case on adversarial inputs.
 // Triangles with an exactly-zero edge are never accepted by Moller-Trumbore
 // (DEN == 0) and get A = +inf ("never", d = +inf).  Triangles with |E1||E2| below
 // 1e-6/Dcap can never reach |DEN| >= 1e-6 for rays with |D| <= Dcap and are
-// "never" too (the engine checks |D| <= Dcap at run time).
+// "never" too (the engine checks |D| <= Dcap at run time).  negB = -1e30 marks a
+// record that always passes ("always"; triangles with kappa >= 0.1 are slivers).
 struct FiltRec {
     float cx, cy, cz;   // sphere centre (float)
-    float onemB;        // 1 - B
+    float negB;         // -B
     float negA;         // -A
     int32_t idx;        // original triangle index
     int32_t pad0, pad1;
 };
 
+LPC_HD float filter_test(float cx, float cy, float cz, float negB, float negA, float ox, float oy, float oz,
+                         float nx, float ny, float nz)
+{
+    const float wx = cx - ox, wy = cy - oy, wz = cz - oz;
+    const float px = wy * nz - wz * ny, py = wz * nx - wx * nz, pz = wx * ny - wy * nx;
+    const float pp = px * px + py * py + pz * pz;
+    const float ww = wx * wx + wy * wy + wz * wz;
+    return pp + (negA + negB * ww);
+}
+
+// Float-evaluation slack of filter_test, both ways (factor on A and B, and an
+// absolute term on B = (1 + 1/h') 49 eps^2 with h' = 1e-3, rounded up).
+#define LPC_FILT_REL 2e-3
+#define LPC_FILT_ABS 2e-10
+
 // One node of a mesh run's 4-wide sphere hierarchy, children in SoA form.
 // ref[k] >= 0: child node; ref[k] < 0: triangle ~ref[k], whose test is the
-// triangle's own filter record.  A node's test (in its parent) is
-// cluster_record() of ALL triangles below it, so a ray that is a candidate for
+// triangle's own filter record.  A node's test (in its parent) is node_record()
+// of ALL triangles below it, so a ray whose line Moller-Trumbore accepts against
 // some triangle passes every test on the way down.  Unused children: never.
 struct Node4 {
-    float cx[4], cy[4], cz[4], onemB[4], negA[4];
+    float cx[4], cy[4], cz[4], negB[4], negA[4];
     int32_t ref[4];
     int32_t pad[8];
 };
@@ -321,21 +339,21 @@ struct PacketRec {
 };
 
 // Packet test of a sphere record: false only if NO ray of the packet can pass the
-// per-ray float test d = ww (1-B) - A - wd^2 <= 0.  A passing ray satisfies
-// (exactly) dist(c, line)^2 <= A + (B + 32 eps) |w|^2 (see cluster_record), so the
-// angle psi between w = c - O and its line obeys sin^2 psi <= B' + A / |w|^2 =: sin^2 beta.
+// per-ray float test (filter_test).  A passing ray satisfies (exactly)
+// dist(c, line)^2 <= A + B |w|^2 with (A, B) = implied_test, so the angle psi
+// between w = c - O and its line obeys sin^2 psi <= B + A / |w|^2 =: sin^2 beta.
 // With W = c - o_c, L = |W|, |w| >= L - ro, angle(W, w) <= gamma = asin(ro / L) and
 // angle(line n, line a) <= th, the angle phi between W and the axis line obeys
 //     phi <= th + gamma + beta =: Sigma,
 // tested as |W x a| <= L sin(Sigma) (all angles in [0, pi/2]).  Float evaluation
 // error is covered by 1e-3 relative + 1e-6 absolute on sin(Sigma) and by passing
 // outright when a cosine would be computed with cancellation (sin > 0.99).
-LPC_HD bool packet_sphere_test(const PacketRec &Q, float cx, float cy, float cz, float onemB, float negA)
+LPC_HD bool packet_sphere_test(const PacketRec &Q, float cx, float cy, float cz, float negB, float negA)
 {
     if (Q.all) return true;
     if (!(negA < INFINITY)) return false;                  // never record
-    const float A = -negA * 1.00001f;
-    const float B = (1.0f - onemB) + 4e-6f;
+    const float A = -negA * (1.0f + 2.0f * (float)LPC_FILT_REL);
+    const float B = -negB * (1.0f + 2.0f * (float)LPC_FILT_REL) + 2.0f * (float)LPC_FILT_ABS;
     const float wx = cx - Q.ox, wy = cy - Q.oy, wz = cz - Q.oz;
     const float L2 = wx * wx + wy * wy + wz * wz;
     const float L = sqrtf(L2);
@@ -406,6 +424,41 @@ struct ExactRec {       // V0, E1 = V1-V0, E2 = V2-V0 (float, exactly as the ref
     float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, pad0, pad1, pad2;
 };
 
+// Host: float record of the exact bound dist^2 <= A + B ww (A rounded up, B up).
+static inline void store_test(double A, double B, float *negB, float *negA)
+{
+    const double As = A * (1.0 + LPC_FILT_REL), Bs = B * (1.0 + LPC_FILT_REL) + LPC_FILT_ABS;
+    if (!(Bs < 1.0) || !(As < 1e30)) { *negB = -1e30f; *negA = 0.0f; return; }   // always
+    float Af = (float)As, Bf = (float)Bs;
+    if ((double)Af < As) Af = nextafterf(Af, INFINITY);
+    if ((double)Bf < Bs) Bf = nextafterf(Bf, INFINITY);
+    *negA = -Af;
+    *negB = -Bf;
+}
+
+// Host: exact bound implied by a passing float test of the record (negB, negA).
+static inline void implied_test(float negB, float negA, double &A, double &B)
+{
+    A = -(double)negA * (1.0 + LPC_FILT_REL);
+    B = -(double)negB * (1.0 + LPC_FILT_REL) + LPC_FILT_ABS;
+}
+
+// Host: Moller-Trumbore's line-distance error factor of a triangle: an accepted
+// pair's line passes within kappa |T| of the triangle, kappa = kmt eps |E|^2 / |E1 x E2|
+// (kmt = 256, deliberately generous; inf for a degenerate triangle).
+static inline double tri_kappa(const float *V0, const float *V1, const float *V2)
+{
+    const double eps = 1.0 / 16777216.0, kmt = 256.0;
+    double a[3], b[3];
+    for (int k = 0; k < 3; ++k) { a[k] = (double)V1[k] - (double)V0[k]; b[k] = (double)V2[k] - (double)V0[k]; }
+    const double n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    const double nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+    const double aa = a[0] * a[0] + a[1] * a[1] + a[2] * a[2], bb = b[0] * b[0] + b[1] * b[1] + b[2] * b[2];
+    const double cc = (b[0] - a[0]) * (b[0] - a[0]) + (b[1] - a[1]) * (b[1] - a[1]) + (b[2] - a[2]) * (b[2] - a[2]);
+    const double emax2 = fmax(aa, fmax(bb, cc));
+    return nn > 0.0 ? kmt * eps * emax2 / sqrt(nn) : INFINITY;
+}
+
 // Host: build the filter record of triangle (V0,V1,V2) given as floats.
 #if defined(__HIPCC__)
 static inline __host__ FiltRec filter_record(
@@ -413,12 +466,12 @@ static inline __host__ FiltRec filter_record(
 static inline FiltRec filter_record(
 #endif
                                     const float *V0, const float *V1, const float *V2,
-                                    int32_t idx, double Dcap)
+                                    int32_t idx, double Dcap, double S)
 {
     const double eps = 1.0 / 16777216.0;   // 2^-24
     FiltRec r;
     r.idx = idx; r.pad0 = 0; r.pad1 = 0;
-    double a[3], b[3], c3[3], p0[3];
+    double a[3], b[3], p0[3];
     float e1f[3], e2f[3];
     for (int k = 0; k < 3; ++k) {
         p0[k] = V0[k];
@@ -463,22 +516,14 @@ static inline FiltRec filter_record(
     double e2n = sqrt((double)e2f[0] * e2f[0] + (double)e2f[1] * e2f[1] + (double)e2f[2] * e2f[2]);
     bool tiny = e1n * e2n * Dcap * (1.0 + 1e-4) < 1e-6;
     if (zero_edge || tiny) {           // never a candidate: d = +inf
-        r.onemB = 1.0f; r.negA = INFINITY;
+        r.negB = 0.0f; r.negA = INFINITY;
         return r;
     }
-    double emax2 = aa > bb ? aa : bb;
-    emax2 = emax2 > cc ? emax2 : cc;
-    double asp = (nn > 0.0) ? emax2 / sqrt(nn) : INFINITY;   // |E|^2 / |E1 x E2|
-    const double h = 0.05, kmt = 256.0, kround = 64.0;
-    double g2 = (1.0 + 1.0 / h) * 2.0 * (kmt * eps * asp) * (kmt * eps * asp);
-    double A = rho2 * ((1.0 + h) + g2);
-    double B = g2 + kround * eps;
-    if (!(B < 0.5)) { r.onemB = -1e30f; r.negA = 0.0f; return r; }   // always a candidate
-    float onemB = (float)(1.0 - B * (1.0 + 1e-6));
-    if ((double)onemB > 1.0 - B) onemB = nextafterf(onemB, -INFINITY);
-    float Af = (float)(A * (1.0 + 1e-6));
-    if ((double)Af < A) Af = nextafterf(Af, INFINITY);
-    r.onemB = onemB; r.negA = -Af;
+    const double kappa = tri_kappa(V0, V1, V2);
+    if (!(kappa < 0.1)) { r.negB = -1e30f; r.negA = 0.0f; return r; }   // always (sliver)
+    const double ra = sqrt(rho2) * (1.0 + kappa);
+    const double h = ra > 0.0 ? fmin(1.0, fmax(1e-3, kappa * S / ra)) : 1.0;
+    store_test((1.0 + h) * ra * ra, (1.0 + 1.0 / h) * kappa * kappa, &r.negB, &r.negA);
     return r;
 }
 
@@ -509,55 +554,43 @@ static inline void sliver_params(const float *V0, const float *V1, const float *
     *a_out = af; *b_out = bf;
 }
 
-// Host: round a sphere test (A, B) to the float record form (A up, 1-B down).
-static inline void round_test(double A, double B, float *onemB_out, float *negA_out)
+// Host: test of a hierarchy node over `count` triangles (vertex pointers
+// tri[3*i .. 3*i+2]).  It must pass for every ray whose line Moller-Trumbore
+// accepts against SOME triangle below the node (the triangles' own filter tests
+// then pick the candidates).  With C the centre and R the radius of a sphere
+// containing all their vertices, an accepted triangle's closest point X to the
+// line lies in that sphere, so dist(C, line) <= R + kappa |T| with
+// |T| <= |w_C| + R:  dist <= R (1 + kappa) + kappa |w_C|, kappa = max over the
+// triangles (tri_kappa) -- the same form as a triangle's own record.
+static inline void node_record(const float *const *tri, int count, double S, float *cx, float *cy, float *cz,
+                               float *negB, float *negA)
 {
-    if (!(B < 0.5)) { *onemB_out = -1e30f; *negA_out = 0.0f; return; }   // always a candidate
-    float onemB = (float)(1.0 - B * (1.0 + 1e-6));
-    if ((double)onemB > 1.0 - B) onemB = nextafterf(onemB, -INFINITY);
-    float Af = (float)(A * (1.0 + 1e-6));
-    if ((double)Af < A) Af = nextafterf(Af, INFINITY);
-    *onemB_out = onemB; *negA_out = -Af;
-}
-
-// Host: test of a cluster of TRIANGLES (any subtree of the hierarchy) implied by
-// the member triangles' tests.  If a member's float test passes, the exact line
-// distance to its centre obeys dist_i^2 <= A_i + Bp_i w_i^2 (Bp_i = B_i + 32 eps
-// covers the float evaluation).  With delta_i = |c_i - C|:
-// dist_C <= delta_i + sqrt(A_i) + sqrt(Bp_i)(|w_C| + delta_i) <= R0 + b |w_C|, so
-// dist_C^2 <= (1+h) R0^2 + (1+1/h) b^2 w_C^2; +64 eps on B for the cluster's own
-// float evaluation.  `never` members are skipped; an `always` member makes the
-// cluster always a candidate.
-static inline void cluster_record(const FiltRec *m, int count, float *cx, float *cy, float *cz,
-                                  float *onemB, float *negA)
-{
-    const double eps = 1.0 / 16777216.0, h = 0.05;
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    int live = 0;
-    bool always = false;
+    double kappa = 0.0;
     for (int i = 0; i < count; ++i) {
-        if (m[i].negA == INFINITY) continue;                 // never
-        if (m[i].onemB < -1e29f) { always = true; continue; }
-        const float c[3] = {m[i].cx, m[i].cy, m[i].cz};
-        for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], c[k]); hi[k] = fmax(hi[k], c[k]); }
-        ++live;
+        kappa = fmax(kappa, tri_kappa(tri[3 * i], tri[3 * i + 1], tri[3 * i + 2]));
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = fmin(lo[k], (double)tri[3 * i + v][k]);
+                hi[k] = fmax(hi[k], (double)tri[3 * i + v][k]);
+            }
     }
     *cx = *cy = *cz = 0.0f;
-    if (always) { *onemB = -1e30f; *negA = 0.0f; return; }
-    if (live == 0) { *onemB = 1.0f; *negA = INFINITY; return; }
+    if (count == 0) { *negB = 0.0f; *negA = INFINITY; return; }                 // never
+    if (!(kappa < 0.1)) { *negB = -1e30f; *negA = 0.0f; return; }             // always
     const float C[3] = {(float)(0.5 * (lo[0] + hi[0])), (float)(0.5 * (lo[1] + hi[1])),
                         (float)(0.5 * (lo[2] + hi[2]))};
-    double R0 = 0.0, b = 0.0;
-    for (int i = 0; i < count; ++i) {
-        if (m[i].negA == INFINITY) continue;
-        const double A = -(double)m[i].negA, B = 1.0 - (double)m[i].onemB + 32.0 * eps;
-        const double dx = (double)m[i].cx - C[0], dy = (double)m[i].cy - C[1], dz = (double)m[i].cz - C[2];
-        const double dl = sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 1e-9);
-        R0 = fmax(R0, dl + sqrt(A) + sqrt(B) * dl);
-        b = fmax(b, sqrt(B));
-    }
+    double R2 = 0.0;
+    for (int i = 0; i < count; ++i)
+        for (int v = 0; v < 3; ++v) {
+            double d2 = 0.0;
+            for (int k = 0; k < 3; ++k) { const double q = (double)tri[3 * i + v][k] - C[k]; d2 += q * q; }
+            R2 = fmax(R2, d2);
+        }
     *cx = C[0]; *cy = C[1]; *cz = C[2];
-    round_test((1.0 + h) * R0 * R0 * (1.0 + 1e-6), (1.0 + 1.0 / h) * b * b + 64.0 * eps, onemB, negA);
+    const double ra = sqrt(R2 * (1.0 + 1e-6)) * (1.0 + kappa);
+    const double h = ra > 0.0 ? fmin(1.0, fmax(1e-3, kappa * S / ra)) : 1.0;
+    store_test((1.0 + h) * ra * ra, (1.0 + 1.0 / h) * kappa * kappa, negB, negA);
 }
 
 }  // namespace lpc

@@ -72,6 +72,7 @@ struct lpc_handle {
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
+    double scene_scale = 1.0;                        // half diagonal of the scene box (filter h)
     std::vector<int32_t> slot_run;
     std::vector<int32_t> meas_meshes;
     DBuf d_nodes, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
@@ -177,15 +178,15 @@ static inline uint64_t spread21(uint64_t x)
 
 // Per mesh run: a 4-wide sphere hierarchy built bottom-up over its triangles in
 // Morton order of the centroids (bottom nodes hold up to 4 triangles); every
-// node's test is cluster_record() of ALL triangles below it, so the slack does
-// not compound from level to level.  Triangles whose sphere test is degenerate
+// node's test is node_record() of ALL triangles below it (their vertices), so
+// the slack does not compound from level to level.  Triangles whose sphere test is degenerate
 // ("always", B >= 0.5) go to the run's sliver list (line filter, sliver_params)
 // instead; triangles that can never be hit are dropped.  Results do not depend
 // on the order (ties are resolved by triangle index).
-static FiltRec test_rec(float cx, float cy, float cz, float onemB, float negA)
+static FiltRec test_rec(float cx, float cy, float cz, float negB, float negA)
 {
     FiltRec r;
-    r.cx = cx; r.cy = cy; r.cz = cz; r.onemB = onemB; r.negA = negA; r.idx = -1; r.pad0 = r.pad1 = 0;
+    r.cx = cx; r.cy = cy; r.cz = cz; r.negB = negB; r.negA = negA; r.idx = -1; r.pad0 = r.pad1 = 0;
     return r;
 }
 
@@ -204,7 +205,7 @@ static int build_records(lpc_handle *h)
     h->node_self.clear();
     h->run_slo.clear(); h->run_shi.clear();
     h->n_slivers = 0;
-    const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 1.0f, INFINITY);
+    const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 0.0f, INFINITY);
     for (size_t r = 0; r < h->run_lo.size(); ++r) {
         const int32_t lo = h->run_lo[r], cnt_all = h->run_hi[r] - lo;
         std::vector<FiltRec> fr;
@@ -213,9 +214,10 @@ static int build_records(lpc_handle *h)
         double bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int32_t i = 0; i < cnt_all; ++i) {
             const size_t t = (size_t)(lo + i);
-            const FiltRec f = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap);
+            const FiltRec f = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap,
+                                            h->scene_scale);
             if (f.negA == INFINITY) continue;                     // never a candidate
-            if (f.onemB < -1e29f) { sl.push_back(lo + i); continue; }
+            if (f.negB < -1e29f) { sl.push_back(lo + i); continue; }
             fr.push_back(f);
             for (int k = 0; k < 3; ++k) {
                 const double c = ((double)h->hv0[4 * t + k] + h->hv1[4 * t + k] + h->hv2[4 * t + k]) / 3.0;
@@ -255,10 +257,15 @@ static int build_records(lpc_handle *h)
         std::vector<FiltRec> ord((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)key[(size_t)i].second];
         // every entry covers a contiguous range of `ord`; its test is
-        // cluster_record() of the triangles in that range
+        // node_record() of the triangles in that range
+        std::vector<const float *> tv((size_t)cnt * 3);
+        for (int32_t i = 0; i < cnt; ++i) {
+            const size_t t = (size_t)ord[(size_t)i].idx;
+            tv[3 * (size_t)i] = &h->hv0[4 * t]; tv[3 * (size_t)i + 1] = &h->hv1[4 * t]; tv[3 * (size_t)i + 2] = &h->hv2[4 * t];
+        }
         auto range_test = [&](int32_t a, int32_t b) {
             FiltRec t = never;
-            cluster_record(&ord[(size_t)a], b - a, &t.cx, &t.cy, &t.cz, &t.onemB, &t.negA);
+            node_record(&tv[3 * (size_t)a], b - a, h->scene_scale, &t.cx, &t.cy, &t.cz, &t.negB, &t.negA);
             return t;
         };
         struct Ent { FiltRec t; int32_t ref, a, b; };
@@ -275,7 +282,7 @@ static int build_records(lpc_handle *h)
                     const bool use = i + k < ent.size();
                     const FiltRec &m = use ? ent[i + k].t : never;
                     N.cx[k] = m.cx; N.cy[k] = m.cy; N.cz[k] = m.cz;
-                    N.onemB[k] = m.onemB; N.negA[k] = m.negA;
+                    N.negB[k] = m.negB; N.negA[k] = m.negA;
                     N.ref[k] = use ? ent[i + k].ref : ~0;
                 }
                 const int32_t a = ent[i].a, b = ent[std::min(i + 3, ent.size() - 1)].b;
@@ -344,7 +351,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
                 memset(&p, 0, sizeof(p));
                 p.root = L[2 * lv] + i;
                 const FiltRec &t = h->node_self[(size_t)p.root];
-                p.cx = t.cx; p.cy = t.cy; p.cz = t.cz; p.onemB = t.onemB; p.negA = t.negA;
+                p.cx = t.cx; p.cy = t.cy; p.cz = t.cz; p.negB = t.negB; p.negA = t.negA;
                 p.s_lo = p.s_hi = 0;
                 p.slot = run_slot[r];
                 pcs.push_back(p);
@@ -677,11 +684,14 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
                     const float v = (*vs)[4 * (size_t)i + k];
                     if (std::isfinite(v)) { lo3[k] = std::min(lo3[k], v); hi3[k] = std::max(hi3[k], v); }
                 }
+        double diag2 = 0.0;
         for (int k = 0; k < 3; ++k) {
             const float ext = hi3[k] - lo3[k];
             h->box_lo[k] = std::isfinite(lo3[k]) ? lo3[k] : 0.0f;
             h->box_scale[k] = (std::isfinite(ext) && ext > 0.0f) ? 32.0f / ext : 1.0f;
+            if (std::isfinite(ext)) diag2 += (double)ext * ext;
         }
+        h->scene_scale = diag2 > 0.0 ? 0.5 * sqrt(diag2) : 1.0;
     }
     h->dcap = 16.0;
     RETIF(build_records(h));

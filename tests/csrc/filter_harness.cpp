@@ -1,5 +1,5 @@
 // CPU harness for lpc_math.hpp (the header the HIP kernels include): evaluates the
-// bounding-sphere filter the way k_intersect does (fused multiply-adds in float)
+// bounding-sphere filter the way k_intersect does (plain and FMA-contracted float)
 // and the exact Moller-Trumbore acceptance, for property tests of the filter margin.
 #include <cmath>
 #include <cstring>
@@ -9,21 +9,43 @@
 
 using namespace lpc;
 
-extern "C" void filt_eval(int n, const float *O, const float *D, const float *V, float eps, double dcap,
+// filter_test with explicit FMAs (what the device compiler may contract to)
+static inline float filter_test_fma(float cx, float cy, float cz, float negB, float negA, const float *o, float nx,
+                                    float ny, float nz)
+{
+    const float wx = cx - o[0], wy = cy - o[1], wz = cz - o[2];
+    const float px = fmaf(wy, nz, -(wz * ny)), py = fmaf(wz, nx, -(wx * nz)), pz = fmaf(wx, ny, -(wy * nx));
+    const float pp = fmaf(pz, pz, fmaf(py, py, px * px));
+    const float ww = fmaf(wz, wz, fmaf(wy, wy, wx * wx));
+    return pp + fmaf(negB, ww, negA);
+}
+
+// max of the plain and the fused evaluation: a pair is a sure candidate only if
+// both pass
+static inline float eval_test(const float *o, float nx, float ny, float nz, float cx, float cy, float cz,
+                              float negB, float negA)
+{
+    const float a = filter_test(cx, cy, cz, negB, negA, o[0], o[1], o[2], nx, ny, nz);
+    const float b = filter_test_fma(cx, cy, cz, negB, negA, o, nx, ny, nz);
+    return a > b ? a : b;
+}
+
+static inline void unit_dir(const float *dd, float &nx, float &ny, float &nz)
+{
+    const float s = 1.0f / sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+    nx = dd[0] * s; ny = dd[1] * s; nz = dd[2] * s;
+}
+
+extern "C" void filt_eval(int n, const float *O, const float *D, const float *V, float eps, double dcap, double S,
                           float *d_out, int *hit_out, float *t_out)
 {
     for (int i = 0; i < n; ++i) {
         const float *o = O + 3 * i, *dd = D + 3 * i, *v = V + 9 * i;
         float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
-        FiltRec r = filter_record(v0, v1, v2, 0, dcap);
-        // k_intersect: unit direction, w = c - O, ww, wd, tq = negA - wd^2, d = ww*onemB + tq
-        float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
-        float nx = dd[0] * s, ny = dd[1] * s, nz = dd[2] * s;
-        float wx = r.cx - o[0], wy = r.cy - o[1], wz = r.cz - o[2];
-        float ww = fmaf(wz, wz, fmaf(wy, wy, wx * wx));
-        float wd = fmaf(wz, nz, fmaf(wy, ny, wx * nx));
-        float tq = fmaf(-wd, wd, r.negA);
-        d_out[i] = fmaf(ww, r.onemB, tq);
+        FiltRec r = filter_record(v0, v1, v2, 0, dcap, S);
+        float nx, ny, nz;
+        unit_dir(dd, nx, ny, nz);
+        d_out[i] = r.negB < -1e29f ? -1.0f : eval_test(o, nx, ny, nz, r.cx, r.cy, r.cz, r.negB, r.negA);
         f3 V0 = mk3(v[0], v[1], v[2]);
         f3 E1 = mk3(v[3] - v[0], v[4] - v[1], v[5] - v[2]);
         f3 E2 = mk3(v[6] - v[0], v[7] - v[1], v[8] - v[2]);
@@ -34,36 +56,30 @@ extern "C" void filt_eval(int n, const float *O, const float *D, const float *V,
     }
 }
 
-// Cluster test vs member tests: rays (n) x one cluster of m triangles.  Writes
-// each member's float test value (n*m) and the cluster's (n).
-static inline float eval_test(const float *o, float nx, float ny, float nz, float cx, float cy, float cz,
-                              float onemB, float negA)
+// Node test vs its triangles: rays (n) x one node over m triangles.  Writes each
+// triangle's exact Moller-Trumbore acceptance (n*m, t > eps) and the node's float
+// test value (n, the max of the plain and the fused evaluation).
+extern "C" void cluster_eval(int n, const float *O, const float *D, int m, const float *V, float eps, double S,
+                             int *hit_tri, float *d_cl)
 {
-    float wx = cx - o[0], wy = cy - o[1], wz = cz - o[2];
-    float ww = fmaf(wz, wz, fmaf(wy, wy, wx * wx));
-    float wd = fmaf(wz, nz, fmaf(wy, ny, wx * nx));
-    float tq = fmaf(-wd, wd, negA);
-    return fmaf(ww, onemB, tq);
-}
-
-extern "C" void cluster_eval(int n, const float *O, const float *D, int m, const float *V, double dcap,
-                             float *d_tri, float *d_cl)
-{
-    FiltRec rec[64];
-    for (int j = 0; j < m; ++j) {
-        const float *v = V + 9 * j;
-        float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
-        rec[j] = filter_record(v0, v1, v2, j, dcap);
-    }
-    float cx, cy, cz, ob, na;
-    cluster_record(rec, m, &cx, &cy, &cz, &ob, &na);
+    std::vector<const float *> tv((size_t)m * 3);
+    for (int j = 0; j < m; ++j)
+        for (int v = 0; v < 3; ++v) tv[3 * (size_t)j + v] = V + 9 * j + 3 * v;
+    float cx, cy, cz, nb, na;
+    node_record(tv.data(), m, S, &cx, &cy, &cz, &nb, &na);
     for (int i = 0; i < n; ++i) {
         const float *o = O + 3 * i, *dd = D + 3 * i;
-        float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
-        float nx = dd[0] * s, ny = dd[1] * s, nz = dd[2] * s;
-        for (int j = 0; j < m; ++j)
-            d_tri[(size_t)i * m + j] = eval_test(o, nx, ny, nz, rec[j].cx, rec[j].cy, rec[j].cz, rec[j].onemB, rec[j].negA);
-        d_cl[i] = eval_test(o, nx, ny, nz, cx, cy, cz, ob, na);
+        float nx, ny, nz;
+        unit_dir(dd, nx, ny, nz);
+        for (int j = 0; j < m; ++j) {
+            const float *v = V + 9 * j;
+            float t = 0.0f;
+            const int h = mt_exact(mk3(o[0], o[1], o[2]), mk3(dd[0], dd[1], dd[2]), mk3(v[0], v[1], v[2]),
+                                   mk3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), mk3(v[6] - v[0], v[7] - v[1], v[8] - v[2]),
+                                   &t);
+            hit_tri[(size_t)i * m + j] = h && t > eps;
+        }
+        d_cl[i] = nb < -1e29f ? -1.0f : eval_test(o, nx, ny, nz, cx, cy, cz, nb, na);
     }
 }
 
@@ -108,13 +124,13 @@ extern "C" void sliver_eval(int n, const float *O, const float *D, const float *
 }
 
 // filter_record's classification: 0 sphere test, 1 never, 2 always (-> sliver list)
-extern "C" void filt_class(int n, const float *V, double dcap, int *cls)
+extern "C" void filt_class(int n, const float *V, double dcap, double S, int *cls)
 {
     for (int i = 0; i < n; ++i) {
         const float *v = V + 9 * i;
         float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
-        FiltRec r = filter_record(v0, v1, v2, 0, dcap);
-        cls[i] = r.negA == INFINITY ? 1 : (r.onemB < -1e29f ? 2 : 0);
+        FiltRec r = filter_record(v0, v1, v2, 0, dcap, S);
+        cls[i] = r.negA == INFINITY ? 1 : (r.negB < -1e29f ? 2 : 0);
     }
 }
 
@@ -157,7 +173,7 @@ static PacketRec packet_build(int n, const float *O, const float *D)
 // test but the packet test fails), out[1] = (packet, record) pairs passing the
 // packet test, out[2] = pairs with some ray passing, out[3] = incoherent packets.
 extern "C" void packet_eval(int n, const float *O, const float *D, int pk, int m, const float *V, int kind,
-                            double dcap, long long *out)
+                            double dcap, double S, long long *out)
 {
     std::vector<FiltRec> recs;
     std::vector<SliverRec> sl;
@@ -172,16 +188,18 @@ extern "C" void packet_eval(int n, const float *O, const float *D, int pk, int m
             sliver_params(v0, v1, v2, &S.a, &S.b);
             sl.push_back(S);
         } else {
-            recs.push_back(filter_record(v0, v1, v2, j, dcap));
+            recs.push_back(filter_record(v0, v1, v2, j, dcap, S));
         }
     }
     if (kind == 1) {
         std::vector<FiltRec> cl;
-        for (size_t a = 0; a < recs.size(); a += 64) {
+        std::vector<const float *> tv((size_t)m * 3);
+        for (int j = 0; j < m; ++j)
+            for (int v = 0; v < 3; ++v) tv[3 * (size_t)j + v] = V + 9 * j + 3 * v;
+        for (int a = 0; a < m; a += 64) {
             FiltRec c;
             memset(&c, 0, sizeof(c));
-            cluster_record(&recs[a], (int)std::min<size_t>(64, recs.size() - a), &c.cx, &c.cy, &c.cz, &c.onemB,
-                           &c.negA);
+            node_record(&tv[3 * (size_t)a], std::min(64, m - a), S, &c.cx, &c.cy, &c.cz, &c.negB, &c.negA);
             cl.push_back(c);
         }
         recs.swap(cl);
@@ -208,12 +226,14 @@ extern "C" void packet_eval(int n, const float *O, const float *D, int pk, int m
                     any = fmaf(x, x, -(rhs * rhs)) <= 0.0f;
                 } else {
                     const FiltRec &r = recs[j];
-                    float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
-                    any = eval_test(o, dd[0] * s, dd[1] * s, dd[2] * s, r.cx, r.cy, r.cz, r.onemB, r.negA) <= 0.0f;
+                    float nx, ny, nz;
+                    unit_dir(dd, nx, ny, nz);
+                    any = filter_test(r.cx, r.cy, r.cz, r.negB, r.negA, o[0], o[1], o[2], nx, ny, nz) <= 0.0f ||
+                          filter_test_fma(r.cx, r.cy, r.cz, r.negB, r.negA, o, nx, ny, nz) <= 0.0f;
                 }
             }
             const bool pass = kind == 2 ? packet_sliver_test(Q, sl[j])
-                                        : packet_sphere_test(Q, recs[j].cx, recs[j].cy, recs[j].cz, recs[j].onemB,
+                                        : packet_sphere_test(Q, recs[j].cx, recs[j].cy, recs[j].cz, recs[j].negB,
                                                              recs[j].negA);
             out[1] += pass;
             out[2] += any;
@@ -224,23 +244,36 @@ extern "C" void packet_eval(int n, const float *O, const float *D, int pk, int m
 
 // Per-ray filter candidate count over m triangles (kernel evaluation of the
 // sphere test; "always" records are skipped, they go to the sliver list).
-extern "C" void cand_count(int n, const float *O, const float *D, int m, const float *V, double dcap, int *cnt)
+extern "C" void cand_count(int n, const float *O, const float *D, int m, const float *V, double dcap, double S,
+                           int *cnt)
 {
     std::vector<FiltRec> rec((size_t)m);
     for (int j = 0; j < m; ++j) {
         const float *v = V + 9 * j;
         float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
-        rec[(size_t)j] = filter_record(v0, v1, v2, j, dcap);
+        rec[(size_t)j] = filter_record(v0, v1, v2, j, dcap, S);
     }
     for (int i = 0; i < n; ++i) {
         const float *o = O + 3 * i, *dd = D + 3 * i;
-        float s = 1.0f / sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
+        float nx, ny, nz;
+        unit_dir(dd, nx, ny, nz);
         int c = 0;
         for (int j = 0; j < m; ++j) {
             const FiltRec &r = rec[(size_t)j];
-            if (r.onemB < -1e29f) continue;
-            c += eval_test(o, dd[0] * s, dd[1] * s, dd[2] * s, r.cx, r.cy, r.cz, r.onemB, r.negA) <= 0.0f;
+            if (r.negB < -1e29f) continue;
+            c += filter_test(r.cx, r.cy, r.cz, r.negB, r.negA, o[0], o[1], o[2], nx, ny, nz) <= 0.0f;
         }
         cnt[i] = c;
+    }
+}
+
+// Filter records of m triangles: (cx, cy, cz, negB, negA) each.
+extern "C" void filt_records(int m, const float *V, double dcap, double S, float *out)
+{
+    for (int j = 0; j < m; ++j) {
+        const float *v = V + 9 * j;
+        float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
+        const FiltRec r = filter_record(v0, v1, v2, j, dcap, S);
+        out[5 * j] = r.cx; out[5 * j + 1] = r.cy; out[5 * j + 2] = r.cz; out[5 * j + 3] = r.negB; out[5 * j + 4] = r.negA;
     }
 }

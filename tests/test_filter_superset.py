@@ -26,16 +26,16 @@ def harness():
     L = ctypes.CDLL(SO)
     P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
     I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
-    L.filt_eval.argtypes = [ctypes.c_int, P, P, P, ctypes.c_float, ctypes.c_double, P, I, P]
+    L.filt_eval.argtypes = [ctypes.c_int, P, P, P, ctypes.c_float, ctypes.c_double, ctypes.c_double, P, I, P]
     L.filt_eval.restype = None
 
-    def run(O, D, V, eps, dcap=16.0):
+    def run(O, D, V, eps, dcap=16.0, S=1000.0):
         n = O.shape[0]
         d = np.zeros(n, np.float32)
         h = np.zeros(n, np.int32)
         t = np.zeros(n, np.float32)
         L.filt_eval(n, np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32),
-                    np.ascontiguousarray(V, np.float32), np.float32(eps), dcap, d, h, t)
+                    np.ascontiguousarray(V, np.float32), np.float32(eps), dcap, S, d, h, t)
         return d, h.astype(bool), t
     return run
 
@@ -79,10 +79,12 @@ def adversarial(rng, n, scale, dist, aspect, graze, tiny_shift):
 def test_filter_is_superset_of_exact(harness, scale, dist, aspect, graze):
     rng = np.random.default_rng(int(scale * 1000 + dist + aspect * 7 + graze * 100))
     O, D, V = adversarial(rng, 200_000, scale, dist, aspect, graze, tiny_shift=1e-6)
-    d, hit, t = harness(O, D, V, eps=1e-6 * dist)
-    assert hit.sum() > 1000                     # the cases do exercise accepted hits
-    lost = hit & ~(d <= 0)
-    assert not lost.any(), f"{lost.sum()} exact hits rejected by the filter"
+    # the per-record split h depends on the assumed scene scale S; every S must hold
+    for S in (dist, 1.0, 1e5):
+        d, hit, t = harness(O, D, V, eps=1e-6 * dist, S=S)
+        assert hit.sum() > 1000                 # the cases do exercise accepted hits
+        lost = hit & ~(d <= 0)
+        assert not lost.any(), f"S={S}: {lost.sum()} exact hits rejected by the filter"
 
 
 def test_filter_rejects_most_far_misses(harness):
@@ -110,25 +112,27 @@ def test_degenerate_triangles_never_candidates(harness):
 def cluster_harness(harness):
     L = ctypes.CDLL(SO)
     P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
-    L.cluster_eval.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_double, P, P]
+    I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+    L.cluster_eval.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_float, ctypes.c_double, I, P]
     L.cluster_eval.restype = None
 
-    def run(O, D, V, dcap=16.0):
+    def run(O, D, V, eps, S=1000.0):
         n, m = O.shape[0], V.shape[0]
-        dt = np.zeros(n * m, np.float32)
+        ht = np.zeros(n * m, np.int32)
         dc = np.zeros(n, np.float32)
         L.cluster_eval(n, np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32), m,
-                       np.ascontiguousarray(V, np.float32), dcap, dt, dc)
-        return dt.reshape(n, m), dc
+                       np.ascontiguousarray(V, np.float32), np.float32(eps), S, ht, dc)
+        return ht.reshape(n, m).astype(bool), dc
     return run
 
 
 @pytest.mark.parametrize("name", ["lens", "eye", "synthetic", "parabolic"])
-def test_cluster_test_implied_by_member_tests(cluster_harness, name):
-    """Every ray whose test passes for some triangle of a 64-triangle cluster must
-    pass the cluster's test (k_intersect skips the cluster's triangles otherwise).
-    Clusters are consecutive triangles of the real scenes' meshes; rays are aimed
-    at those triangles from near and far origins."""
+def test_node_test_passes_for_every_accepted_triangle(cluster_harness, name):
+    """Every ray whose line the exact test accepts against some triangle of a
+    64-triangle node must pass the node's test (k_intersect skips the node's
+    triangles otherwise).  Nodes are consecutive triangles of the real scenes'
+    meshes; rays are aimed at those triangles (and their edges) from near and far
+    origins, including grazing ones."""
     from lightpycl_amd import scenes
     from lightpycl_amd.engine import flatten_meshes
     sc = scenes.BUILDERS[name](n=8, seed=1)
@@ -141,15 +145,17 @@ def test_cluster_test_implied_by_member_tests(cluster_harness, name):
         bu, bv = rng.random(2000), rng.random(2000)
         flip = bu + bv > 1
         bu[flip], bv[flip] = 1 - bu[flip], 1 - bv[flip]
+        edge = rng.random(2000) < 0.3
+        bv[edge] = 1 - bu[edge]                    # on the far edge
         tgt = V[j, :3] + bu[:, None] * (V[j, 3:6] - V[j, :3]) + bv[:, None] * (V[j, 6:9] - V[j, :3])
-        tgt += rng.normal(size=tgt.shape) * np.abs(V).max() * 1e-3
         O = (tgt + rng.normal(size=tgt.shape) * rng.choice([1e-2, 1.0, 1e2, 1e3], (2000, 1))).astype(np.float32)
         D = (tgt - O)
         D /= np.linalg.norm(D, axis=1, keepdims=True)
-        dt, dc = cluster_harness(O, D.astype(np.float32), V.astype(np.float32))
-        tri_pass = (dt <= 0).any(axis=1)
-        assert not (tri_pass & ~(dc <= 0)).any()
-        checked += int(tri_pass.sum())
+        for S in (1.0, 1e3):
+            ht, dc = cluster_harness(O, D.astype(np.float32), V.astype(np.float32), 1e-6, S=S)
+            acc = ht.any(axis=1)
+            assert not (acc & ~(dc <= 0)).any()
+            checked += int(acc.sum())
     assert checked > 10000
 
 
@@ -160,7 +166,7 @@ def sliver_harness(harness):
     I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
     L.sliver_eval.argtypes = [ctypes.c_int, P, P, P, ctypes.c_float, ctypes.c_int, P, I, P]
     L.sliver_eval.restype = None
-    L.filt_class.argtypes = [ctypes.c_int, P, ctypes.c_double, I]
+    L.filt_class.argtypes = [ctypes.c_int, P, ctypes.c_double, ctypes.c_double, I]
     L.filt_class.restype = None
 
     def run(O, D, V, eps, fused):
@@ -172,9 +178,9 @@ def sliver_harness(harness):
                       np.ascontiguousarray(V, np.float32), np.float32(eps), int(fused), d, h, t)
         return d, h.astype(bool), t
 
-    def classify(V, dcap=16.0):
+    def classify(V, dcap=16.0, S=1000.0):
         c = np.zeros(V.shape[0], np.int32)
-        L.filt_class(V.shape[0], np.ascontiguousarray(V, np.float32), dcap, c)
+        L.filt_class(V.shape[0], np.ascontiguousarray(V, np.float32), dcap, S, c)
         return c
     run.classify = classify
     return run
@@ -259,13 +265,14 @@ def packet_harness(harness):
     L = ctypes.CDLL(SO)
     P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
     Q = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
-    L.packet_eval.argtypes = [ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_double, Q]
+    L.packet_eval.argtypes = [ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_double,
+                              ctypes.c_double, Q]
     L.packet_eval.restype = None
 
-    def run(O, D, V, kind, pk=128, dcap=16.0):
+    def run(O, D, V, kind, pk=128, dcap=16.0, S=1000.0):
         out = np.zeros(4, np.int64)
         L.packet_eval(O.shape[0], np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32), pk,
-                      V.shape[0], np.ascontiguousarray(V, np.float32), kind, dcap, out)
+                      V.shape[0], np.ascontiguousarray(V, np.float32), kind, dcap, S, out)
         return dict(violations=int(out[0]), packet_pass=int(out[1]), ray_pass=int(out[2]), incoherent=int(out[3]))
     return run
 
