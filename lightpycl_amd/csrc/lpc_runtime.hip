@@ -165,19 +165,34 @@ static inline unsigned grid1(int64_t n, int bs = 256) { return (unsigned)((n + b
 
 // ---------------------------------------------------------------------------
 // scene records
-static inline uint64_t spread21(uint64_t x)
+// Top-down partition of idx[0, n) for a subtree of capacity cap (4 * 2^k): split
+// at min(n, cap/2) along the longest axis of the centroids' bbox (nth_element),
+// recurse on both halves with cap/2, down to groups of 4.
+static void split_order(int32_t *idx, int64_t n, int64_t cap, const std::vector<double> &cen)
 {
-    x &= 0x1fffff;
-    x = (x | x << 32) & 0x1f00000000ffffull;
-    x = (x | x << 16) & 0x1f0000ff0000ffull;
-    x = (x | x << 8) & 0x100f00f00f00f00full;
-    x = (x | x << 4) & 0x10c30c30c30c30c3ull;
-    x = (x | x << 2) & 0x1249249249249249ull;
-    return x;
+    if (cap <= 4 || n <= 1) return;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            const double c = cen[3 * (size_t)idx[i] + k];
+            if (std::isfinite(c)) { lo[k] = std::min(lo[k], c); hi[k] = std::max(hi[k], c); }
+        }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (hi[k] - lo[k] > hi[ax] - lo[ax]) ax = k;
+    const int64_t half = std::min(n, cap / 2);
+    if (half < n)
+        std::nth_element(idx, idx + half, idx + n, [&](int32_t a, int32_t b) {
+            const double ca = cen[3 * (size_t)a + ax], cb = cen[3 * (size_t)b + ax];
+            return ca < cb || (ca == cb && a < b);
+        });
+    split_order(idx, half, cap / 2, cen);
+    split_order(idx + half, n - half, cap / 2, cen);
 }
 
 // Per mesh run: a 4-wide sphere hierarchy built bottom-up over its triangles in
-// Morton order of the centroids (bottom nodes hold up to 4 triangles); every
+// a top-down median-split order (split_order; bottom nodes hold up to 4
+// triangles); every
 // node's test is node_record() of ALL triangles below it (their vertices), so
 // the slack does not compound from level to level.  Triangles whose sphere test is degenerate
 // ("always", B >= 0.5) go to the run's sliver list (line filter, sliver_params)
@@ -211,7 +226,6 @@ static int build_records(lpc_handle *h)
         std::vector<FiltRec> fr;
         std::vector<double> cen;
         std::vector<int32_t> sl;
-        double bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int32_t i = 0; i < cnt_all; ++i) {
             const size_t t = (size_t)(lo + i);
             const FiltRec f = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap,
@@ -222,7 +236,6 @@ static int build_records(lpc_handle *h)
             for (int k = 0; k < 3; ++k) {
                 const double c = ((double)h->hv0[4 * t + k] + h->hv1[4 * t + k] + h->hv2[4 * t + k]) / 3.0;
                 cen.push_back(c);
-                if (std::isfinite(c)) { bl[k] = std::min(bl[k], c); bh[k] = std::max(bh[k], c); }
             }
         }
         h->run_slo.push_back((int32_t)slivers.size());
@@ -243,19 +256,15 @@ static int build_records(lpc_handle *h)
         h->run_levels.push_back(std::vector<int32_t>());
         const int32_t cnt = (int32_t)fr.size();
         if (cnt == 0) continue;
-        std::vector<std::pair<uint64_t, int32_t>> key((size_t)cnt);
-        for (int32_t i = 0; i < cnt; ++i) {
-            uint64_t q[3];
-            for (int k = 0; k < 3; ++k) {
-                const double ext = bh[k] - bl[k];
-                const double v = ext > 0 ? (cen[3 * (size_t)i + k] - bl[k]) / ext : 0.0;
-                q[k] = (uint64_t)std::min(std::max(v * 2097151.0, 0.0), 2097151.0);
-            }
-            key[(size_t)i] = {spread21(q[0]) | spread21(q[1]) << 1 | spread21(q[2]) << 2, i};
-        }
-        std::sort(key.begin(), key.end());
+        // top-down order: every aligned group of 4^k triangles is one median-split
+        // cluster, so the bottom-up 4-wide grouping below reproduces that tree
+        std::vector<int32_t> perm_t((size_t)cnt);
+        for (int32_t i = 0; i < cnt; ++i) perm_t[(size_t)i] = i;
+        int64_t cap = 4;
+        while (cap < cnt) cap *= 4;
+        split_order(perm_t.data(), cnt, cap, cen);
         std::vector<FiltRec> ord((size_t)cnt);
-        for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)key[(size_t)i].second];
+        for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)perm_t[(size_t)i]];
         // every entry covers a contiguous range of `ord`; its test is
         // node_record() of the triangles in that range
         std::vector<const float *> tv((size_t)cnt * 3);
