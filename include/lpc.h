@@ -179,9 +179,15 @@ typedef struct {
     int64_t tail_exact;      /* their exact tests                               */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
- * k_intersect traversal counters (2, diagnostic: adds atomics), or disable (0). */
+ * k_intersect traversal counters (2, diagnostic: adds atomics), timing plus
+ * per-wave records of the grid traversal (3, diagnostic), or disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
+/* Level 3: the last k_intersect launch's per-(piece, packet) records, 4 uint32
+ * each {wall-clock ticks (100 MHz), hierarchy nodes visited, exact tests,
+ * piece}, ordered [piece][packet]; *count = records available, at most `cap`
+ * are copied into rec4 (may be NULL to query the count). */
+int lpc_prof_waves(lpc_handle *h, uint32_t *rec4, int64_t cap, int64_t *count);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,7 @@ _PROTOS = {
                          _P],
     "lpc_prof_enable": [_P, _INT],
     "lpc_prof_read": [_P, _P, _INT],
+    "lpc_prof_waves": [_P, _P, _I64, _P],
 }
 
 EXPORTED = tuple(_PROTOS) + ("lpc_last_error",)

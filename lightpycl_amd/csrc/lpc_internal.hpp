@@ -38,6 +38,17 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 #define LPC_STATS_PIECES 4096
 #define LPC_STATS_WORDS (LPC_STATS_PIECE + LPC_STATS_PIECES)
 
+// Per-launch device words of the intersect stage (uint32, reset by k_slot_init):
+// [0..5] population origin box (k_bbox, coherence key modes 1-2).
+#define LPC_MISC_WORDS 8
+
+// A fan group met by a k_intersect wave (packet, piece): group id and the rays
+// that passed the group's test; k_groups processes them.
+struct GItem {
+    int32_t g, pad;
+    uint64_t m;
+};
+
 struct RaysIn {                       // a ray population (SoA)
     const float *ox, *oy, *oz, *dx, *dy, *dz, *pw;
     const int32_t *pmid;              // previous intersected mesh (-2 emitted, -1 outside)

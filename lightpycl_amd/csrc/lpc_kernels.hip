@@ -1,11 +1,14 @@
 // lpc_kernels.hip -- gfx950 kernels of the LightPyCL per-bounce path.
 //
-//   k_packet         per-wave bound (origin ball + direction cone) of 128 rays.
+//   k_packet         per-wave bound (origin ball + direction cone) of 64 or 128 rays.
 //   k_intersect      the hot loop (replaces __kernel intersect, .cl:243-289):
-//                    packet-culled cluster -> triangle traversal of one "piece"
-//                    (part of one mesh run), per-ray conservative sphere tests,
-//                    exact Moller-Trumbore only for candidates -> per-slot
-//                    nearest hit (64-bit atomicMin) and hit count.
+//                    (packet, piece) waves walk a piece's sphere hierarchy for
+//                    64 rays at once, per-ray conservative tests, exact
+//                    Moller-Trumbore only for candidates -> per-slot nearest hit
+//                    (64-bit atomicMin) and hit count; fan groups met on the
+//                    way are deferred to k_groups.
+//   k_groups         fan groups (thin triangles around revolve poles) lane-
+//                    parallel per packet, exact tests one ray per lane.
 //   k_gather         rays into coherence order (after k_raykey + radix sort).
 //   k_slot_init/k_slot_export
 //                    per-mesh scratch slots (.cl:260-288): pieces flush their
@@ -38,7 +41,8 @@ namespace lpck {
 // the per-mesh slots with order-independent atomics (slot_flush), so the kernels
 // and their pieces may run in any order:
 //   k_intersect  a mesh run's sphere hierarchy (filter_test), 64-ray packets;
-//   k_packet     per-wave bound of 128 rays (origin ball + direction cone);
+//   k_groups     the fan groups the traversal met;
+//   k_packet     per-wave bound of 64 / 128 rays (origin ball + direction cone);
 //   k_slivers    the runs' slivers: lane-parallel packet_sliver_test, then the
 //                per-ray line filter.
 // Every filter level is implied by the one below it and the lowest one by the
@@ -65,18 +69,23 @@ static __device__ __forceinline__ T wave_red(T v, int op)   // 0 min, 1 max, 2 s
     return v;
 }
 
-// Packet bound of each 128-ray wave (one wave per packet, same ray->lane map as
-// k_intersect).
+// Packet bound of each wave of 64 * RPL rays (one wave per packet; ray
+// w*64*RPL + r*64 + lane on lane `lane`, the map of k_intersect (RPL 1) and
+// k_slivers (RPL 2)).
+template <int RPL>
 __global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                 PacketRec *__restrict__ pk)
 {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w * 128 >= n) return;
-    const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
-    const int64_t q[2] = {s0 < n ? s0 : n - 1, s1 < n ? s1 : n - 1};
-    float o[2][3], d[2][3];
-    for (int r = 0; r < 2; ++r) {
+    if (w * 64 * RPL >= n) return;
+    int64_t q[RPL];
+    for (int r = 0; r < RPL; ++r) {
+        const int64_t s = w * 64 * RPL + r * 64 + lane;
+        q[r] = s < n ? s : n - 1;
+    }
+    float o[RPL][3], d[RPL][3];
+    for (int r = 0; r < RPL; ++r) {
         if (rs) {
             for (int k = 0; k < 3; ++k) { o[r][k] = rs[k * n + q[r]]; d[r][k] = rs[(3 + k) * n + q[r]]; }
         } else {
@@ -84,11 +93,14 @@ __global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restric
             d[r][0] = R.dx[q[r]]; d[r][1] = R.dy[q[r]]; d[r][2] = R.dz[q[r]];
         }
     }
-    float mn[3], mx[3], nrm[2][3];
+    float mn[3], mx[3], nrm[RPL][3];
     int fin = 1;
     float sx = 0.0f, sy = 0.0f, sz = 0.0f;
-    for (int k = 0; k < 3; ++k) { mn[k] = fminf(o[0][k], o[1][k]); mx[k] = fmaxf(o[0][k], o[1][k]); }
-    for (int r = 0; r < 2; ++r) {
+    for (int k = 0; k < 3; ++k) {
+        mn[k] = o[0][k]; mx[k] = o[0][k];
+        for (int r = 1; r < RPL; ++r) { mn[k] = fminf(mn[k], o[r][k]); mx[k] = fmaxf(mx[k], o[r][k]); }
+    }
+    for (int r = 0; r < RPL; ++r) {
         const float l = sqrtf(d[r][0] * d[r][0] + d[r][1] * d[r][1] + d[r][2] * d[r][2]);
         fin &= (l > 0.0f && l < INFINITY && fabsf(o[r][0] + o[r][1] + o[r][2]) < INFINITY) ? 1 : 0;
         for (int k = 0; k < 3; ++k) nrm[r][k] = d[r][k] / l;
@@ -100,14 +112,15 @@ __global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restric
     PacketRec Q;
     packet_centre(mn, mx, Q);
     float rr = 0.0f;
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < RPL; ++r) {
         const float x = o[r][0] - Q.ox, y = o[r][1] - Q.oy, z = o[r][2] - Q.oz;
         rr = fmaxf(rr, sqrtf(x * x + y * y + z * z));
     }
     rr = wave_red(rr, 1);
     packet_finish(rr, sx, sy, sz, Q);
-    float ang = fmaxf(packet_angle(nrm[0][0], nrm[0][1], nrm[0][2], Q.ax, Q.ay, Q.az),
-                      packet_angle(nrm[1][0], nrm[1][1], nrm[1][2], Q.ax, Q.ay, Q.az));
+    float ang = packet_angle(nrm[0][0], nrm[0][1], nrm[0][2], Q.ax, Q.ay, Q.az);
+    for (int r = 1; r < RPL; ++r)
+        ang = fmaxf(ang, packet_angle(nrm[r][0], nrm[r][1], nrm[r][2], Q.ax, Q.ay, Q.az));
     if (!(ang == ang)) ang = INFINITY;
     ang = wave_red(ang, 1);
     packet_angle_finish(ang, fin != 0, Q);
@@ -140,13 +153,6 @@ static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__
 // Stack depth per wave (node refs); the host checks every hierarchy fits.
 #define LPC_STACK 32
 
-// k_intersect: packets of 64 rays of the coherence order (one per lane),
-// grid = (ceil(n/256), pieces), block = 4 waves.  A wave walks the piece's
-// subtree with a wave-uniform stack in LDS: a node's four children are tested
-// against all 64 rays (filter form d <= 0, see filter_record; node data
-// wave-uniform through the scalar cache); a child node is pushed when any ray
-// passes it, a child triangle gets the exact Moller-Trumbore test for the rays
-// that pass its own test.
 // k-th set bit (0-based) of m.
 static __device__ __forceinline__ int select_bit(uint64_t m, int k)
 {
@@ -159,40 +165,52 @@ static __device__ __forceinline__ int select_bit(uint64_t m, int k)
     return pos;
 }
 
-__global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                   const int32_t *__restrict__ perm,
+// LDS of one wave's traversal.
+struct WaveLds {
+    int32_t stack[LPC_STACK];
+    int32_t qidx[64], qscan[64];
+    uint64_t qmask[64];
+    float ray[6][64];                  // the packet's rays (O, D) for the drain
+    unsigned long long lkey[64];       // per-ray nearest hit (slot_key)
+    int32_t lcnt[64];                  // per-ray hit count
+};
+
+// One packet (64 rays of the coherence order from w*64, one per lane) against
+// one piece (a subtree of one mesh run).  The wave walks the subtree with a
+// wave-uniform stack in LDS: a node's four children are tested against all 64
+// rays (filter form d <= 0, see filter_record; node data wave-uniform through
+// the scalar cache); a child node is pushed when any ray passes it, a child
+// triangle's (index, lane mask) is queued for the exact test.
+static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, const float *__restrict__ rs,
+                                                   int64_t n, const int32_t *__restrict__ perm,
                                                    const Node4 *__restrict__ nodes,
-                                                   const ExactRec *__restrict__ xrec,
-                                                   const Piece *__restrict__ pieces, float eps,
+                                                   const ExactRec *__restrict__ xrec, GItem *__restrict__ gitems,
+                                                   int32_t *__restrict__ gcount, int gmax, int64_t gslot,
+                                                   const Piece &P, int64_t w, int piece_id, float eps,
                                                    float max_ray_len,
                                                    unsigned long long *__restrict__ skey,
                                                    int32_t *__restrict__ scnt,
-                                                   unsigned long long *__restrict__ stats)
+                                                   unsigned long long *__restrict__ stats,
+                                                   uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0)
 {
-    __shared__ int32_t stack[4][LPC_STACK];
-    __shared__ int32_t qidx[4][64], qscan[4][64];
-    __shared__ uint64_t qmask[4][64];
-    __shared__ float ray[4][6][64];                // the wave's rays (O, D) for the drain
-    __shared__ unsigned long long lkey[4][64];     // per-ray nearest hit (slot_key)
-    __shared__ int32_t lcnt[4][64];                // per-ray hit count
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
-    if (w * 64 >= n) return;                       // whole wave past the end
+    const int lane = threadIdx.x & 63;
     const int64_t s = w * 64 + lane;
     f3 O, D;
     load_ray(R, rs, n, s < n ? s : n - 1, O, D);
     // unit direction for the filter only (its rounding is inside the margin)
     const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
     const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
-    const Piece P = pieces[blockIdx.y];
-    ray[wv][0][lane] = O.x; ray[wv][1][lane] = O.y; ray[wv][2][lane] = O.z;
-    ray[wv][3][lane] = D.x; ray[wv][4][lane] = D.y; ray[wv][5][lane] = D.z;
+    if (!(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f))) {
+        if (gcount && lane == 0) gcount[gslot] = 0;
+        return;
+    }
+    L.ray[0][lane] = O.x; L.ray[1][lane] = O.y; L.ray[2][lane] = O.z;
+    L.ray[3][lane] = D.x; L.ray[4][lane] = D.y; L.ray[5][lane] = D.z;
     const unsigned long long key0 = slot_key(max_ray_len, -1);
-    lkey[wv][lane] = key0;
-    lcnt[wv][lane] = 0;
+    L.lkey[lane] = key0;
+    L.lcnt[lane] = 0;
 
-    const uint64_t clk0 = stats ? wall_clock64() : 0;
-    int32_t *stk = stack[wv];
+    const uint64_t clk0 = (stats || wrec) ? wall_clock64() : 0;
     int32_t top = 0, nq = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
     // Exact tests are deferred: candidate (triangle, ray lanes) entries queue up
@@ -203,13 +221,13 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
     auto drain = [&]() {
         if (nq == 0) return;
-        const int pc = lane < nq ? __builtin_popcountll(qmask[wv][lane]) : 0;
+        const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
         int incl = pc;
         for (int o = 1; o < 64; o <<= 1) {
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        qscan[wv][lane] = incl;
+        L.qscan[lane] = incl;
         const int total = __shfl(incl, 63, 64);
         for (int base = 0; base < total; base += 64) {
             const int q = base + lane;
@@ -217,28 +235,28 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
                 int e = 0;                         // first entry with qscan[e] > q
 #pragma unroll
                 for (int step = 32; step >= 1; step >>= 1)
-                    if (e + step <= 63 && qscan[wv][e + step - 1] <= q) e += step;
-                const int k = q - (e > 0 ? qscan[wv][e - 1] : 0);
-                const int r = select_bit(qmask[wv][e], k);
-                const int32_t idx = qidx[wv][e];
+                    if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
+                const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
+                const int r = select_bit(L.qmask[e], k);
+                const int32_t idx = L.qidx[e];
                 const ExactRec x = xrec[idx];
-                const f3 Or = mk3(ray[wv][0][r], ray[wv][1][r], ray[wv][2][r]);
-                const f3 Dr = mk3(ray[wv][3][r], ray[wv][4][r], ray[wv][5][r]);
+                const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
+                const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
                 float t;
                 if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
                     t > eps) {
-                    atomicAdd(&lcnt[wv][r], 1);
-                    if (t < max_ray_len) atomicMin(&lkey[wv][r], slot_key(t, idx));
+                    atomicAdd(&L.lcnt[r], 1);
+                    if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
                 }
                 ++n_exact;
             }
         }
         nq = 0;
     };
-    if (P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f))
-        stk[top++] = P.root;
+    int ngr = 0;                                   // fan groups deferred to k_groups
+    L.stack[top++] = P.root;
     while (top > 0) {
-        const int32_t node = __builtin_amdgcn_readfirstlane(stk[--top]);
+        const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
         const Node4 N = nodes[node];
         ++n_nodes;
         float d[4];
@@ -248,14 +266,25 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
         if (N.ref[0] >= 0) {                       // internal node: children are nodes
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (any_lane(d[k] <= 0.0f)) stk[top++] = N.ref[k];
-        } else {                                   // leaf: children are triangles -> queue
+                if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
+        } else {                                   // leaf: triangles -> queue, fan groups -> k_groups
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
                 if (!m) continue;
-                if (lane == 0) { qidx[wv][nq] = ~N.ref[k]; qmask[wv][nq] = m; }
-                if (++nq == 64) drain();
+                const int32_t ref = N.ref[k];
+                if (ref >= LPC_GROUP_REF) {
+                    if (lane == 0) { L.qidx[nq] = ~ref; L.qmask[nq] = m; }
+                    if (++nq == 64) drain();
+                } else {
+                    // the host sizes gmax to the piece's group count: never full
+                    if (lane == 0 && ngr < gmax) {
+                        GItem gi;
+                        gi.g = LPC_GROUP_REF - 1 - ref; gi.pad = 0; gi.m = m;
+                        gitems[gslot * gmax + ngr] = gi;
+                    }
+                    ++ngr;
+                }
             }
         }
     }
@@ -278,16 +307,105 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
             atomicAdd(&stats[2], 1ull);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
             atomicAdd(&stats[LPC_STATS_HIST + b], 1ull);
-            if (blockIdx.y < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + blockIdx.y], (unsigned long long)dt);
+            if (piece_id < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + piece_id], (unsigned long long)dt);
+        }
+    }
+    if (gcount && lane == 0) gcount[gslot] = ngr;
+    if (wrec) {                                // per-wave record (diagnostic, no contention)
+        for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
+        if (lane == 0) {
+            uint32_t *r = wrec + 4 * ridx;
+            r[0] = (uint32_t)(wall_clock64() - clk0); r[1] = n_nodes; r[2] = n_exact; r[3] = (uint32_t)piece_id;
         }
     }
     if (s < n) {
-        const unsigned long long k = lkey[wv][lane];
-        const int32_t c = lcnt[wv][lane];
+        const unsigned long long k = L.lkey[lane];
+        const int32_t c = L.lcnt[lane];
         const int64_t o = (int64_t)P.slot * n, q = perm ? perm[s] : s;
         if (c) atomicAdd(&scnt[o + q], c);
         if (k != key0) atomicMin(&skey[o + q], k);
     }
+}
+
+// k_intersect: grid = (ceil(n/256), pieces), block = 4 waves, one (packet,
+// piece) per wave.
+__global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                   const int32_t *__restrict__ perm,
+                                                   const Node4 *__restrict__ nodes,
+                                                   const ExactRec *__restrict__ xrec,
+                                                   GItem *__restrict__ gitems, int32_t *__restrict__ gcount,
+                                                   int gmax, const Piece *__restrict__ pieces, float eps,
+                                                   float max_ray_len,
+                                                   unsigned long long *__restrict__ skey,
+                                                   int32_t *__restrict__ scnt,
+                                                   unsigned long long *__restrict__ stats,
+                                                   uint32_t *__restrict__ wrec)
+{
+    __shared__ WaveLds lds[4];
+    const int wv = threadIdx.x >> 6;
+    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+    if (w * 64 >= n) return;                       // whole wave past the end
+    const Piece P = pieces[blockIdx.y];
+    trav_packet(lds[wv], R, rs, n, perm, nodes, xrec, gitems, gcount, gmax,
+                (int64_t)blockIdx.y * ((n + 63) / 64) + w, P, w, (int)blockIdx.y, eps, max_ray_len,
+                skey, scnt, stats,
+                wrec, (int64_t)blockIdx.y * ((n + 63) / 64) + w);
+}
+
+// k_groups: the fan groups k_intersect's wave (packet w, piece y) met, same
+// grid.  Per group: members' filter and exact records load lane-parallel, the
+// members are tested against the packet bound (packet_sphere_test), then each
+// candidate per ray (only the rays of the item's mask can hit a member: the
+// group's own test is node_record() of its members) and the exact test runs
+// one ray per lane from the broadcast record -- no gather, no queue.
+__global__ __launch_bounds__(256) void k_groups(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                const int32_t *__restrict__ perm,
+                                                const FiltRec *__restrict__ grec,
+                                                const ExactRec *__restrict__ gxrec,
+                                                const PacketRec *__restrict__ pk64,
+                                                const Piece *__restrict__ pieces,
+                                                const GItem *__restrict__ gitems,
+                                                const int32_t *__restrict__ gcount, int gmax, float eps,
+                                                float max_ray_len, unsigned long long *__restrict__ skey,
+                                                int32_t *__restrict__ scnt)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t npk = (n + 63) / 64;
+    if (w >= npk) return;
+    const int64_t gslot = (int64_t)blockIdx.y * npk + w;
+    const int items = min(gcount[gslot], gmax);
+    if (items == 0) return;
+    const int64_t s = w * 64 + lane;
+    f3 O, D;
+    load_ray(R, rs, n, s < n ? s : n - 1, O, D);
+    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
+    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+    const PacketRec Q = pk64[w];
+    float tmin = max_ray_len;
+    int32_t imin = -1, cnt = 0;
+    for (int it = 0; it < items; ++it) {
+        const GItem I = gitems[gslot * gmax + it];
+        const int64_t gi = (int64_t)I.g * LPC_GROUP_SIZE + lane;
+        const FiltRec f = grec[gi];
+        uint64_t cm = __builtin_amdgcn_ballot_w64(packet_sphere_test(Q, f.cx, f.cy, f.cz, f.negB, f.negA));
+        if (!cm) continue;
+        const ExactRec x = gxrec[gi];
+        while (cm) {
+            const int j = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const float dj = filter_test(bcast(f.cx, j), bcast(f.cy, j), bcast(f.cz, j), bcast(f.negB, j),
+                                         bcast(f.negA, j), O.x, O.y, O.z, nx, ny, nz);
+            const uint64_t mm = __builtin_amdgcn_ballot_w64(dj <= 0.0f) & I.m;
+            if (!mm) continue;
+            const int32_t idx = bcasti(f.idx, j);
+            const f3 V0 = mk3(bcast(x.v0x, j), bcast(x.v0y, j), bcast(x.v0z, j));
+            const f3 E1 = mk3(bcast(x.e1x, j), bcast(x.e1y, j), bcast(x.e1z, j));
+            const f3 E2 = mk3(bcast(x.e2x, j), bcast(x.e2y, j), bcast(x.e2z, j));
+            if ((mm >> lane) & 1ull) mt_accumulate(O, D, V0, E1, E2, idx, eps, tmin, imin, cnt);
+        }
+    }
+    if (s < n) slot_flush(skey, scnt, (int64_t)pieces[blockIdx.y].slot * n, perm ? perm[s] : s, tmin, imin, cnt);
 }
 
 // k_slivers: the run's slivers (line filter) for packets of 128 rays (two per
@@ -376,12 +494,13 @@ __global__ __launch_bounds__(256) void k_gather(RaysIn R, int64_t n, const int32
 
 // Slot initial state: slots a run flushes into start at (max_ray_len, idx -1,
 // count 0); slots no run writes keep the reference's initial scratch
-// (max_ray_len, idx 0, count 0).
+// (max_ray_len, idx 0, count 0).  Also empties the launch's origin box (misc).
 __global__ __launch_bounds__(256) void k_slot_init(int64_t n, int32_t K, const int32_t *__restrict__ live,
                                                    float max_ray_len, unsigned long long *__restrict__ skey,
-                                                   int32_t *__restrict__ scnt)
+                                                   int32_t *__restrict__ scnt, uint32_t *__restrict__ misc)
 {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (misc && r < LPC_MISC_WORDS) misc[r] = r < 3 ? 0xffffffffu : 0u;
     if (r >= n) return;
     for (int32_t j = 0; j < K; ++j) {
         skey[(int64_t)j * n + r] = slot_key(max_ray_len, live[j] ? -1 : 0);
@@ -408,8 +527,8 @@ __global__ __launch_bounds__(256) void k_slot_export(int64_t n, int32_t K, const
     }
 }
 
-// Ray coherence key: 15-bit Morton code of the origin cell (32^3 grid over the
-// scene box) above a 16-bit Morton code of the octahedral-mapped direction.
+// Ray coherence key: 15-bit Morton code of the origin cell (32^3 grid) above a
+// 16-bit Morton code of the octahedral-mapped direction.
 static __device__ __forceinline__ uint32_t spread2(uint32_t x)   // 8 bits -> even bits
 {
     x &= 0xff;
@@ -427,12 +546,58 @@ static __device__ __forceinline__ uint32_t spread3(uint32_t x)   // 5 bits -> ev
     return x;
 }
 
+// Origin box of the population (finite origins) as order-preserving uint
+// encodings in misc[0..5] (min xyz, max xyz; k_slot_init empties it).
+static __device__ __forceinline__ uint32_t ord_enc(float f)
+{
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+static __device__ __forceinline__ float ord_dec(uint32_t u)
+{
+    return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ __launch_bounds__(256) void k_bbox(RaysIn R, int64_t n, uint32_t *__restrict__ bb)
+{
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float o[3] = {R.ox[i], R.oy[i], R.oz[i]};
+        if (!(fabsf(o[0]) < INFINITY && fabsf(o[1]) < INFINITY && fabsf(o[2]) < INFINITY)) continue;
+        for (int k = 0; k < 3; ++k) { mn[k] = fminf(mn[k], o[k]); mx[k] = fmaxf(mx[k], o[k]); }
+    }
+    for (int k = 0; k < 3; ++k) { mn[k] = wave_red(mn[k], 0); mx[k] = wave_red(mx[k], 1); }
+    if ((threadIdx.x & 63) == 0 && mn[0] <= mx[0]) {
+        for (int k = 0; k < 3; ++k) { atomicMin(&bb[k], ord_enc(mn[k])); atomicMax(&bb[3 + k], ord_enc(mx[k])); }
+    }
+}
+
+// Key = [class 1 bit][origin cell 15 bits][direction 16 bits] (dir_major: the
+// direction bits above the origin cell's).  bb != NULL: the
+// origin grid spans the population's origin box (k_bbox), so secondary rays that
+// leave one small object still spread over the 32^3 cells (otherwise the scene
+// box bx0.., sx..).  class = (i >= split): the refracted block of a population
+// ([reflected ; refracted], k_append) sorts apart from the reflected one.
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
-                                                float sx, float sy, float sz, uint32_t *__restrict__ keys,
+                                                float sx, float sy, float sz, const uint32_t *__restrict__ bb,
+                                                int64_t split, int dir_major, uint32_t *__restrict__ keys,
                                                 int32_t *__restrict__ vals)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (bb) {
+        const float lo[3] = {ord_dec(bb[0]), ord_dec(bb[1]), ord_dec(bb[2])};
+        const float hi[3] = {ord_dec(bb[3]), ord_dec(bb[4]), ord_dec(bb[5])};
+        float sc[3];
+        for (int k = 0; k < 3; ++k) {
+            const float ext = hi[k] - lo[k];
+            sc[k] = (ext > 0.0f && ext < INFINITY) ? 32.0f / ext : 0.0f;
+        }
+        bx0 = lo[0] <= hi[0] ? lo[0] : 0.0f;
+        by0 = lo[1] <= hi[1] ? lo[1] : 0.0f;
+        bz0 = lo[2] <= hi[2] ? lo[2] : 0.0f;
+        sx = sc[0]; sy = sc[1]; sz = sc[2];
+    }
     const float dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
     const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
     float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
@@ -447,7 +612,8 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     const uint32_t oy = (uint32_t)fminf(fmaxf((R.oy[i] - by0) * sy, 0.0f), 31.0f);
     const uint32_t oz = (uint32_t)fminf(fmaxf((R.oz[i] - bz0) * sz, 0.0f), 31.0f);
     const uint32_t okey = spread3(ox) | (spread3(oy) << 1) | (spread3(oz) << 2);
-    keys[i] = (okey << 16) | spread2(du) | (spread2(dv) << 1);
+    const uint32_t dkey = spread2(du) | (spread2(dv) << 1);
+    keys[i] = (i >= split ? 0x80000000u : 0u) | (dir_major ? (dkey << 15) | okey : (okey << 16) | dkey);
     vals[i] = (int32_t)i;
 }
 

@@ -316,6 +316,16 @@ struct Node4 {
     int32_t pad[8];
 };
 
+// Leaf children are triangles or "fan groups".  A fan group holds up to
+// LPC_GROUP_SIZE thin triangles whose filter spheres pile up around a common
+// point (revolve_curve's poles): reached through the hierarchy, a wave tests all
+// of them lane-parallel against its packet bound (packet_sphere_test) and then
+// each candidate per ray, instead of walking the many subtrees that share the
+// pole.  A group's own test is node_record() of its members.
+//   ref >= LPC_GROUP_REF: triangle ~ref;  ref < LPC_GROUP_REF: group LPC_GROUP_REF - 1 - ref.
+#define LPC_GROUP_REF (-(1 << 30))
+#define LPC_GROUP_SIZE 64
+
 // A "sliver": a triangle whose sphere test degenerates (B >= 0.5, e.g.
 // revolve_curve's pole triangles with two vertices 1e-11 apart).  For it
 // Moller-Trumbore is rounding noise that can accept rays anywhere along the line

@@ -50,6 +50,7 @@ struct Pop {
 struct PieceTable {
     DBuf pieces, spieces;              // hierarchy pieces (k_intersect), sliver pieces (k_slivers)
     int32_t npieces = 0, nspieces = 0;
+    int32_t gmax = 0;                  // most fan groups under one piece (k_groups item slots)
 };
 
 const int kShadeF = 12;   // float arrays of the shade outputs
@@ -69,6 +70,7 @@ struct lpc_handle {
     std::vector<int32_t> run_lo, run_hi;
     std::vector<std::vector<int32_t>> run_levels;    // per run: (first node, count) per level, root first
     std::vector<FiltRec> node_self;                  // each node's own test (piece roots)
+    std::vector<int32_t> node_groups;                // fan groups in each node's subtree
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
@@ -76,6 +78,9 @@ struct lpc_handle {
     std::vector<int32_t> slot_run;
     std::vector<int32_t> meas_meshes;
     DBuf d_nodes, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
+    DBuf d_grec, d_gxrec;                            // fan-group member filter / exact records
+    double flat_ratio = 0.0;                         // fan-group threshold on rho^2 / area (0: no groups)
+    int64_t n_groups = 0, n_grouped = 0;
     double dcap = 16.0;
     std::map<int32_t, PieceTable> ptabs;
     // workspace
@@ -84,9 +89,16 @@ struct lpc_handle {
     DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf d_live;                                    // [K] slot written by some run
-    DBuf w_pk;                                      // PacketRec per 128-ray wave
+    DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
+    DBuf w_pk64;                                    // PacketRec per 64-ray packet (k_groups)
+    DBuf w_gitems, w_gcount;                        // k_intersect -> k_groups fan-group items
+    DBuf d_misc;                                    // LPC_MISC_WORDS per-launch words
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
+    // launch policy (defaults; LPC_* environment overrides read at lpc_open)
+    int key_mode = 0;                               // coherence key, see run_intersect
+    int64_t target_blocks = 8192;                   // k_intersect: blocks x pieces to fill the GPU
+    int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     // trace
     Pop A, B, T, I;
     int64_t n_cur = 0, n_init = 0;
@@ -97,8 +109,10 @@ struct lpc_handle {
     DBuf d_acc;
     DBuf d_tmp;                                     // misc small device scratch
     DBuf d_stats;                                   // k_intersect counters (profiling)
+    DBuf d_wrec;                                    // per-wave records of the last k_intersect (level 3)
+    int64_t wrec_count = 0;
     // profiling
-    bool prof = false, prof_stats = false;
+    bool prof = false, prof_stats = false, prof_waves = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest;
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0;
@@ -218,30 +232,45 @@ static int build_records(lpc_handle *h)
     std::vector<SliverRec> slivers;
     h->run_levels.clear();
     h->node_self.clear();
+    h->node_groups.clear();
     h->run_slo.clear(); h->run_shi.clear();
     h->n_slivers = 0;
     const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 0.0f, INFINITY);
+    std::vector<FiltRec> grec;                      // fan-group members, LPC_GROUP_SIZE per group
+    std::vector<ExactRec> gxrec;                    // their exact records
+    h->n_groups = h->n_grouped = 0;
+    auto vptr = [&](int32_t t, int v) -> const float * {
+        return v == 0 ? &h->hv0[4 * (size_t)t] : v == 1 ? &h->hv1[4 * (size_t)t] : &h->hv2[4 * (size_t)t];
+    };
     for (size_t r = 0; r < h->run_lo.size(); ++r) {
         const int32_t lo = h->run_lo[r], cnt_all = h->run_hi[r] - lo;
-        std::vector<FiltRec> fr;
-        std::vector<double> cen;
+        std::vector<FiltRec> fr, fl;                 // plain triangles, fan (thin) triangles
+        std::vector<double> cen, fcen;
         std::vector<int32_t> sl;
         for (int32_t i = 0; i < cnt_all; ++i) {
-            const size_t t = (size_t)(lo + i);
-            const FiltRec f = filter_record(&h->hv0[4 * t], &h->hv1[4 * t], &h->hv2[4 * t], lo + i, h->dcap,
-                                            h->scene_scale);
+            const int32_t t = lo + i;
+            const float *V0 = vptr(t, 0), *V1 = vptr(t, 1), *V2 = vptr(t, 2);
+            const FiltRec f = filter_record(V0, V1, V2, t, h->dcap, h->scene_scale);
             if (f.negA == INFINITY) continue;                     // never a candidate
-            if (f.negB < -1e29f) { sl.push_back(lo + i); continue; }
-            fr.push_back(f);
-            for (int k = 0; k < 3; ++k) {
-                const double c = ((double)h->hv0[4 * t + k] + h->hv1[4 * t + k] + h->hv2[4 * t + k]) / 3.0;
-                cen.push_back(c);
+            if (f.negB < -1e29f) { sl.push_back(t); continue; }
+            // thin triangles (filter sphere radius^2 / area above flat_ratio) pile
+            // their spheres around shared points: they go to fan groups
+            double rho2 = 0.0, e1[3], e2[3];
+            for (int k = 0; k < 3; ++k) { e1[k] = (double)V1[k] - V0[k]; e2[k] = (double)V2[k] - V0[k]; }
+            for (const float *V : {V0, V1, V2}) {
+                const double x = V[0] - (double)f.cx, y = V[1] - (double)f.cy, z = V[2] - (double)f.cz;
+                rho2 = std::max(rho2, x * x + y * y + z * z);
             }
+            const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2],
+                         cz = e1[0] * e2[1] - e1[1] * e2[0];
+            const double area = 0.5 * sqrt(cx * cx + cy * cy + cz * cz);
+            const bool flat = h->flat_ratio > 0.0 && area > 0.0 && rho2 > h->flat_ratio * area;
+            (flat ? fl : fr).push_back(f);
+            for (int k = 0; k < 3; ++k) (flat ? fcen : cen).push_back(((double)V0[k] + V1[k] + V2[k]) / 3.0);
         }
         h->run_slo.push_back((int32_t)slivers.size());
         for (int32_t t32 : sl) {
-            const size_t t = (size_t)t32;
-            const float *V0 = &h->hv0[4 * t], *V1 = &h->hv1[4 * t], *V2 = &h->hv2[4 * t];
+            const float *V0 = vptr(t32, 0), *V1 = vptr(t32, 1), *V2 = vptr(t32, 2);
             SliverRec S;
             memset(&S, 0, sizeof(S));
             S.v0x = V0[0]; S.v0y = V0[1]; S.v0z = V0[2];
@@ -254,32 +283,94 @@ static int build_records(lpc_handle *h)
         h->run_shi.push_back((int32_t)slivers.size());
         h->n_slivers += (int64_t)sl.size();
         h->run_levels.push_back(std::vector<int32_t>());
-        const int32_t cnt = (int32_t)fr.size();
+        // hierarchy entries: plain triangles and fan groups (each with its test,
+        // child ref, centroid and triangle list)
+        struct Entry { FiltRec t; int32_t ref; double c[3]; int32_t t0, t1; };
+        std::vector<Entry> E;
+        std::vector<int32_t> etri;                   // triangle ids of the entries, [t0, t1) each
+        for (size_t i = 0; i < fr.size(); ++i) {
+            Entry e;
+            e.t = fr[i]; e.ref = ~fr[i].idx;
+            for (int k = 0; k < 3; ++k) e.c[k] = cen[3 * i + k];
+            e.t0 = (int32_t)etri.size(); etri.push_back(fr[i].idx); e.t1 = (int32_t)etri.size();
+            E.push_back(e);
+        }
+        if (!fl.empty()) {
+            const int64_t nf = (int64_t)fl.size();
+            std::vector<int32_t> pf((size_t)nf);
+            for (int64_t i = 0; i < nf; ++i) pf[(size_t)i] = (int32_t)i;
+            int64_t capf = 4;
+            while (capf < nf) capf *= 4;
+            split_order(pf.data(), nf, capf, fcen);
+            for (int64_t c0 = 0; c0 < nf; c0 += LPC_GROUP_SIZE) {
+                const int64_t c1 = std::min<int64_t>(nf, c0 + LPC_GROUP_SIZE);
+                const int32_t g = (int32_t)(grec.size() / LPC_GROUP_SIZE);
+                Entry e;
+                e.c[0] = e.c[1] = e.c[2] = 0.0;
+                e.t0 = (int32_t)etri.size();
+                std::vector<const float *> gv;
+                for (int64_t j = c0; j < c0 + LPC_GROUP_SIZE; ++j) {
+                    gxrec.push_back(ExactRec{});               // zero edges: never accepts
+                    if (j >= c1) { grec.push_back(never); continue; }
+                    const FiltRec &f = fl[(size_t)pf[(size_t)j]];
+                    grec.push_back(f);
+                    {
+                        const float *A = vptr(f.idx, 0), *B = vptr(f.idx, 1), *C = vptr(f.idx, 2);
+                        ExactRec x;
+                        x.v0x = A[0]; x.v0y = A[1]; x.v0z = A[2];
+                        x.e1x = B[0] - A[0]; x.e1y = B[1] - A[1]; x.e1z = B[2] - A[2];
+                        x.e2x = C[0] - A[0]; x.e2y = C[1] - A[1]; x.e2z = C[2] - A[2];
+                        x.pad0 = x.pad1 = x.pad2 = 0.0f;
+                        gxrec[gxrec.size() - 1] = x;
+                    }
+                    etri.push_back(f.idx);
+                    for (int v = 0; v < 3; ++v) gv.push_back(vptr(f.idx, v));
+                    for (int k = 0; k < 3; ++k) e.c[k] += fcen[3 * (size_t)pf[(size_t)j] + k] / (double)(c1 - c0);
+                }
+                e.t1 = (int32_t)etri.size();
+                e.t = never;
+                node_record(gv.data(), (int)(c1 - c0), h->scene_scale, &e.t.cx, &e.t.cy, &e.t.cz, &e.t.negB,
+                            &e.t.negA);
+                e.ref = LPC_GROUP_REF - 1 - g;
+                E.push_back(e);
+                h->n_groups += 1;
+                h->n_grouped += c1 - c0;
+            }
+        }
+        const int32_t cnt = (int32_t)E.size();
         if (cnt == 0) continue;
-        // top-down order: every aligned group of 4^k triangles is one median-split
+        // top-down order: every aligned group of 4^k entries is one median-split
         // cluster, so the bottom-up 4-wide grouping below reproduces that tree
+        std::vector<double> ecen((size_t)cnt * 3);
+        for (int32_t i = 0; i < cnt; ++i)
+            for (int k = 0; k < 3; ++k) ecen[3 * (size_t)i + k] = E[(size_t)i].c[k];
         std::vector<int32_t> perm_t((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) perm_t[(size_t)i] = i;
         int64_t cap = 4;
         while (cap < cnt) cap *= 4;
-        split_order(perm_t.data(), cnt, cap, cen);
-        std::vector<FiltRec> ord((size_t)cnt);
-        for (int32_t i = 0; i < cnt; ++i) ord[(size_t)i] = fr[(size_t)perm_t[(size_t)i]];
-        // every entry covers a contiguous range of `ord`; its test is
-        // node_record() of the triangles in that range
-        std::vector<const float *> tv((size_t)cnt * 3);
+        split_order(perm_t.data(), cnt, cap, ecen);
+        // every hierarchy entry covers a contiguous range of ordered entries; its
+        // test is node_record() of all their triangles
+        std::vector<const float *> tv;
+        std::vector<int32_t> eo((size_t)cnt + 1, 0);
         for (int32_t i = 0; i < cnt; ++i) {
-            const size_t t = (size_t)ord[(size_t)i].idx;
-            tv[3 * (size_t)i] = &h->hv0[4 * t]; tv[3 * (size_t)i + 1] = &h->hv1[4 * t]; tv[3 * (size_t)i + 2] = &h->hv2[4 * t];
+            const Entry &e = E[(size_t)perm_t[(size_t)i]];
+            for (int32_t q = e.t0; q < e.t1; ++q)
+                for (int v = 0; v < 3; ++v) tv.push_back(vptr(etri[(size_t)q], v));
+            eo[(size_t)i + 1] = (int32_t)(tv.size() / 3);
         }
         auto range_test = [&](int32_t a, int32_t b) {
             FiltRec t = never;
-            node_record(&tv[3 * (size_t)a], b - a, h->scene_scale, &t.cx, &t.cy, &t.cz, &t.negB, &t.negA);
+            node_record(&tv[3 * (size_t)eo[(size_t)a]], eo[(size_t)b] - eo[(size_t)a], h->scene_scale, &t.cx, &t.cy,
+                        &t.cz, &t.negB, &t.negA);
             return t;
         };
         struct Ent { FiltRec t; int32_t ref, a, b; };
         std::vector<Ent> ent((size_t)cnt);
-        for (int32_t a = 0; a < cnt; ++a) ent[(size_t)a] = {ord[(size_t)a], ~ord[(size_t)a].idx, a, a + 1};
+        for (int32_t a = 0; a < cnt; ++a) {
+            const Entry &e = E[(size_t)perm_t[(size_t)a]];
+            ent[(size_t)a] = {e.t, e.ref, a, a + 1};
+        }
         std::vector<std::pair<int32_t, int32_t>> levels;   // (first node, count), bottom up
         do {
             std::vector<Ent> up;
@@ -296,9 +387,15 @@ static int build_records(lpc_handle *h)
                 }
                 const int32_t a = ent[i].a, b = ent[std::min(i + 3, ent.size() - 1)].b;
                 const FiltRec self = range_test(a, b);
+                int32_t ng = 0;
+                for (int k = 0; k < 4 && i + k < ent.size(); ++k) {
+                    const int32_t ref = ent[i + k].ref;
+                    ng += ref >= 0 ? h->node_groups[(size_t)ref] : ref < LPC_GROUP_REF ? 1 : 0;
+                }
                 up.push_back({self, (int32_t)nodes.size(), a, b});
                 nodes.push_back(N);
                 h->node_self.push_back(self);
+                h->node_groups.push_back(ng);
             }
             levels.push_back({first, (int32_t)up.size()});
             ent.swap(up);
@@ -310,6 +407,11 @@ static int build_records(lpc_handle *h)
             h->run_levels.back().push_back(it->second);
         }
     }
+    if (grec.empty()) { grec.assign(LPC_GROUP_SIZE, never); gxrec.assign(LPC_GROUP_SIZE, ExactRec{}); }
+    RETIF(dalloc(h, h->d_grec, grec.size() * sizeof(FiltRec)));
+    RETIF(dalloc(h, h->d_gxrec, gxrec.size() * sizeof(ExactRec)));
+    HIPCHK(h, hipMemcpy(h->d_grec.p, grec.data(), grec.size() * sizeof(FiltRec), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_gxrec.p, gxrec.data(), gxrec.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
     if ((int64_t)nodes.size() > INT32_MAX / 2) return set_err(h, LPC_E_ARG, "too many triangles");
     // spare records so no buffer is empty
     if (nodes.empty()) { Node4 N; memset(&N, 0, sizeof(N)); nodes.push_back(N); }
@@ -343,12 +445,13 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     int64_t live_runs = 0;
     for (int32_t v : run_slot) live_runs += v >= 0;
     live_runs = std::max<int64_t>(live_runs, 1);
-    const int64_t target_blocks = 8192;
+    const int64_t target_blocks = h->target_blocks;
     int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (target_blocks + bx * live_runs - 1) /
-                                                                          (bx * live_runs)));
+                                                                        (bx * live_runs)));
     auto it = h->ptabs.find(g);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
     std::vector<Piece> pcs, spc;
+    int32_t gmax = 0;
     for (size_t r = 0; r < nr; ++r) {
         if (run_slot[r] < 0) continue;
         const std::vector<int32_t> &L = h->run_levels[r];
@@ -364,6 +467,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
                 p.s_lo = p.s_hi = 0;
                 p.slot = run_slot[r];
                 pcs.push_back(p);
+                gmax = std::max(gmax, h->node_groups[(size_t)p.root]);
             }
         }
         for (int32_t a = h->run_slo[r]; a < h->run_shi[r]; a += 64) {
@@ -380,6 +484,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     PieceTable &t = h->ptabs[g];
     t.npieces = (int32_t)pcs.size();
     t.nspieces = (int32_t)spc.size();
+    t.gmax = gmax;
     if (!pcs.empty()) {
         RETIF(dalloc(h, t.pieces, pcs.size() * sizeof(Piece)));
         HIPCHK(h, hipMemcpy(t.pieces.p, pcs.data(), pcs.size() * sizeof(Piece), hipMemcpyHostToDevice));
@@ -407,6 +512,8 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_sc, (size_t)h->K * C * 4));
         RETIF(dalloc(h, h->w_rs, (size_t)6 * C * 4));
         RETIF(dalloc(h, h->w_pk, (size_t)((C + 127) / 128) * sizeof(PacketRec)));
+        RETIF(dalloc(h, h->w_pk64, (size_t)((C + 63) / 64) * sizeof(PacketRec)));
+        RETIF(dalloc(h, h->d_misc, LPC_MISC_WORDS * 4));
         RETIF(dalloc(h, h->w_shf, (size_t)kShadeF * C * 4));
         RETIF(dalloc(h, h->w_shi, (size_t)kShadeI * C * 4));
         const int64_t nb = (C + 1023) / 1024;
@@ -418,7 +525,7 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
         size_t tb = 0;
         HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                     (const int32_t *)nullptr, (int32_t *)nullptr, (int)C, 0, 31,
+                                                     (const int32_t *)nullptr, (int32_t *)nullptr, (int)C, 0, 32,
                                                      h->stream));
         RETIF(dalloc(h, h->w_sort_tmp, tb));
         h->sort_tmp_bytes = tb;
@@ -475,8 +582,10 @@ static void prof_resolve(lpc_handle *h)
 
 // intersect for n rays of `in` into the slot arrays, and optionally into a
 // caller's [ray][mesh] buffers (st_user != NULL, the reference's scratch layout).
+// split: rows [0, split) of `in` are a population's reflected block (key class
+// bit, k_raykey); INT64_MAX when the rows are not a trace population.
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
-                         float *st_user, int32_t *si_user, int32_t *sc_user)
+                         float *st_user, int32_t *si_user, int32_t *sc_user, int64_t split = INT64_MAX)
 {
     RETIF(ensure_ws(h, n));
     PieceTable *pt;
@@ -484,8 +593,9 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
     unsigned long long *skey = (unsigned long long *)h->w_key.p;
     int32_t *scnt = (int32_t *)h->w_sc.p;
-    hipLaunchKernelGGL(k_slot_init, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
-                       (const int32_t *)h->d_live.p, max_ray_len, skey, scnt);
+    uint32_t *misc = (uint32_t *)h->d_misc.p;
+    hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream, n,
+                       h->K, (const int32_t *)h->d_live.p, max_ray_len, skey, scnt, misc);
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
     if (h->sort_rays && n >= 4096) {
@@ -493,10 +603,20 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         const size_t C = (size_t)h->ws_rays;
         uint32_t *kin = (uint32_t *)h->w_sort.p, *kout = kin + C;
         int32_t *vin = (int32_t *)(kout + C), *vout = vin + C;
+        // key_mode: 0 [scene-box origin cell | direction], 1 population origin box,
+        // 2 = 1 + refracted-block bit, 3 [direction | scene-box origin cell],
+        // 4 = 3 + refracted-block bit
+        const bool pop_box = h->key_mode == 1 || h->key_mode == 2;
+        const bool cls = h->key_mode == 2 || h->key_mode == 4;
+        if (pop_box)
+            hipLaunchKernelGGL(k_bbox, dim3((unsigned)std::min<int64_t>(grid1(n), 1024)), dim3(256), 0, h->stream,
+                               in, n, misc);
         hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
-                           h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin);
+                           h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
+                           pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
+                           h->key_mode >= 3 ? 1 : 0, kin, vin);
         size_t tb = h->sort_tmp_bytes;
-        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (int)n, 0, 31,
+        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (int)n, 0, 32,
                                                      h->stream));
         perm = vout;
         hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
@@ -504,20 +624,45 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+    unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
     if (pt->npieces > 0) {
-        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + 255) / 256), (unsigned)pt->npieces), dim3(256), 0,
-                           h->stream, in, rs, n, perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
-                           (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt,
-                           h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr);
+        uint32_t *wrec = nullptr;
+        if (h->prof_waves) {
+            h->wrec_count = (int64_t)pt->npieces * ((n + 63) / 64);
+            RETIF(dalloc(h, h->d_wrec, (size_t)h->wrec_count * 16));
+            HIPCHK(h, hipMemsetAsync(h->d_wrec.p, 0, (size_t)h->wrec_count * 16, h->stream));
+            wrec = (uint32_t *)h->d_wrec.p;
+        }
+        const int64_t npk = (n + 63) / 64;
+        const int gmax = pt->gmax;
+        GItem *gitems = nullptr;
+        int32_t *gcount = nullptr;
+        if (gmax > 0) {               // fan-group item slots: one list per (piece, packet) wave
+            RETIF(dalloc(h, h->w_gcount, (size_t)pt->npieces * npk * 4));
+            RETIF(dalloc(h, h->w_gitems, (size_t)pt->npieces * npk * gmax * sizeof(GItem)));
+            gitems = (GItem *)h->w_gitems.p;
+            gcount = (int32_t *)h->w_gcount.p;
+        }
+        const dim3 grid((unsigned)((n + 255) / 256), (unsigned)pt->npieces);
+        hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, rs, n, perm, (const Node4 *)h->d_nodes.p,
+                           (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax, (const Piece *)pt->pieces.p, eps,
+                           max_ray_len, skey, scnt, stats, wrec);
+        if (gmax > 0) {
+            hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
+                               (PacketRec *)h->w_pk64.p);
+            hipLaunchKernelGGL(k_groups, grid, dim3(256), 0, h->stream, in, rs, n, perm, (const FiltRec *)h->d_grec.p,
+                               (const ExactRec *)h->d_gxrec.p, (const PacketRec *)h->w_pk64.p,
+                               (const Piece *)pt->pieces.p, (const GItem *)gitems, (const int32_t *)gcount, gmax,
+                               eps, max_ray_len, skey, scnt);
+        }
         HIPCHK(h, hipGetLastError());
     }
     if (pt->nspieces > 0) {
-        hipLaunchKernelGGL(k_packet, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, h->stream, in, rs, n,
+        hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, h->stream, in, rs, n,
                            (PacketRec *)h->w_pk.p);
         hipLaunchKernelGGL(k_slivers, dim3((unsigned)((n + 511) / 512), (unsigned)pt->nspieces), dim3(256), 0,
                            h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p, (const SliverRec *)h->d_srec.p,
-                           (const Piece *)pt->spieces.p, eps, max_ray_len, skey, scnt,
-                           h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr);
+                           (const Piece *)pt->spieces.p, eps, max_ray_len, skey, scnt, stats);
         HIPCHK(h, hipGetLastError());
     }
     if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
@@ -598,6 +743,15 @@ int lpc_open(int device, lpc_handle **out)
     }
     int rc = dalloc(h, h->d_acc, sizeof(DevAcc));
     if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
+    // launch-policy overrides (A/B measurements; results do not depend on them)
+    auto env_int = [](const char *k, int64_t dflt) -> int64_t {
+        const char *v = getenv(k);
+        return (v && *v) ? strtoll(v, nullptr, 10) : dflt;
+    };
+    h->key_mode = (int)env_int("LPC_KEY", h->key_mode);
+    h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
+    h->sort_rays = env_int("LPC_SORT", 1) != 0;
+    if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     *out = h;
     return 0;
 }
@@ -611,7 +765,7 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec};
     for (DBuf *b : bufs) dfree(*b);
     for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
     prof_resolve(h);
@@ -640,6 +794,8 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     if (tri_count <= 0 || mesh_count <= 0 || !v0 || !v1 || !v2 || !mesh_id || !mat_type || !ior ||
         !refl || !diss)
         return set_err(h, LPC_E_ARG, "scene needs >= 1 triangle, >= 1 mesh and all tables");
+    if (tri_count >= (1 << 30) - 1)   // child refs: ~idx above LPC_GROUP_REF
+        return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^30 - 2)");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const int32_t M = tri_count, K = mesh_count;
@@ -966,6 +1122,7 @@ int lpc_trace_reset(lpc_handle *h)
     RETIF(pop_reserve(h, h->A, std::max<int64_t>(h->n_init, 1)));
     if (h->n_init > 0) RETIF(copy_pop(h, h->A, h->I, h->n_init));
     h->n_cur = h->n_init;
+    h->split = INT64_MAX;                       // emitted rays: one class
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return reset_measured(h);
 }
@@ -1021,7 +1178,8 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         const RaysIn in = h->A.in(base);
-        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr));
+        const int64_t split = h->split == INT64_MAX ? INT64_MAX : std::max<int64_t>(0, h->split - base);
+        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split));
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
         RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
@@ -1067,6 +1225,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (h->prof) prof_resolve(h);
     std::swap(h->A, h->B);
     h->n_cur = nR + nT;
+    h->split = nR;
     h->m_total = (int64_t)acc.m_total;
     S.n_reflect = nR; S.n_refract = nT; S.n_measured = (int64_t)acc.nM_iter;
     S.power_next = acc.pow_next;
@@ -1193,7 +1352,8 @@ int lpc_prof_enable(lpc_handle *h, int on)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     h->prof = on != 0;
-    h->prof_stats = on >= 2;
+    h->prof_stats = on == 2;
+    h->prof_waves = on == 3;
     if (h->prof_stats && !h->d_stats.p) {
         RETIF(dalloc(h, h->d_stats, LPC_STATS_WORDS * 8));
         HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
@@ -1228,6 +1388,18 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     if (reset) {
         h->prof_isect_ms = h->prof_rest_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
         if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
+    }
+    return 0;
+}
+
+int lpc_prof_waves(lpc_handle *h, uint32_t *rec4, int64_t cap, int64_t *count)
+{
+    if (!h || !count) return set_err(h, LPC_E_ARG, "null argument");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    *count = h->d_wrec.p ? h->wrec_count : 0;
+    if (rec4 && *count > 0) {
+        const int64_t m = std::min(cap, *count);
+        if (m > 0) HIPCHK(h, hipMemcpy(rec4, h->d_wrec.p, (size_t)m * 16, hipMemcpyDeviceToHost));
     }
     return 0;
 }

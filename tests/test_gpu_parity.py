@@ -15,8 +15,10 @@ from lightpycl_amd import scenes
 
 pytestmark = pytest.mark.gpu
 
+# n >= 4096 runs the coherence-sorted path (k_raykey + radix sort + k_gather) and
+# the work-list traversal on sorted packets; smaller n the unsorted packets.
 SCENES = [("parabolic", 2000), ("lens", 2000), ("eye", 600), ("cube", 2000), ("nested_cubes", 10),
-          ("synthetic", 700)]
+          ("synthetic", 700), ("synthetic", 20000), ("lens", 30000), ("eye", 12000), ("parabolic", 25000)]
 
 
 def rays_of(sc):
@@ -67,6 +69,30 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
     g2 = engine.bounce(o2, d2, p2, z, m2, sc.max_ray_len, sc.ior_env)
     r2 = oracle_mod.bounce(S, o2, d2, p2, z, m2, sc.max_ray_len, sc.ior_env)
     _cmp_bounce(g2, r2, diss)
+
+
+@pytest.mark.parametrize("cfg", [dict(LPC_FLAT="0"), dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"),
+                                 dict(LPC_FLAT="20", LPC_KEY="2"), dict(LPC_KEY="3"), dict(LPC_KEY="1"),
+                                 dict(LPC_SORT="0")])
+def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
+    """The launch policies (fan-group threshold, piece granularity, coherence
+    key, no sort) change only speed."""
+    from lightpycl_amd.engine import Engine
+    for k, v in cfg.items():
+        monkeypatch.setenv(k, v)
+    sc = scenes.synthetic(n=9000, seed=8)
+    o4, d4, pw = rays_of(sc)
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        S = oracle_mod.Scene(sc.meshes)
+        z = np.zeros(len(pw), np.int32)
+        pm = np.full(len(pw), -2, np.int32)
+        g = e.bounce(o4, d4, pw, z, pm, sc.max_ray_len, sc.ior_env)
+        o = oracle_mod.bounce(S, o4, d4, pw, z, pm, sc.max_ray_len, sc.ior_env)
+        _cmp_bounce(g, o, False)
+    finally:
+        e.close()
 
 
 @pytest.mark.parametrize("name,n", [("parabolic", 3000), ("lens", 3000), ("eye", 300), ("cube", 3000),
