@@ -39,8 +39,24 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 #define LPC_STATS_WORDS (LPC_STATS_PIECE + LPC_STATS_PIECES)
 
 // Per-launch device words of the intersect stage (uint32, reset by k_slot_init):
-// [0..5] population origin box (k_bbox, coherence key modes 1-2).
+// [0..5] population origin box (k_bbox, coherence key modes 1-2), [6] spill
+// items queued by k_intersect (k_spill).
 #define LPC_MISC_WORDS 8
+#define LPC_MISC_SPILL 6
+
+// Work hand-over: a k_intersect wave that has visited `budget` nodes with two or
+// more subtrees still on its stack queues each of them as one item; k_spill
+// runs the items, one wave each (per-ray results flush with the same
+// order-independent atomics, so the split does not change the result).
+struct SpillItem {
+    int32_t w, node, slot, piece;     // packet, subtree root, slot, piece (stats)
+};
+struct SpillArgs {
+    SpillItem *items;
+    uint32_t *ctr;                    // misc + LPC_MISC_SPILL
+    uint32_t cap;
+    int budget;                       // nodes before hand-over (0: never)
+};
 
 // A fan group met by a k_intersect wave (packet, piece): group id and the rays
 // that passed the group's test; k_groups processes them.

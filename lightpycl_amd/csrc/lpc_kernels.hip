@@ -191,7 +191,9 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
                                                    unsigned long long *__restrict__ skey,
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
-                                                   uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0)
+                                                   uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0,
+                                                   SpillArgs SP = SpillArgs{nullptr, nullptr, 0u, 0},
+                                                   int32_t start = -1)
 {
     const int lane = threadIdx.x & 63;
     const int64_t s = w * 64 + lane;
@@ -200,7 +202,9 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     // unit direction for the filter only (its rounding is inside the margin)
     const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
     const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
-    if (!(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f))) {
+    // start >= 0: a k_spill item (subtree root `start`, its parent passed)
+    if (start < 0 &&
+        !(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f))) {
         if (gcount && lane == 0) gcount[gslot] = 0;
         return;
     }
@@ -254,15 +258,40 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
         nq = 0;
     };
     int ngr = 0;                                   // fan groups deferred to k_groups
-    L.stack[top++] = P.root;
+    int budget = SP.budget;
+    L.stack[top++] = start >= 0 ? start : P.root;
     while (top > 0) {
+        // work hand-over: after `budget` nodes the subtrees left on the stack go
+        // to k_spill, one wave each (a wave stuck in a dense region would
+        // otherwise be the launch's critical path)
+        if (budget > 0 && (int)n_nodes >= budget && top >= 2) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(SP.ctr, (uint32_t)top);
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0);
+            if (base + (uint32_t)top <= SP.cap) {
+                if (lane < top) {
+                    SpillItem it;
+                    it.w = (int32_t)w; it.node = L.stack[lane]; it.slot = P.slot; it.piece = piece_id;
+                    SP.items[base + lane] = it;
+                }
+                top = 0;
+                break;
+            }
+            // queue full: void the part of the range inside it, carry on here
+            if (lane < top && base + (uint32_t)lane < SP.cap) SP.items[base + lane].node = -1;
+            budget = 0;
+        }
         const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
         const Node4 N = nodes[node];
         ++n_nodes;
-        float d[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            d[k] = filter_test(N.cx[k], N.cy[k], N.cz[k], N.negB[k], N.negA[k], O.x, O.y, O.z, nx, ny, nz);
+        // the four child tests as two packed pairs
+        const lpc_f2 d01 = filter_test2(lpc_f2{N.cx[0], N.cx[1]}, lpc_f2{N.cy[0], N.cy[1]}, lpc_f2{N.cz[0], N.cz[1]},
+                                        lpc_f2{N.negB[0], N.negB[1]}, lpc_f2{N.negA[0], N.negA[1]}, O.x, O.y, O.z,
+                                        nx, ny, nz);
+        const lpc_f2 d23 = filter_test2(lpc_f2{N.cx[2], N.cx[3]}, lpc_f2{N.cy[2], N.cy[3]}, lpc_f2{N.cz[2], N.cz[3]},
+                                        lpc_f2{N.negB[2], N.negB[3]}, lpc_f2{N.negA[2], N.negA[3]}, O.x, O.y, O.z,
+                                        nx, ny, nz);
+        const float d[4] = {d01.x, d01.y, d23.x, d23.y};
         if (N.ref[0] >= 0) {                       // internal node: children are nodes
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -339,17 +368,46 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
                                                    unsigned long long *__restrict__ skey,
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
-                                                   uint32_t *__restrict__ wrec)
+                                                   uint32_t *__restrict__ wrec, SpillArgs SP, int loop_pieces)
 {
     __shared__ WaveLds lds[4];
     const int wv = threadIdx.x >> 6;
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     if (w * 64 >= n) return;                       // whole wave past the end
-    const Piece P = pieces[blockIdx.y];
-    trav_packet(lds[wv], R, rs, n, perm, nodes, xrec, gitems, gcount, gmax,
-                (int64_t)blockIdx.y * ((n + 63) / 64) + w, P, w, (int)blockIdx.y, eps, max_ray_len,
-                skey, scnt, stats,
-                wrec, (int64_t)blockIdx.y * ((n + 63) / 64) + w);
+    // loop_pieces > 0: grid.y = 1 and the wave takes the pieces in turn (no
+    // waves launched only to fail a piece's root test)
+    const int p0 = loop_pieces > 0 ? 0 : (int)blockIdx.y;
+    const int p1 = loop_pieces > 0 ? loop_pieces : p0 + 1;
+    for (int p = p0; p < p1; ++p) {
+        const Piece P = pieces[p];
+        const int64_t slot = (int64_t)p * ((n + 63) / 64) + w;
+        trav_packet(lds[wv], R, rs, n, perm, nodes, xrec, gitems, gcount, gmax, slot, P, w, p, eps, max_ray_len,
+                    skey, scnt, stats, wrec, slot, SP);
+    }
+}
+
+// k_spill: the subtrees k_intersect handed over (SpillArgs), one item per wave,
+// grid-stride over the queue (its length is read on the device).  Items do not
+// hand over again.  Only used without fan groups (the host checks).
+__global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                               const int32_t *__restrict__ perm, const Node4 *__restrict__ nodes,
+                                               const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
+                                               unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
+                                               unsigned long long *__restrict__ stats, SpillArgs SP)
+{
+    __shared__ WaveLds lds[4];
+    const int wv = threadIdx.x >> 6;
+    const uint32_t total = min(*SP.ctr, SP.cap);
+    const uint32_t W = gridDim.x * 4u;
+    for (uint32_t it = blockIdx.x * 4u + (uint32_t)wv; it < total; it += W) {
+        const SpillItem I = SP.items[it];
+        if (I.node < 0) continue;
+        Piece P;
+        memset(&P, 0, sizeof(P));
+        P.root = I.node; P.slot = I.slot;
+        trav_packet(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
+                    max_ray_len, skey, scnt, stats, nullptr, 0, SpillArgs{nullptr, nullptr, 0u, 0}, I.node);
+    }
 }
 
 // k_groups: the fan groups k_intersect's wave (packet w, piece y) met, same
@@ -831,6 +889,28 @@ __global__ __launch_bounds__(256) void k_append(RaysOut dst, RaysIn src, const D
         dst.ox[q] = src.ox[i]; dst.oy[q] = src.oy[i]; dst.oz[q] = src.oz[i];
         dst.dx[q] = src.dx[i]; dst.dy[q] = src.dy[i]; dst.dz[q] = src.dz[i];
         dst.pw[q] = src.pw[i]; dst.pmid[q] = src.pmid[i];
+    }
+}
+
+// Population copy (trace reset: emitted rays -> current population), one launch.
+__global__ __launch_bounds__(256) void k_copy_pop(RaysOut dst, RaysIn src, int64_t n)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        dst.ox[i] = src.ox[i]; dst.oy[i] = src.oy[i]; dst.oz[i] = src.oz[i];
+        dst.dx[i] = src.dx[i]; dst.dy[i] = src.dy[i]; dst.dz[i] = src.dz[i];
+        dst.pw[i] = src.pw[i]; dst.pmid[i] = src.pmid[i];
+    }
+}
+
+// Iteration counters start: kept children 0, measured record length m_total
+// (in-stream, no host round trip).
+__global__ void k_acc_init(DevAcc *acc, unsigned long long m_total)
+{
+    if (threadIdx.x == 0) {
+        DevAcc z;
+        memset(&z, 0, sizeof(z));
+        z.m_total = m_total;
+        *acc = z;
     }
 }
 

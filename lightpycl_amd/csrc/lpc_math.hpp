@@ -300,6 +300,20 @@ LPC_HD float filter_test(float cx, float cy, float cz, float negB, float negA, f
     return pp + (negA + negB * ww);
 }
 
+// filter_test for two records at once (packed FP32 on gfx950: v_pk_fma_f32 /
+// v_pk_mul_f32 evaluate both halves with the same IEEE operations, so each half
+// is one plain or FMA-contracted evaluation of filter_test, inside the slack).
+typedef float lpc_f2 __attribute__((ext_vector_type(2)));
+LPC_HD lpc_f2 filter_test2(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2 negA, float ox, float oy,
+                           float oz, float nx, float ny, float nz)
+{
+    const lpc_f2 wx = cx - ox, wy = cy - oy, wz = cz - oz;
+    const lpc_f2 px = wy * nz - wz * ny, py = wz * nx - wx * nz, pz = wx * ny - wy * nx;
+    const lpc_f2 pp = px * px + py * py + pz * pz;
+    const lpc_f2 ww = wx * wx + wy * wy + wz * wz;
+    return pp + (negA + negB * ww);
+}
+
 // Float-evaluation slack of filter_test, both ways (factor on A and B, and an
 // absolute term on B = (1 + 1/h') 49 eps^2 with h' = 1e-3, rounded up).
 #define LPC_FILT_REL 2e-3

@@ -6,7 +6,7 @@
 #include "lpc_kernels.hip"
 #include "lpc.h"
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -97,7 +97,13 @@ struct lpc_handle {
     bool sort_rays = true;
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
-    int64_t target_blocks = 8192;                   // k_intersect: blocks x pieces to fill the GPU
+    int64_t target_blocks = 16384;                  // k_intersect: blocks x pieces to fill the GPU
+    int spill_budget = 0;                           // k_intersect nodes before hand-over to k_spill (0 off)
+    int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
+    int64_t spill_blocks = 2048;                    // k_spill grid (4 waves each, grid-stride)
+    bool piece_loop = false;                        // k_intersect: waves loop over the pieces
+    DBuf w_spill;                                   // k_spill queue
+    DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     // trace
     Pop A, B, T, I;
@@ -497,6 +503,12 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     return 0;
 }
 
+// Coherence sort: rocPRIM's default algorithm choice (block merge sort up to
+// 1 Mi items, onesweep above).  Forcing onesweep at every size measured slower
+// (189 vs 131 us per 1 M-ray iteration incl. k_raykey/k_gather: 4 digit passes +
+// histogram + lookback-state fills, each latency-bound).
+using RaySortCfg = rocprim::default_config;
+
 static int64_t chunk_rays(const lpc_handle *h)
 {
     return h->chunk > 0 ? h->chunk : (int64_t)8 << 20;
@@ -524,9 +536,9 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
         RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
         size_t tb = 0;
-        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                     (const int32_t *)nullptr, (int32_t *)nullptr, (int)C, 0, 32,
-                                                     h->stream));
+        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                        (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)C, 0,
+                                                        32, h->stream));
         RETIF(dalloc(h, h->w_sort_tmp, tb));
         h->sort_tmp_bytes = tb;
         h->ws_rays = C;
@@ -616,8 +628,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
                            h->key_mode >= 3 ? 1 : 0, kin, vin);
         size_t tb = h->sort_tmp_bytes;
-        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (int)n, 0, 32,
-                                                     h->stream));
+        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, 0, 32,
+                                                        h->stream));
         perm = vout;
         hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
         rs = (const float *)h->w_rs.p;
@@ -643,10 +655,24 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             gitems = (GItem *)h->w_gitems.p;
             gcount = (int32_t *)h->w_gcount.p;
         }
-        const dim3 grid((unsigned)((n + 255) / 256), (unsigned)pt->npieces);
+        // work hand-over (not with fan groups: a k_spill item has no group slots)
+        SpillArgs SP{nullptr, nullptr, 0u, 0};
+        if (h->spill_budget > 0 && gmax == 0 && !wrec) {
+            RETIF(dalloc(h, h->w_spill, (size_t)h->spill_cap * sizeof(SpillItem)));
+            SP.items = (SpillItem *)h->w_spill.p;
+            SP.ctr = misc + LPC_MISC_SPILL;
+            SP.cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
+            SP.budget = h->spill_budget;
+        }
+        const int loop = h->piece_loop ? (int)pt->npieces : 0;
+        const dim3 grid((unsigned)((n + 255) / 256), loop ? 1u : (unsigned)pt->npieces);
         hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, rs, n, perm, (const Node4 *)h->d_nodes.p,
                            (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax, (const Piece *)pt->pieces.p, eps,
-                           max_ray_len, skey, scnt, stats, wrec);
+                           max_ray_len, skey, scnt, stats, wrec, SP, loop);
+        if (SP.budget > 0)
+            hipLaunchKernelGGL(k_spill, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n, perm,
+                               (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
+                               scnt, stats, SP);
         if (gmax > 0) {
             hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
                                (PacketRec *)h->w_pk64.p);
@@ -752,6 +778,15 @@ int lpc_open(int device, lpc_handle **out)
     h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
     if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
+    h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
+    h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
+    h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
+    h->piece_loop = env_int("LPC_LOOP", h->piece_loop) != 0;
+    if (hipHostMalloc((void **)&h->acc_host, sizeof(DevAcc), hipHostMallocDefault) != hipSuccess) {
+        g_open_err = "pinned host buffer";
+        lpc_close(h);
+        return LPC_E_HIP;
+    }
     *out = h;
     return 0;
 }
@@ -765,8 +800,10 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill};
     for (DBuf *b : bufs) dfree(*b);
+    if (h->acc_host) (void)hipHostFree(h->acc_host);
+    h->acc_host = nullptr;
     for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
     prof_resolve(h);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -1120,11 +1157,15 @@ int lpc_trace_reset(lpc_handle *h)
     if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_reset before trace_set_rays");
     HIPCHK(h, hipSetDevice(h->device));
     RETIF(pop_reserve(h, h->A, std::max<int64_t>(h->n_init, 1)));
-    if (h->n_init > 0) RETIF(copy_pop(h, h->A, h->I, h->n_init));
+    if (h->n_init > 0)
+        hipLaunchKernelGGL(k_copy_pop, dim3((unsigned)std::min<int64_t>(grid1(h->n_init), 8192)), dim3(256), 0,
+                           h->stream, h->A.out(), h->I.in(0), h->n_init);
     h->n_cur = h->n_init;
     h->split = INT64_MAX;                       // emitted rays: one class
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return reset_measured(h);
+    h->m_total = 0;                             // measured record emptied in-stream
+    hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p, 0ull);
+    HIPCHK(h, hipGetLastError());
+    return 0;
 }
 
 int lpc_trace_population(lpc_handle *h, int64_t *n)
@@ -1169,10 +1210,8 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     RETIF(pop_reserve(h, h->B, 2 * N));
     RETIF(pop_reserve(h, h->T, N));
     RETIF(ensure_measured(h, h->m_total + N));
-    DevAcc acc;
-    memset(&acc, 0, sizeof(acc));
-    acc.m_total = (unsigned long long)h->m_total;
-    HIPCHK(h, hipMemcpy(h->d_acc.p, &acc, sizeof(acc), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p,
+                       (unsigned long long)h->m_total);
     const size_t mc = (size_t)h->m_cap;
     float *mf = (float *)h->m_buf.p;
     for (int64_t base = 0; base < N; base += C) {
@@ -1210,18 +1249,19 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         HIPCHK(h, hipGetLastError());
         if (h->prof) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
     }
+    // refracted block after the reflected one (k_append reads the counts on the
+    // device), then the counters to the pinned copy: one host sync per iteration
+    hipLaunchKernelGGL(k_append, dim3((unsigned)std::min<int64_t>(grid1(N), 8192)), dim3(256), 0, h->stream,
+                       h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(h->acc_host, h->d_acc.p, sizeof(DevAcc), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(&acc, h->d_acc.p, sizeof(acc), hipMemcpyDeviceToHost));
+    DevAcc acc = *h->acc_host;
     const int64_t nR = (int64_t)acc.nR, nT = (int64_t)acc.nT;
-    if (nT > 0) {
-        hipLaunchKernelGGL(k_append, dim3((unsigned)std::min<int64_t>(grid1(nT), 8192)), dim3(256), 0,
-                           h->stream, h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
-        HIPCHK(h, hipGetLastError());
-    }
     if (out_next_pow && nR + nT > 0) {
         HIPCHK(h, hipMemcpyAsync(out_next_pow, h->B.f(6), (size_t)(nR + nT) * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
     }
-    HIPCHK(h, hipStreamSynchronize(h->stream));
     if (h->prof) prof_resolve(h);
     std::swap(h->A, h->B);
     h->n_cur = nR + nT;

@@ -68,7 +68,10 @@ class ShardedTrace:
             return np.asarray(vals, dtype=np.float64)
         return self.comm.allreduce_sum(vals)
 
-    def run(self, iterations, tau, input_power_local):
+    def run(self, iterations, tau, input_power_local, hist=None):
+        """Trace to the reference's termination.  hist=(limits, points): also bin
+        the measured rays (get_binned_data_angular) on every rank and all-reduce
+        the histogram (float64, bin counts are additive)."""
         in_pow = float(self._sum([input_power_local])[0])
         thr = (1.0 - tau) * in_pow
         bounces = 0
@@ -86,4 +89,9 @@ class ShardedTrace:
                 break
         _, mesh_pow = self.engine.measured()
         mesh_pow = self._sum(np.asarray(mesh_pow, dtype=np.float64))
-        return dict(bounces=bounces, iterations=iters, global_counts=counts, mesh_power=mesh_pow)
+        out = dict(bounces=bounces, iterations=iters, global_counts=counts, mesh_power=mesh_pow)
+        if hist is not None:
+            limits, points = hist
+            H, xe, ye = self.engine.project_hist(None, None, limits, points)[:3]
+            out["hist"] = (self._sum(np.asarray(H, np.float64).ravel()).reshape(H.shape), xe, ye)
+        return out

@@ -18,6 +18,7 @@ class OracleEngine:
         self.mrl, self.ior = np.float32(max_ray_len), np.float32(ior_env)
         self.mesh_power = np.zeros(self.S.mesh_count, np.float64)
         self.count = 0
+        self.pos, self.pwr = [], []
 
     def iterate(self):
         n = self.p.shape[0]
@@ -27,6 +28,8 @@ class OracleEngine:
         m = out["meas"] == 1
         np.add.at(self.mesh_power, out["isect_mid"][m], out["pow"][m].astype(np.float64))
         self.count += int(m.sum())
+        self.pos.append(out["dest"][m])
+        self.pwr.append(out["pow"][m])
         kr, kt = out["r_meas"] == 0, out["t_meas"] == 0
         self.o = np.concatenate((out["r_origin"][kr], out["t_origin"][kt]))
         self.d = np.concatenate((out["r_dir"][kr], out["t_dir"][kt]))
@@ -38,3 +41,10 @@ class OracleEngine:
 
     def measured(self):
         return self.count, self.mesh_power
+
+    def project_hist(self, pos4, pwr, limits, points):
+        """get_binned_data_angular over the measured record (pos4=None) or the given rays."""
+        if pos4 is None:
+            pos4 = np.concatenate(self.pos) if self.pos else np.zeros((0, 4), np.float32)
+            pwr = np.concatenate(self.pwr) if self.pwr else np.zeros(0, np.float32)
+        return oracle.binned_angular(pos4, pwr, limits, points)

@@ -1,8 +1,9 @@
 """Multi-process (world_size 2, gloo, CPU) run of the sharded trace driver
 (lightpycl_amd.distributed): each rank traces its contiguous shard of the rays
 and all ranks take the reference's global termination decision from all-reduced
-(live rays, power left).  The global per-iteration ray counts and the summed
-per-mesh measured power must equal a single-process trace of all rays."""
+(live rays, power left).  The global per-iteration ray counts, the summed
+per-mesh measured power and the all-reduced angular histogram must equal a
+single-process trace of all rays."""
 import json
 import os
 import socket
@@ -16,6 +17,8 @@ import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+HIST_LIMITS = ((-np.pi / 2, np.pi / 2), (-np.pi / 2, np.pi / 2))
+HIST_POINTS = 30
 
 
 def _free_port():
@@ -41,10 +44,12 @@ def _worker(rank, world, port, name, n, out_path):
     p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
     lo, hi = shard_bounds(len(p), rank, world)
     eng = OracleEngine(sc.meshes, o[lo:hi], d[lo:hi], p[lo:hi], sc.max_ray_len, sc.ior_env)
-    r = ShardedTrace(eng, TorchComm(dist)).run(sc.iterations, sc.tau, float(np.sum(p[lo:hi], dtype=np.float64)))
+    r = ShardedTrace(eng, TorchComm(dist)).run(sc.iterations, sc.tau, float(np.sum(p[lo:hi], dtype=np.float64)),
+                                               hist=(HIST_LIMITS, HIST_POINTS))
     if rank == 0:
         with open(out_path, "w") as f:
-            json.dump(dict(counts=r["global_counts"], mesh_power=list(map(float, r["mesh_power"]))), f)
+            json.dump(dict(counts=r["global_counts"], mesh_power=list(map(float, r["mesh_power"])),
+                           hist=r["hist"][0].tolist()), f)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -56,10 +61,15 @@ def test_sharded_trace_matches_single_process(oracle_mod, tmp_path, name, n):
     mp.spawn(_worker, args=(2, _free_port(), name, n, out), nprocs=2, join=True)
     got = json.load(open(out))
     sc = scenes.BUILDERS[name](n=n, seed=2)
-    _, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
-                               keep_results=False)
+    res, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env)
     assert got["counts"] == info["counts"]
     np.testing.assert_allclose(got["mesh_power"], info["mesh_power"], rtol=1e-12, atol=1e-12)
+    # angular histogram of the measured rays: per-rank bins all-reduced (float64;
+    # only the summation order differs from the single-process binning)
+    pos, pwr = oracle_mod.measured_rays(res)
+    H = oracle_mod.binned_angular(pos, pwr, HIST_LIMITS, HIST_POINTS)[0]
+    assert np.sum(H) > 0
+    np.testing.assert_allclose(np.asarray(got["hist"]), H, rtol=1e-12, atol=1e-9 * float(np.max(H)))
 
 
 def test_shard_bounds_cover():

@@ -73,10 +73,13 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
 
 @pytest.mark.parametrize("cfg", [dict(LPC_FLAT="0"), dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"),
                                  dict(LPC_FLAT="20", LPC_KEY="2"), dict(LPC_KEY="3"), dict(LPC_KEY="1"),
-                                 dict(LPC_SORT="0")])
+                                 dict(LPC_SORT="0"), dict(LPC_BUDGET="16"), dict(LPC_BUDGET="4"),
+                                 dict(LPC_BUDGET="6", LPC_SPILL_CAP="100"), dict(LPC_LOOP="1"),
+                                 dict(LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1")])
 def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
     """The launch policies (fan-group threshold, piece granularity, coherence
-    key, no sort) change only speed."""
+    key, no sort, work hand-over budget incl. a queue that overflows) change
+    only speed."""
     from lightpycl_amd.engine import Engine
     for k, v in cfg.items():
         monkeypatch.setenv(k, v)

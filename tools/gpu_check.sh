@@ -15,4 +15,4 @@ run() {  # run <limit> <log> <cmd...>
 run 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 run ${PYTEST_LIMIT:-600} pytest_gpu.log python -m pytest tests -m gpu -x -q ${PYTEST_ARGS}
 run 300 bench.log python bench.py ${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu}
-tail -3 gpurun_out/smoke.log gpurun_out/pytest_gpu.log gpurun_out/bench.log
+tail -n 3 gpurun_out/smoke.log gpurun_out/pytest_gpu.log gpurun_out/bench.log

@@ -28,7 +28,7 @@ in_pow = float(np.sum(p, dtype=np.float64))
 ref = None
 for cfg in configs:
     env = dict(kv.split("=") for kv in cfg.split(",") if kv)
-    for k in ("KEY", "FLAT", "TARGET_BLOCKS", "SORT"):
+    for k in ("KEY", "FLAT", "TARGET_BLOCKS", "SORT", "BUDGET", "SPILL_CAP", "SPILL_BLOCKS", "LOOP"):
         os.environ.pop("LPC_" + k, None)
     for k, v in env.items():
         os.environ["LPC_" + k] = v

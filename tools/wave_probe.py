@@ -33,7 +33,14 @@ print(f"{name} level {level}: {nin} rays, intersect stage {pr['intersect_ms']:.3
       f"{rec.shape[0]} (piece, packet) waves, {live.sum()} past the root")
 q = np.percentile(us[live], [50, 90, 99, 99.9, 100]) if live.any() else []
 print("wave us p50/p90/p99/p99.9/max:", " ".join(f"{v:.1f}" for v in q))
-print(f"sum of wave time {us.sum() / 1e3:.2f} ms; nodes {rec[:, 1].sum()}, exact {rec[:, 2].sum()}")
+print(f"sum of wave time {us.sum() / 1e3:.2f} ms; nodes {rec[:, 1].sum()}, exact {rec[:, 2].sum()}; "
+      f"sum / 7168 resident waves = {us.sum() / 7168 / 1e3:.3f} ms; "
+      f"us per node (waves without exact tests) {np.median(us[live & (rec[:, 2] == 0)] / np.maximum(rec[live & (rec[:, 2] == 0), 1], 1)) if (live & (rec[:, 2] == 0)).any() else 0:.2f}")
+big = live & (rec[:, 2] > 0)
+if big.any():
+    A = np.stack([rec[big, 1], rec[big, 2], np.ones(big.sum())], 1).astype(np.float64)
+    coef = np.linalg.lstsq(A, us[big], rcond=None)[0]
+    print(f"fit wave us = {coef[0]:.3f}*nodes + {coef[1]:.4f}*exact + {coef[2]:.2f}")
 order = np.argsort(-us)[:15]
 for i in order:
     print(f"  piece {rec[i, 3]:4d} packet {i % max(1, (nin + 63) // 64):7d}: {us[i]:8.1f} us  "
