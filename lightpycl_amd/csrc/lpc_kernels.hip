@@ -151,7 +151,7 @@ static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__
 }
 
 // Stack depth per wave (node refs); the host checks every hierarchy fits.
-#define LPC_STACK 32
+#define LPC_STACK 64
 
 // k-th set bit (0-based) of m.
 static __device__ __forceinline__ int select_bit(uint64_t m, int k)
@@ -181,9 +181,10 @@ struct WaveLds {
 // rays (filter form d <= 0, see filter_record; node data wave-uniform through
 // the scalar cache); a child node is pushed when any ray passes it, a child
 // triangle's (index, lane mask) is queued for the exact test.
+template <int W>
 static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, const float *__restrict__ rs,
                                                    int64_t n, const int32_t *__restrict__ perm,
-                                                   const Node4 *__restrict__ nodes,
+                                                   const NodeW<W> *__restrict__ nodes,
                                                    const ExactRec *__restrict__ xrec, GItem *__restrict__ gitems,
                                                    int32_t *__restrict__ gcount, int gmax, int64_t gslot,
                                                    const Piece &P, int64_t w, int piece_id, float eps,
@@ -282,23 +283,25 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
             budget = 0;
         }
         const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
-        const Node4 N = nodes[node];
+        const NodeW<W> N = nodes[node];
         ++n_nodes;
-        // the four child tests as two packed pairs
-        const lpc_f2 d01 = filter_test2(lpc_f2{N.cx[0], N.cx[1]}, lpc_f2{N.cy[0], N.cy[1]}, lpc_f2{N.cz[0], N.cz[1]},
-                                        lpc_f2{N.negB[0], N.negB[1]}, lpc_f2{N.negA[0], N.negA[1]}, O.x, O.y, O.z,
-                                        nx, ny, nz);
-        const lpc_f2 d23 = filter_test2(lpc_f2{N.cx[2], N.cx[3]}, lpc_f2{N.cy[2], N.cy[3]}, lpc_f2{N.cz[2], N.cz[3]},
-                                        lpc_f2{N.negB[2], N.negB[3]}, lpc_f2{N.negA[2], N.negA[3]}, O.x, O.y, O.z,
-                                        nx, ny, nz);
-        const float d[4] = {d01.x, d01.y, d23.x, d23.y};
+        // the W child tests as packed pairs
+        float d[W];
+#pragma unroll
+        for (int k = 0; k < W; k += 2) {
+            const lpc_f2 r = filter_test2(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
+                                          lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
+                                          lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz);
+            d[k] = r.x;
+            d[k + 1] = r.y;
+        }
         if (N.ref[0] >= 0) {                       // internal node: children are nodes
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
+            for (int k = 0; k < W; ++k)
                 if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
         } else {                                   // leaf: triangles -> queue, fan groups -> k_groups
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < W; ++k) {
                 const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
                 if (!m) continue;
                 const int32_t ref = N.ref[k];
@@ -358,9 +361,10 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
 
 // k_intersect: grid = (ceil(n/256), pieces), block = 4 waves, one (packet,
 // piece) per wave.
+template <int W>
 __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                    const int32_t *__restrict__ perm,
-                                                   const Node4 *__restrict__ nodes,
+                                                   const NodeW<W> *__restrict__ nodes,
                                                    const ExactRec *__restrict__ xrec,
                                                    GItem *__restrict__ gitems, int32_t *__restrict__ gcount,
                                                    int gmax, const Piece *__restrict__ pieces, float eps,
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
     for (int p = p0; p < p1; ++p) {
         const Piece P = pieces[p];
         const int64_t slot = (int64_t)p * ((n + 63) / 64) + w;
-        trav_packet(lds[wv], R, rs, n, perm, nodes, xrec, gitems, gcount, gmax, slot, P, w, p, eps, max_ray_len,
+        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, gitems, gcount, gmax, slot, P, w, p, eps, max_ray_len,
                     skey, scnt, stats, wrec, slot, SP);
     }
 }
@@ -389,8 +393,9 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
 // k_spill: the subtrees k_intersect handed over (SpillArgs), one item per wave,
 // grid-stride over the queue (its length is read on the device).  Items do not
 // hand over again.  Only used without fan groups (the host checks).
+template <int W>
 __global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                               const int32_t *__restrict__ perm, const Node4 *__restrict__ nodes,
+                                               const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                unsigned long long *__restrict__ stats, SpillArgs SP)
@@ -398,14 +403,14 @@ __global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict
     __shared__ WaveLds lds[4];
     const int wv = threadIdx.x >> 6;
     const uint32_t total = min(*SP.ctr, SP.cap);
-    const uint32_t W = gridDim.x * 4u;
-    for (uint32_t it = blockIdx.x * 4u + (uint32_t)wv; it < total; it += W) {
+    const uint32_t stride = gridDim.x * 4u;
+    for (uint32_t it = blockIdx.x * 4u + (uint32_t)wv; it < total; it += stride) {
         const SpillItem I = SP.items[it];
         if (I.node < 0) continue;
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
-        trav_packet(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
+        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
                     max_ray_len, skey, scnt, stats, nullptr, 0, SpillArgs{nullptr, nullptr, 0u, 0}, I.node);
     }
 }
@@ -467,9 +472,12 @@ __global__ __launch_bounds__(256) void k_groups(RaysIn R, const float *__restric
 }
 
 // k_slivers: the run's slivers (line filter) for packets of 128 rays (two per
-// lane), grid = (ceil(n/512), sliver pieces of <= 64 slivers): lane-parallel
-// packet_sliver_test against the wave's PacketRec, then the per-ray line filter
-// and the exact test for the candidates.
+// lane), grid = (ceil(n / (512 ppw)), sliver pieces of <= 64 slivers): a wave
+// holds its piece's slivers one per lane and takes ppw consecutive packets in
+// turn: lane-parallel packet_sliver_test against the packet's PacketRec (scalar
+// loads), then, for the slivers that pass, the per-ray line filter and the exact
+// test.  Most (packet, piece) pairs fail the packet test, so a wave's fixed cost
+// (sliver records, loop setup) is spread over ppw packets.
 __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                  const int32_t *__restrict__ perm,
                                                  const PacketRec *__restrict__ pk,
@@ -477,65 +485,69 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
                                                  const Piece *__restrict__ pieces, float eps, float max_ray_len,
                                                  unsigned long long *__restrict__ skey,
                                                  int32_t *__restrict__ scnt,
-                                                 unsigned long long *__restrict__ stats)
+                                                 unsigned long long *__restrict__ stats, int ppw)
 {
     const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w * 128 >= n) return;
+    const int64_t npk = (n + 127) / 128;
+    const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
+    if (w0 >= npk) return;
+    const int64_t w1 = min(w0 + (int64_t)ppw, npk);
     const Piece P = pieces[blockIdx.y];
-    const PacketRec Q = pk[w];
     const int32_t j = P.s_lo + lane;
     SliverRec S;
     if (j < P.s_hi) S = srec[j];
     else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
-    uint64_t m = __builtin_amdgcn_ballot_w64(packet_sliver_test(Q, S));
-    if (!m) return;
-    const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
-    f3 O0, O1, D0, D1;
-    load_ray(R, rs, n, s0 < n ? s0 : n - 1, O0, D0);
-    load_ray(R, rs, n, s1 < n ? s1 : n - 1, O1, D1);
-    const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
-    const f2 dx = {D0.x, D1.x}, dy = {D0.y, D1.y}, dz = {D0.z, D1.z};
-    const f2 dl = {sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z), sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z)};
-    float t0 = max_ray_len, t1 = max_ray_len;
-    int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
+    const int64_t o = (int64_t)P.slot * n;
     uint32_t n_tests = 0, n_exact = 0;
-    while (m) {
-        const int k = __builtin_ctzll(m);
-        m &= m - 1;
-        const float v0x = bcast(S.v0x, k), v0y = bcast(S.v0y, k), v0z = bcast(S.v0z, k);
-        const float e2x = bcast(S.e2x, k), e2y = bcast(S.e2y, k), e2z = bcast(S.e2z, k);
-        const float sa = bcast(S.a, k), sbb = bcast(S.b, k);
-        const f2 tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
-        const f2 cx = e2y * tz - e2z * ty;
-        const f2 cy = e2z * tx - e2x * tz;
-        const f2 cz = e2x * ty - e2y * tx;
-        const f2 x = dx * cx + dy * cy + dz * cz;
-        const f2 tm = {fmaxf(fmaxf(fabsf(tx.x), fabsf(ty.x)), fabsf(tz.x)),
-                       fmaxf(fmaxf(fabsf(tx.y), fabsf(ty.y)), fabsf(tz.y))};
-        const f2 rhs = dl * (sa + sbb * tm);
-        const f2 d = x * x - rhs * rhs;
-        ++n_tests;
-        const bool r0 = d.x <= 0.0f, r1 = d.y <= 0.0f;
-        if (!any_lane(r0 || r1)) continue;
-        const int32_t idx = bcasti(S.idx, k);
-        const f3 V0 = mk3(v0x, v0y, v0z);
-        const f3 E1 = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
-        const f3 E2 = mk3(e2x, e2y, e2z);
-        if (r0) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
-        if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
-        n_exact += (uint32_t)r0 + (uint32_t)r1;
+    for (int64_t w = w0; w < w1; ++w) {
+        const PacketRec Q = pk[w];
+        uint64_t m = __builtin_amdgcn_ballot_w64(packet_sliver_test(Q, S));
+        if (!m) continue;
+        const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
+        f3 O0, O1, D0, D1;
+        load_ray(R, rs, n, s0 < n ? s0 : n - 1, O0, D0);
+        load_ray(R, rs, n, s1 < n ? s1 : n - 1, O1, D1);
+        const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
+        const f2 dx = {D0.x, D1.x}, dy = {D0.y, D1.y}, dz = {D0.z, D1.z};
+        const f2 dl = {sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z), sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z)};
+        float t0 = max_ray_len, t1 = max_ray_len;
+        int32_t i0 = -1, i1 = -1, c0 = 0, c1 = 0;
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            const float v0x = bcast(S.v0x, k), v0y = bcast(S.v0y, k), v0z = bcast(S.v0z, k);
+            const float e2x = bcast(S.e2x, k), e2y = bcast(S.e2y, k), e2z = bcast(S.e2z, k);
+            const float sa = bcast(S.a, k), sbb = bcast(S.b, k);
+            const f2 tx = ox - v0x, ty = oy - v0y, tz = oz - v0z;
+            const f2 cx = e2y * tz - e2z * ty;
+            const f2 cy = e2z * tx - e2x * tz;
+            const f2 cz = e2x * ty - e2y * tx;
+            const f2 x = dx * cx + dy * cy + dz * cz;
+            const f2 tm = {fmaxf(fmaxf(fabsf(tx.x), fabsf(ty.x)), fabsf(tz.x)),
+                           fmaxf(fmaxf(fabsf(tx.y), fabsf(ty.y)), fabsf(tz.y))};
+            const f2 rhs = dl * (sa + sbb * tm);
+            const f2 d = x * x - rhs * rhs;
+            ++n_tests;
+            const bool r0 = d.x <= 0.0f, r1 = d.y <= 0.0f;
+            if (!any_lane(r0 || r1)) continue;
+            const int32_t idx = bcasti(S.idx, k);
+            const f3 V0 = mk3(v0x, v0y, v0z);
+            const f3 E1 = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
+            const f3 E2 = mk3(e2x, e2y, e2z);
+            if (r0) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
+            if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
+            n_exact += (uint32_t)r0 + (uint32_t)r1;
+        }
+        if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
+        if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1);
     }
     if (stats) {
-        for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
+        for (int q = 32; q >= 1; q >>= 1) n_exact += __shfl_xor(n_exact, q, 64);
         if (lane == 0) {
             atomicAdd(&stats[1], (unsigned long long)n_tests);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
         }
     }
-    const int64_t o = (int64_t)P.slot * n;
-    if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
-    if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1);
 }
 
 // Rays in coherence order, SoA [6][n] (ox oy oz dx dy dz), read coalesced by

@@ -319,16 +319,20 @@ LPC_HD lpc_f2 filter_test2(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2 
 #define LPC_FILT_REL 2e-3
 #define LPC_FILT_ABS 2e-10
 
-// One node of a mesh run's 4-wide sphere hierarchy, children in SoA form.
-// ref[k] >= 0: child node; ref[k] < 0: triangle ~ref[k], whose test is the
-// triangle's own filter record.  A node's test (in its parent) is node_record()
-// of ALL triangles below it, so a ray whose line Moller-Trumbore accepts against
-// some triangle passes every test on the way down.  Unused children: never.
-struct Node4 {
-    float cx[4], cy[4], cz[4], negB[4], negA[4];
-    int32_t ref[4];
-    int32_t pad[8];
+// One node of a mesh run's W-wide sphere hierarchy (W = 4 or 8), children in
+// SoA form.  ref[k] >= 0: child node; ref[k] < 0: triangle ~ref[k], whose test
+// is the triangle's own filter record.  A node's test (in its parent) is
+// node_record() of ALL triangles below it, so a ray whose line Moller-Trumbore
+// accepts against some triangle passes every test on the way down.  Unused
+// children: never.  128 B (W 4) / 256 B (W 8): whole scalar-load lines.
+template <int W>
+struct NodeW {
+    float cx[W], cy[W], cz[W], negB[W], negA[W];
+    int32_t ref[W];
+    int32_t pad[W == 4 ? 8 : 16];
 };
+typedef NodeW<4> Node4;
+typedef NodeW<8> Node8;
 
 // Leaf children are triangles or "fan groups".  A fan group holds up to
 // LPC_GROUP_SIZE thin triangles whose filter spheres pile up around a common

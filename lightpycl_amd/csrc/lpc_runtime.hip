@@ -102,6 +102,10 @@ struct lpc_handle {
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 2048;                    // k_spill grid (4 waves each, grid-stride)
     bool piece_loop = false;                        // k_intersect: waves loop over the pieces
+    int node_w = 8;                                 // hierarchy width for the next build (4 or 8)
+    int built_w = 4;                                // width of the records in d_nodes
+    int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
+    int64_t sliver_ppw = 0;                         // k_slivers: packets per wave (0: from sliver_waves)
     DBuf w_spill;                                   // k_spill queue
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
@@ -188,9 +192,9 @@ static inline unsigned grid1(int64_t n, int bs = 256) { return (unsigned)((n + b
 // Top-down partition of idx[0, n) for a subtree of capacity cap (4 * 2^k): split
 // at min(n, cap/2) along the longest axis of the centroids' bbox (nth_element),
 // recurse on both halves with cap/2, down to groups of 4.
-static void split_order(int32_t *idx, int64_t n, int64_t cap, const std::vector<double> &cen)
+static void split_order(int32_t *idx, int64_t n, int64_t cap, const std::vector<double> &cen, int64_t leaf = 4)
 {
-    if (cap <= 4 || n <= 1) return;
+    if (cap <= leaf || n <= 1) return;
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int64_t i = 0; i < n; ++i)
         for (int k = 0; k < 3; ++k) {
@@ -206,8 +210,8 @@ static void split_order(int32_t *idx, int64_t n, int64_t cap, const std::vector<
             const double ca = cen[3 * (size_t)a + ax], cb = cen[3 * (size_t)b + ax];
             return ca < cb || (ca == cb && a < b);
         });
-    split_order(idx, half, cap / 2, cen);
-    split_order(idx + half, n - half, cap / 2, cen);
+    split_order(idx, half, cap / 2, cen, leaf);
+    split_order(idx + half, n - half, cap / 2, cen, leaf);
 }
 
 // Per mesh run: a 4-wide sphere hierarchy built bottom-up over its triangles in
@@ -234,7 +238,10 @@ static void drop_piece_tables(lpc_handle *h)
 static int build_records(lpc_handle *h)
 {
     drop_piece_tables(h);   // pieces index the records built here
-    std::vector<Node4> nodes;
+    const int W = h->node_w;                        // hierarchy width (4 or 8)
+    const size_t node_bytes = W == 8 ? sizeof(Node8) : sizeof(Node4);
+    std::vector<uint8_t> nodes;                     // NodeW<W> records
+    int32_t n_nodes = 0;
     std::vector<SliverRec> slivers;
     h->run_levels.clear();
     h->node_self.clear();
@@ -352,9 +359,9 @@ static int build_records(lpc_handle *h)
             for (int k = 0; k < 3; ++k) ecen[3 * (size_t)i + k] = E[(size_t)i].c[k];
         std::vector<int32_t> perm_t((size_t)cnt);
         for (int32_t i = 0; i < cnt; ++i) perm_t[(size_t)i] = i;
-        int64_t cap = 4;
-        while (cap < cnt) cap *= 4;
-        split_order(perm_t.data(), cnt, cap, ecen);
+        int64_t cap = W;
+        while (cap < cnt) cap *= W;
+        split_order(perm_t.data(), cnt, cap, ecen, W);
         // every hierarchy entry covers a contiguous range of ordered entries; its
         // test is node_record() of all their triangles
         std::vector<const float *> tv;
@@ -380,34 +387,36 @@ static int build_records(lpc_handle *h)
         std::vector<std::pair<int32_t, int32_t>> levels;   // (first node, count), bottom up
         do {
             std::vector<Ent> up;
-            const int32_t first = (int32_t)nodes.size();
-            for (size_t i = 0; i < ent.size(); i += 4) {
-                Node4 N;
-                memset(&N, 0, sizeof(N));
-                for (int k = 0; k < 4; ++k) {
+            const int32_t first = n_nodes;
+            for (size_t i = 0; i < ent.size(); i += (size_t)W) {
+                // NodeW<W> layout: cx cy cz negB negA [W] floats, ref [W], pad
+                std::vector<uint32_t> N(node_bytes / 4, 0u);
+                for (int k = 0; k < W; ++k) {
                     const bool use = i + k < ent.size();
                     const FiltRec &m = use ? ent[i + k].t : never;
-                    N.cx[k] = m.cx; N.cy[k] = m.cy; N.cz[k] = m.cz;
-                    N.negB[k] = m.negB; N.negA[k] = m.negA;
-                    N.ref[k] = use ? ent[i + k].ref : ~0;
+                    const float f5[5] = {m.cx, m.cy, m.cz, m.negB, m.negA};
+                    for (int q = 0; q < 5; ++q) memcpy(&N[(size_t)q * W + k], &f5[q], 4);
+                    const int32_t ref = use ? ent[i + k].ref : ~0;
+                    memcpy(&N[(size_t)5 * W + k], &ref, 4);
                 }
-                const int32_t a = ent[i].a, b = ent[std::min(i + 3, ent.size() - 1)].b;
+                const int32_t a = ent[i].a, b = ent[std::min(i + (size_t)W - 1, ent.size() - 1)].b;
                 const FiltRec self = range_test(a, b);
                 int32_t ng = 0;
-                for (int k = 0; k < 4 && i + k < ent.size(); ++k) {
+                for (int k = 0; k < W && i + k < ent.size(); ++k) {
                     const int32_t ref = ent[i + k].ref;
                     ng += ref >= 0 ? h->node_groups[(size_t)ref] : ref < LPC_GROUP_REF ? 1 : 0;
                 }
-                up.push_back({self, (int32_t)nodes.size(), a, b});
-                nodes.push_back(N);
+                up.push_back({self, n_nodes, a, b});
+                nodes.insert(nodes.end(), (const uint8_t *)N.data(), (const uint8_t *)N.data() + node_bytes);
+                ++n_nodes;
                 h->node_self.push_back(self);
                 h->node_groups.push_back(ng);
             }
             levels.push_back({first, (int32_t)up.size()});
             ent.swap(up);
         } while (ent.size() > 1);
-        // 4-wide: at most 3 siblings wait per level on a wave's stack
-        if (3 * (int)levels.size() + 1 > LPC_STACK) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
+        // W-wide: at most W - 1 siblings wait per level on a wave's stack
+        if ((W - 1) * (int)levels.size() + 1 > LPC_STACK) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
         for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
             h->run_levels.back().push_back(it->first);
             h->run_levels.back().push_back(it->second);
@@ -418,19 +427,19 @@ static int build_records(lpc_handle *h)
     RETIF(dalloc(h, h->d_gxrec, gxrec.size() * sizeof(ExactRec)));
     HIPCHK(h, hipMemcpy(h->d_grec.p, grec.data(), grec.size() * sizeof(FiltRec), hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_gxrec.p, gxrec.data(), gxrec.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
-    if ((int64_t)nodes.size() > INT32_MAX / 2) return set_err(h, LPC_E_ARG, "too many triangles");
     // spare records so no buffer is empty
-    if (nodes.empty()) { Node4 N; memset(&N, 0, sizeof(N)); nodes.push_back(N); }
+    if (n_nodes == 0) { nodes.assign(node_bytes, 0); n_nodes = 1; }
     if (slivers.empty()) {
         SliverRec ss;
         memset(&ss, 0, sizeof(ss));
         ss.a = NAN; ss.idx = -1;
         slivers.push_back(ss);
     }
-    h->Mpad = (int32_t)nodes.size();
-    RETIF(dalloc(h, h->d_nodes, nodes.size() * sizeof(Node4)));
+    h->Mpad = n_nodes;
+    h->built_w = W;
+    RETIF(dalloc(h, h->d_nodes, nodes.size()));
     RETIF(dalloc(h, h->d_srec, slivers.size() * sizeof(SliverRec)));
-    HIPCHK(h, hipMemcpy(h->d_nodes.p, nodes.data(), nodes.size() * sizeof(Node4), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_nodes.p, nodes.data(), nodes.size(), hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_srec.p, slivers.data(), slivers.size() * sizeof(SliverRec),
                         hipMemcpyHostToDevice));
     return 0;
@@ -666,13 +675,24 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         }
         const int loop = h->piece_loop ? (int)pt->npieces : 0;
         const dim3 grid((unsigned)((n + 255) / 256), loop ? 1u : (unsigned)pt->npieces);
-        hipLaunchKernelGGL(k_intersect, grid, dim3(256), 0, h->stream, in, rs, n, perm, (const Node4 *)h->d_nodes.p,
-                           (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax, (const Piece *)pt->pieces.p, eps,
-                           max_ray_len, skey, scnt, stats, wrec, SP, loop);
-        if (SP.budget > 0)
-            hipLaunchKernelGGL(k_spill, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n, perm,
-                               (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
-                               scnt, stats, SP);
+        if (h->built_w == 8)
+            hipLaunchKernelGGL(k_intersect<8>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
+                               (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
+                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, loop);
+        else
+            hipLaunchKernelGGL(k_intersect<4>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
+                               (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
+                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, loop);
+        if (SP.budget > 0) {
+            if (h->built_w == 8)
+                hipLaunchKernelGGL(k_spill<8>, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n,
+                                   perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
+                                   max_ray_len, skey, scnt, stats, SP);
+            else
+                hipLaunchKernelGGL(k_spill<4>, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n,
+                                   perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
+                                   max_ray_len, skey, scnt, stats, SP);
+        }
         if (gmax > 0) {
             hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
                                (PacketRec *)h->w_pk64.p);
@@ -686,9 +706,14 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (pt->nspieces > 0) {
         hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, h->stream, in, rs, n,
                            (PacketRec *)h->w_pk.p);
-        hipLaunchKernelGGL(k_slivers, dim3((unsigned)((n + 511) / 512), (unsigned)pt->nspieces), dim3(256), 0,
-                           h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p, (const SliverRec *)h->d_srec.p,
-                           (const Piece *)pt->spieces.p, eps, max_ray_len, skey, scnt, stats);
+        // packets per wave: enough (packet, piece) waves to fill the GPU, no more
+        const int64_t npk128 = (n + 127) / 128;
+        const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
+                                              : std::max<int64_t>(1, npk128 * pt->nspieces / h->sliver_waves);
+        hipLaunchKernelGGL(k_slivers, dim3((unsigned)((npk128 + 4 * ppw - 1) / (4 * ppw)), (unsigned)pt->nspieces),
+                           dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
+                           (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
+                           scnt, stats, (int)ppw);
         HIPCHK(h, hipGetLastError());
     }
     if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
@@ -782,6 +807,9 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
     h->piece_loop = env_int("LPC_LOOP", h->piece_loop) != 0;
+    h->node_w = env_int("LPC_NODE_W", h->node_w) == 4 ? 4 : 8;
+    h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
+    h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
     if (hipHostMalloc((void **)&h->acc_host, sizeof(DevAcc), hipHostMallocDefault) != hipSuccess) {
         g_open_err = "pinned host buffer";
         lpc_close(h);

@@ -75,7 +75,9 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
                                  dict(LPC_FLAT="20", LPC_KEY="2"), dict(LPC_KEY="3"), dict(LPC_KEY="1"),
                                  dict(LPC_SORT="0"), dict(LPC_BUDGET="16"), dict(LPC_BUDGET="4"),
                                  dict(LPC_BUDGET="6", LPC_SPILL_CAP="100"), dict(LPC_LOOP="1"),
-                                 dict(LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1")])
+                                 dict(LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1"),
+                                 dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_NODE_W="4"),
+                                 dict(LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536")])
 def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
     """The launch policies (fan-group threshold, piece granularity, coherence
     key, no sort, work hand-over budget incl. a queue that overflows) change

@@ -30,7 +30,7 @@ for d in sorted(os.listdir(src)):
 summary = {k: {c: {"launches": len(v), "mean": sum(v) / len(v), "values": v} for c, v in cs.items()}
            for k, cs in per.items()}
 json.dump(summary, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
-ki = summary.get("lpck::k_intersect", {})
+ki = next((v for k, v in summary.items() if "k_intersect" in k), {})
 if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
     fetch, write = ki["FETCH_SIZE"]["mean"], ki["WRITE_SIZE"]["mean"]
     rec = {"source": f"profiles/{tag}_pmc.json", "kernel": "k_intersect",
