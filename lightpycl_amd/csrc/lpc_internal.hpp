@@ -39,10 +39,10 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 #define LPC_STATS_WORDS (LPC_STATS_PIECE + LPC_STATS_PIECES)
 
 // Per-launch device words of the intersect stage (uint32, reset by k_slot_init):
-// [0..5] population origin box (k_bbox, coherence key modes 1-2), [6] spill
-// items queued by k_intersect (k_spill).
-#define LPC_MISC_WORDS 8
-#define LPC_MISC_SPILL 6
+// [0..5] population origin box (k_bbox, coherence key modes 1-2), [6..13]
+// hand-over queue lengths (k_intersect -> k_spill level 0 -> level 1 ...).
+#define LPC_MISC_WORDS 16
+#define LPC_MISC_SPILL 6                  // [6 + l]: items queued for hand-over level l (l < 8)
 
 // Work hand-over: a k_intersect wave that has visited `budget` nodes with two or
 // more subtrees still on its stack queues each of them as one item; k_spill
@@ -55,7 +55,8 @@ struct SpillArgs {
     SpillItem *items;
     uint32_t *ctr;                    // misc + LPC_MISC_SPILL
     uint32_t cap;
-    int budget;                       // nodes before hand-over (0: never)
+    int budget;                       // cost before hand-over (0: never), in node visits
+    int pair_shift;                   // exact pairs per node visit = 1 << pair_shift (31: not counted)
 };
 
 // A fan group met by a k_intersect wave (packet, piece): group id and the rays

@@ -193,7 +193,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
                                                    uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0,
-                                                   SpillArgs SP = SpillArgs{nullptr, nullptr, 0u, 0},
+                                                   SpillArgs SP = SpillArgs{nullptr, nullptr, 0u, 0, 31},
                                                    int32_t start = -1)
 {
     const int lane = threadIdx.x & 63;
@@ -218,6 +218,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     const uint64_t clk0 = (stats || wrec) ? wall_clock64() : 0;
     int32_t top = 0, nq = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
+    uint32_t n_pairs = 0;                           // exact pairs drained (wave-uniform; hand-over cost)
     // Exact tests are deferred: candidate (triangle, ray lanes) entries queue up
     // in LDS; a drain expands them into (triangle, ray) pairs, runs 64 pairs at a
     // time one per lane (exact record gathered, ray read from LDS) and folds the
@@ -233,7 +234,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
             if (lane >= o) incl += v;
         }
         L.qscan[lane] = incl;
-        const int total = __shfl(incl, 63, 64);
+        const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+        n_pairs += (uint32_t)total;
         for (int base = 0; base < total; base += 64) {
             const int q = base + lane;
             if (q < total) {
@@ -265,7 +267,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
         // work hand-over: after `budget` nodes the subtrees left on the stack go
         // to k_spill, one wave each (a wave stuck in a dense region would
         // otherwise be the launch's critical path)
-        if (budget > 0 && (int)n_nodes >= budget && top >= 2) {
+        // cost so far in node-visit units: one visit ~ 32 exact pairs (tools/wave_probe.py fit)
+        if (budget > 0 && (int)(n_nodes + (n_pairs >> SP.pair_shift)) >= budget && top >= 2) {
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(SP.ctr, (uint32_t)top);
             base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0);
@@ -390,15 +393,18 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
     }
 }
 
-// k_spill: the subtrees k_intersect handed over (SpillArgs), one item per wave,
-// grid-stride over the queue (its length is read on the device).  Items do not
-// hand over again.  Only used without fan groups (the host checks).
+// k_spill: the subtrees handed over by the previous level (queue `in`), one item
+// per wave, grid-stride over the queue (its length is read on the device).  An
+// item that again exceeds the budget hands its remaining subtrees to the next
+// level's queue (`out`; budget 0 on the last level).  Only used without fan
+// groups (the host checks).
 template <int W>
 __global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
-                                               unsigned long long *__restrict__ stats, SpillArgs SP)
+                                               unsigned long long *__restrict__ stats, SpillArgs SP,
+                                               SpillArgs out)
 {
     __shared__ WaveLds lds[4];
     const int wv = threadIdx.x >> 6;
@@ -411,7 +417,7 @@ __global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
         trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
-                    max_ray_len, skey, scnt, stats, nullptr, 0, SpillArgs{nullptr, nullptr, 0u, 0}, I.node);
+                    max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
     }
 }
 
@@ -562,6 +568,19 @@ __global__ __launch_bounds__(256) void k_gather(RaysIn R, int64_t n, const int32
     rs[3 * n + s] = R.dx[q]; rs[4 * n + s] = R.dy[q]; rs[5 * n + s] = R.dz[q];
 }
 
+// k_gather from the 32-byte rows k_raykey wrote: one cache line per ray instead
+// of one per component (the permutation is random with respect to memory).
+__global__ __launch_bounds__(256) void k_gather_aos(const float4 *__restrict__ aos, int64_t n,
+                                                    const int32_t *__restrict__ perm, float *__restrict__ rs)
+{
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int64_t q = perm[s];
+    const float4 a = aos[2 * q], b = aos[2 * q + 1];
+    rs[s] = a.x; rs[n + s] = a.y; rs[2 * n + s] = a.z;
+    rs[3 * n + s] = a.w; rs[4 * n + s] = b.x; rs[5 * n + s] = b.y;
+}
+
 // Slot initial state: slots a run flushes into start at (max_ray_len, idx -1,
 // count 0); slots no run writes keep the reference's initial scratch
 // (max_ray_len, idx 0, count 0).  Also empties the launch's origin box (misc).
@@ -651,10 +670,14 @@ __global__ __launch_bounds__(256) void k_bbox(RaysIn R, int64_t n, uint32_t *__r
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
                                                 float sx, float sy, float sz, const uint32_t *__restrict__ bb,
                                                 int64_t split, int dir_major, uint32_t *__restrict__ keys,
-                                                int32_t *__restrict__ vals)
+                                                int32_t *__restrict__ vals, float4 *__restrict__ aos)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (aos) {          // the ray as one 32-byte row: k_gather_aos reads it with one line per ray
+        aos[2 * i] = make_float4(R.ox[i], R.oy[i], R.oz[i], R.dx[i]);
+        aos[2 * i + 1] = make_float4(R.dy[i], R.dz[i], 0.0f, 0.0f);
+    }
     if (bb) {
         const float lo[3] = {ord_dec(bb[0]), ord_dec(bb[1]), ord_dec(bb[2])};
         const float hi[3] = {ord_dec(bb[3]), ord_dec(bb[4]), ord_dec(bb[5])};

@@ -88,6 +88,8 @@ struct lpc_handle {
     int64_t ws_rays = 0;
     DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
+    DBuf w_aos;                                     // rays as 32-byte rows for the coherence gather
+    bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
     DBuf w_pk64;                                    // PacketRec per 64-ray packet (k_groups)
@@ -95,13 +97,17 @@ struct lpc_handle {
     DBuf d_misc;                                    // LPC_MISC_WORDS per-launch words
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
+    int64_t sort_min = 4096;                        // populations below this are traced unsorted
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
     int64_t target_blocks = 16384;                  // k_intersect: blocks x pieces to fill the GPU
-    int spill_budget = 0;                           // k_intersect nodes before hand-over to k_spill (0 off)
+    int spill_budget = 16;                          // node visits before a wave hands over (0 off)
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
-    int64_t spill_blocks = 2048;                    // k_spill grid (4 waves each, grid-stride)
+    int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
+    int spill_levels = 4;                           // k_spill launches (hand-over depth)
+    int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
     bool piece_loop = false;                        // k_intersect: waves loop over the pieces
+    int64_t loop_min_packets = 8192;                //   ... when the population has this many packets
     int node_w = 8;                                 // hierarchy width for the next build (4 or 8)
     int built_w = 4;                                // width of the records in d_nodes
     int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
@@ -543,6 +549,7 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_blk_pow, (size_t)nb * 8));
         RETIF(dalloc(h, h->w_soa, (size_t)8 * C * 4));
         RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
+        RETIF(dalloc(h, h->w_aos, (size_t)C * 32));
         RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
         size_t tb = 0;
         HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
@@ -619,7 +626,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                        h->K, (const int32_t *)h->d_live.p, max_ray_len, skey, scnt, misc);
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
-    if (h->sort_rays && n >= 4096) {
+    if (h->sort_rays && n >= h->sort_min) {
         // coherence order: rays of one wave share origin cell and direction
         const size_t C = (size_t)h->ws_rays;
         uint32_t *kin = (uint32_t *)h->w_sort.p, *kout = kin + C;
@@ -635,12 +642,16 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                            h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
-                           h->key_mode >= 3 ? 1 : 0, kin, vin);
+                           h->key_mode >= 3 ? 1 : 0, kin, vin, h->gather_aos ? (float4 *)h->w_aos.p : nullptr);
         size_t tb = h->sort_tmp_bytes;
         HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, 0, 32,
                                                         h->stream));
         perm = vout;
-        hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
+        if (h->gather_aos)
+            hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
+                               perm, (float *)h->w_rs.p);
+        else
+            hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
         rs = (const float *)h->w_rs.p;
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -665,15 +676,16 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             gcount = (int32_t *)h->w_gcount.p;
         }
         // work hand-over (not with fan groups: a k_spill item has no group slots)
-        SpillArgs SP{nullptr, nullptr, 0u, 0};
+        SpillArgs SP{nullptr, nullptr, 0u, 0, 31};
         if (h->spill_budget > 0 && gmax == 0 && !wrec) {
-            RETIF(dalloc(h, h->w_spill, (size_t)h->spill_cap * sizeof(SpillItem)));
+            RETIF(dalloc(h, h->w_spill, (size_t)2 * h->spill_cap * sizeof(SpillItem)));
             SP.items = (SpillItem *)h->w_spill.p;
             SP.ctr = misc + LPC_MISC_SPILL;
             SP.cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
             SP.budget = h->spill_budget;
+            SP.pair_shift = h->spill_pair_shift;
         }
-        const int loop = h->piece_loop ? (int)pt->npieces : 0;
+        const int loop = (h->piece_loop && (n + 63) / 64 >= h->loop_min_packets) ? (int)pt->npieces : 0;
         const dim3 grid((unsigned)((n + 255) / 256), loop ? 1u : (unsigned)pt->npieces);
         if (h->built_w == 8)
             hipLaunchKernelGGL(k_intersect<8>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
@@ -683,15 +695,24 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             hipLaunchKernelGGL(k_intersect<4>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
                                (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
                                (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, loop);
-        if (SP.budget > 0) {
+        // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and
+        // queues what exceeds the budget for level l + 1; the last level finishes
+        const int levels = SP.budget > 0 ? std::max(1, std::min(h->spill_levels, 7)) : 0;
+        for (int l = 0; l < levels; ++l) {
+            SpillArgs I = SP, O = SP;
+            I.items = (SpillItem *)h->w_spill.p + (size_t)(l % 2) * (size_t)h->spill_cap;
+            I.ctr = misc + LPC_MISC_SPILL + l;
+            O.items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
+            O.ctr = misc + LPC_MISC_SPILL + l + 1;
+            O.budget = l + 1 < levels ? SP.budget : 0;
             if (h->built_w == 8)
                 hipLaunchKernelGGL(k_spill<8>, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n,
                                    perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
-                                   max_ray_len, skey, scnt, stats, SP);
+                                   max_ray_len, skey, scnt, stats, I, O);
             else
                 hipLaunchKernelGGL(k_spill<4>, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n,
                                    perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
-                                   max_ray_len, skey, scnt, stats, SP);
+                                   max_ray_len, skey, scnt, stats, I, O);
         }
         if (gmax > 0) {
             hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
@@ -802,11 +823,16 @@ int lpc_open(int device, lpc_handle **out)
     h->key_mode = (int)env_int("LPC_KEY", h->key_mode);
     h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
+    h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
+    h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
+    h->spill_levels = (int)env_int("LPC_SPILL_LEVELS", h->spill_levels);
+    h->spill_pair_shift = (int)std::min<int64_t>(31, std::max<int64_t>(0, env_int("LPC_PAIR_SHIFT", h->spill_pair_shift)));
     h->piece_loop = env_int("LPC_LOOP", h->piece_loop) != 0;
+    h->loop_min_packets = env_int("LPC_LOOP_MIN", h->loop_min_packets);
     h->node_w = env_int("LPC_NODE_W", h->node_w) == 4 ? 4 : 8;
     h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
     h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
@@ -828,7 +854,7 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
