@@ -135,6 +135,15 @@ int lpc_trace_reset(lpc_handle *h);
  *   out_next_pow (n_reflect + n_refract, capacity 2*n_in) -> termination sum :372 */
 int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
                       int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st);
+/* The reference's iteration loop on one device (iterative_tracer.py:241-391):
+ * lpc_trace_iterate until the next population's power is below
+ * power_threshold (= (1 - trace_until_dissipated) * input power, :383) or no
+ * ray is kept (:389), at most max_iter iterations.  per_iter[max_iter]
+ * receives each iteration's stats, *n_iter their number.  Same results as
+ * calling lpc_trace_iterate from the host loop, without a host round trip
+ * through the caller per iteration. */
+int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                  int32_t *n_iter);
 /* Current population size. */
 int lpc_trace_population(lpc_handle *h, int64_t *n);
 /* Measured record so far: count and per-mesh measured power (double[mesh_count]). */

@@ -556,6 +556,71 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
     }
 }
 
+// k_slivers1: k_slivers for 64-ray packets (one ray per lane, PacketRec of
+// k_packet<1>): tighter packet bounds, fewer slivers pass per ray.
+__global__ __launch_bounds__(256) void k_slivers1(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                  const int32_t *__restrict__ perm,
+                                                  const PacketRec *__restrict__ pk,
+                                                  const SliverRec *__restrict__ srec,
+                                                  const Piece *__restrict__ pieces, float eps, float max_ray_len,
+                                                  unsigned long long *__restrict__ skey,
+                                                  int32_t *__restrict__ scnt,
+                                                  unsigned long long *__restrict__ stats, int ppw)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t npk = (n + 63) / 64;
+    const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
+    if (w0 >= npk) return;
+    const int64_t w1 = min(w0 + (int64_t)ppw, npk);
+    const Piece P = pieces[blockIdx.y];
+    const int32_t j = P.s_lo + lane;
+    SliverRec S;
+    if (j < P.s_hi) S = srec[j];
+    else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
+    const int64_t o = (int64_t)P.slot * n;
+    uint32_t n_tests = 0, n_exact = 0;
+    for (int64_t w = w0; w < w1; ++w) {
+        const PacketRec Q = pk[w];
+        uint64_t m = __builtin_amdgcn_ballot_w64(packet_sliver_test(Q, S));
+        if (!m) continue;
+        const int64_t s0 = w * 64 + lane;
+        f3 O, D;
+        load_ray(R, rs, n, s0 < n ? s0 : n - 1, O, D);
+        const float dl = sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
+        float t0 = max_ray_len;
+        int32_t i0 = -1, c0 = 0;
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            const float v0x = bcast(S.v0x, k), v0y = bcast(S.v0y, k), v0z = bcast(S.v0z, k);
+            const float e2x = bcast(S.e2x, k), e2y = bcast(S.e2y, k), e2z = bcast(S.e2z, k);
+            const float sa = bcast(S.a, k), sbb = bcast(S.b, k);
+            const float tx = O.x - v0x, ty = O.y - v0y, tz = O.z - v0z;
+            const float cx = e2y * tz - e2z * ty, cy = e2z * tx - e2x * tz, cz = e2x * ty - e2y * tx;
+            const float x = D.x * cx + D.y * cy + D.z * cz;
+            const float tm = fmaxf(fmaxf(fabsf(tx), fabsf(ty)), fabsf(tz));
+            const float rhs = dl * (sa + sbb * tm);
+            ++n_tests;
+            const bool r0 = x * x - rhs * rhs <= 0.0f;
+            if (!any_lane(r0)) continue;
+            const int32_t idx = bcasti(S.idx, k);
+            const f3 V0 = mk3(v0x, v0y, v0z);
+            const f3 E1 = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
+            const f3 E2 = mk3(e2x, e2y, e2z);
+            if (r0) mt_accumulate(O, D, V0, E1, E2, idx, eps, t0, i0, c0);
+            n_exact += (uint32_t)r0;
+        }
+        if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
+    }
+    if (stats) {
+        for (int q = 32; q >= 1; q >>= 1) n_exact += __shfl_xor(n_exact, q, 64);
+        if (lane == 0) {
+            atomicAdd(&stats[1], (unsigned long long)n_tests);
+            atomicAdd(&stats[3], (unsigned long long)n_exact);
+        }
+    }
+}
+
 // Rays in coherence order, SoA [6][n] (ox oy oz dx dy dz), read coalesced by
 // every piece of k_intersect.
 __global__ __launch_bounds__(256) void k_gather(RaysIn R, int64_t n, const int32_t *__restrict__ perm,

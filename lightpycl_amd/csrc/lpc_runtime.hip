@@ -112,6 +112,7 @@ struct lpc_handle {
     int built_w = 4;                                // width of the records in d_nodes
     int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
     int64_t sliver_ppw = 0;                         // k_slivers: packets per wave (0: from sliver_waves)
+    int sliver_rays = 128;                          // k_slivers packet size (64 or 128 rays)
     DBuf w_spill;                                   // k_spill queue
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
@@ -725,16 +726,25 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         HIPCHK(h, hipGetLastError());
     }
     if (pt->nspieces > 0) {
-        hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, h->stream, in, rs, n,
-                           (PacketRec *)h->w_pk.p);
         // packets per wave: enough (packet, piece) waves to fill the GPU, no more
-        const int64_t npk128 = (n + 127) / 128;
+        const int rpl = h->sliver_rays == 64 ? 1 : 2;
+        const int64_t npkx = (n + 64 * rpl - 1) / (64 * rpl);
         const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
-                                              : std::max<int64_t>(1, npk128 * pt->nspieces / h->sliver_waves);
-        hipLaunchKernelGGL(k_slivers, dim3((unsigned)((npk128 + 4 * ppw - 1) / (4 * ppw)), (unsigned)pt->nspieces),
-                           dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
-                           (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                           scnt, stats, (int)ppw);
+                                              : std::max<int64_t>(1, npkx * pt->nspieces / h->sliver_waves);
+        const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)pt->nspieces);
+        if (rpl == 1) {
+            hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
+                               (PacketRec *)h->w_pk64.p);
+            hipLaunchKernelGGL(k_slivers1, sg, dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk64.p,
+                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
+                               scnt, stats, (int)ppw);
+        } else {
+            hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
+                               (PacketRec *)h->w_pk.p);
+            hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
+                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
+                               scnt, stats, (int)ppw);
+        }
         HIPCHK(h, hipGetLastError());
     }
     if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
@@ -836,6 +846,7 @@ int lpc_open(int device, lpc_handle **out)
     h->node_w = env_int("LPC_NODE_W", h->node_w) == 4 ? 4 : 8;
     h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
     h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
+    h->sliver_rays = env_int("LPC_SLIVER_RAYS", h->sliver_rays) == 64 ? 64 : 128;
     if (hipHostMalloc((void **)&h->acc_host, sizeof(DevAcc), hipHostMallocDefault) != hipSuccess) {
         g_open_err = "pinned host buffer";
         lpc_close(h);
@@ -1219,6 +1230,23 @@ int lpc_trace_reset(lpc_handle *h)
     h->m_total = 0;                             // measured record emptied in-stream
     hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p, 0ull);
     HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                  int32_t *n_iter)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
+    *n_iter = 0;
+    for (int32_t i = 0; i < max_iter; ++i) {
+        lpc_iter_stats S;
+        RETIF(lpc_trace_iterate(h, nullptr, nullptr, nullptr, nullptr, nullptr, &S));
+        per_iter[i] = S;
+        *n_iter = i + 1;
+        if (S.power_next < power_threshold) break;          // :383
+        if (S.n_reflect + S.n_refract == 0) break;          // :389
+    }
     return 0;
 }
 

@@ -77,6 +77,13 @@ class ShardedTrace:
         bounces = 0
         iters = 0
         counts = []
+        if self.comm is None and hasattr(self.engine, "run_local"):
+            # one process: the same loop inside the library (lpc_trace_run)
+            for st in self.engine.run_local(int(iterations), thr):
+                bounces += int(st.n_in)
+                iters += 1
+                counts.append(int(st.n_in))
+            iterations = 0
         for _ in range(int(iterations)):
             st, _ = self.engine.iterate()
             bounces += int(st.n_in)

@@ -162,6 +162,15 @@ class Engine:
         return st, dict(origin=org, dest=dst, pow=pw, meas=ms,
                         next_pow=nxt[: st.n_reflect + st.n_refract])
 
+    def run_local(self, iterations, power_threshold):
+        """lpc_trace_run: iterate until the next population's power is below
+        power_threshold or no ray is kept (at most `iterations`); per-iteration stats."""
+        cap = max(int(iterations), 0)
+        arr = (_lib.IterStats * max(cap, 1))()
+        k = ctypes.c_int32(0)
+        self._c(self.L.lpc_trace_run(self.h, cap, float(power_threshold), arr, ctypes.byref(k)))
+        return [arr[i] for i in range(k.value)]
+
     def measured(self):
         """(count, per-mesh measured power float64[K])."""
         c = ctypes.c_int64(0)

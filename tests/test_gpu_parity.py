@@ -77,7 +77,7 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
                                  dict(LPC_BUDGET="6", LPC_SPILL_CAP="100"),
                                  dict(LPC_BUDGET="3", LPC_SPILL_LEVELS="5"), dict(LPC_BUDGET="2", LPC_SPILL_LEVELS="7", LPC_SPILL_CAP="3000"), dict(LPC_LOOP="1", LPC_LOOP_MIN="1"),
                                  dict(LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1"),
-                                 dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_NODE_W="4"),
+                                 dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_SLIVER_RAYS="64"), dict(LPC_NODE_W="4"),
                                  dict(LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536")])
 def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
     """The launch policies (fan-group threshold, piece granularity, coherence
@@ -246,3 +246,43 @@ def test_dropin_device_kernels(engine, oracle_mod):
     np.testing.assert_array_equal(td2.cpu().numpy()[:, :3], ref["t_dir"][:, :3])
     np.testing.assert_array_equal(rp.cpu().numpy(), ref["r_pow"])
     np.testing.assert_array_equal(tm.cpu().numpy(), ref["meas"])
+
+
+@pytest.mark.gpu
+def test_trace_run_matches_host_loop(oracle_mod):
+    """lpc_trace_run (the loop in the library) gives the host loop's iterations,
+    counts and measured power, and both match the oracle's trace."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.distributed import ShardedTrace
+    from lightpycl_amd.engine import Engine
+    sc = scenes.BUILDERS["lens"](n=6000, seed=3)
+    o = np.asarray(sc.sources[0].rays_origin, np.float32)
+    d = np.asarray(sc.sources[0].rays_dir, np.float32)
+    p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
+    in_pow = float(np.sum(p, dtype=np.float64))
+    e = Engine(0)
+    e.upload_meshes(sc.meshes)
+    e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+    fast = ShardedTrace(e).run(sc.iterations, sc.tau, in_pow)
+    fast_meas = e.measured()
+    e.reset()
+
+    class NoFast:                      # the same engine without run_local: host loop
+        def __init__(self, eng):
+            self.eng = eng
+
+        def iterate(self):
+            return self.eng.iterate()
+
+        def measured(self):
+            return self.eng.measured()
+
+    slow = ShardedTrace(NoFast(e)).run(sc.iterations, sc.tau, in_pow)
+    slow_meas = e.measured()
+    assert fast["global_counts"] == slow["global_counts"]
+    assert fast_meas[0] == slow_meas[0]
+    np.testing.assert_array_equal(fast_meas[1], slow_meas[1])
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                               keep_results=False)
+    assert fast["global_counts"] == info["counts"]
+    e.close()
