@@ -375,16 +375,18 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
                                                    unsigned long long *__restrict__ skey,
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
-                                                   uint32_t *__restrict__ wrec, SpillArgs SP, int loop_pieces)
+                                                   uint32_t *__restrict__ wrec, SpillArgs SP, int pgroup,
+                                                   int npieces)
 {
     __shared__ WaveLds lds[4];
     const int wv = threadIdx.x >> 6;
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     if (w * 64 >= n) return;                       // whole wave past the end
-    // loop_pieces > 0: grid.y = 1 and the wave takes the pieces in turn (no
-    // waves launched only to fail a piece's root test)
-    const int p0 = loop_pieces > 0 ? 0 : (int)blockIdx.y;
-    const int p1 = loop_pieces > 0 ? loop_pieces : p0 + 1;
+    // grid.y = ceil(npieces / pgroup): the wave takes pgroup pieces in turn
+    // (fewer waves launched only to fail a piece's root test; wave launch
+    // rate, ~1 per ns over the chip, bounds a launch of mostly empty waves)
+    const int p0 = (int)blockIdx.y * pgroup;
+    const int p1 = min(p0 + pgroup, npieces);
     for (int p = p0; p < p1; ++p) {
         const Piece P = pieces[p];
         const int64_t slot = (int64_t)p * ((n + 63) / 64) + w;

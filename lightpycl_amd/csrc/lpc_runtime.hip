@@ -108,6 +108,7 @@ struct lpc_handle {
     int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
     bool piece_loop = false;                        // k_intersect: waves loop over the pieces
     int64_t loop_min_packets = 8192;                //   ... when the population has this many packets
+    int64_t wave_target = 65536;                    // k_intersect: group pieces per wave above this many waves
     int node_w = 8;                                 // hierarchy width for the next build (4 or 8)
     int built_w = 4;                                // width of the records in d_nodes
     int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
@@ -686,16 +687,25 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             SP.budget = h->spill_budget;
             SP.pair_shift = h->spill_pair_shift;
         }
-        const int loop = (h->piece_loop && (n + 63) / 64 >= h->loop_min_packets) ? (int)pt->npieces : 0;
-        const dim3 grid((unsigned)((n + 255) / 256), loop ? 1u : (unsigned)pt->npieces);
+        // pieces per wave: all of them (LPC_LOOP) or enough that the grid has
+        // about wave_target waves
+        const int64_t bxw = (n + 255) / 256;
+        int pgroup = 1;
+        if (h->piece_loop && (n + 63) / 64 >= h->loop_min_packets) pgroup = pt->npieces;
+        else if (h->wave_target > 0)
+            pgroup = (int)std::max<int64_t>(1, (4 * bxw * pt->npieces) / h->wave_target);
+        pgroup = std::max(1, std::min(pgroup, (int)pt->npieces));
+        const dim3 grid((unsigned)bxw, (unsigned)((pt->npieces + pgroup - 1) / pgroup));
         if (h->built_w == 8)
             hipLaunchKernelGGL(k_intersect<8>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
                                (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
-                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, loop);
+                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,
+                               (int)pt->npieces);
         else
             hipLaunchKernelGGL(k_intersect<4>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
                                (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
-                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, loop);
+                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,
+                               (int)pt->npieces);
         // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and
         // queues what exceeds the budget for level l + 1; the last level finishes
         const int levels = SP.budget > 0 ? std::max(1, std::min(h->spill_levels, 7)) : 0;
@@ -843,6 +853,7 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_pair_shift = (int)std::min<int64_t>(31, std::max<int64_t>(0, env_int("LPC_PAIR_SHIFT", h->spill_pair_shift)));
     h->piece_loop = env_int("LPC_LOOP", h->piece_loop) != 0;
     h->loop_min_packets = env_int("LPC_LOOP_MIN", h->loop_min_packets);
+    h->wave_target = env_int("LPC_WAVE_TARGET", h->wave_target);
     h->node_w = env_int("LPC_NODE_W", h->node_w) == 4 ? 4 : 8;
     h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
     h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
