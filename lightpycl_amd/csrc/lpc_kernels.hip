@@ -493,7 +493,8 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
                                                  const Piece *__restrict__ pieces, float eps, float max_ray_len,
                                                  unsigned long long *__restrict__ skey,
                                                  int32_t *__restrict__ scnt,
-                                                 unsigned long long *__restrict__ stats, int ppw)
+                                                 unsigned long long *__restrict__ stats, int ppw,
+                                                 float dmax)
 {
     const int lane = threadIdx.x & 63;
     const int64_t npk = (n + 127) / 128;
@@ -505,6 +506,7 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
     SliverRec S;
     if (j < P.s_hi) S = srec[j];
     else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
+    if (!(S.dmin <= dmax)) S.a = NAN;             // no ray of the launch can pass its DEN test
     const int64_t o = (int64_t)P.slot * n;
     uint32_t n_tests = 0, n_exact = 0;
     for (int64_t w = w0; w < w1; ++w) {
@@ -567,7 +569,8 @@ __global__ __launch_bounds__(256) void k_slivers1(RaysIn R, const float *__restr
                                                   const Piece *__restrict__ pieces, float eps, float max_ray_len,
                                                   unsigned long long *__restrict__ skey,
                                                   int32_t *__restrict__ scnt,
-                                                  unsigned long long *__restrict__ stats, int ppw)
+                                                  unsigned long long *__restrict__ stats, int ppw,
+                                                 float dmax)
 {
     const int lane = threadIdx.x & 63;
     const int64_t npk = (n + 63) / 64;
@@ -579,6 +582,7 @@ __global__ __launch_bounds__(256) void k_slivers1(RaysIn R, const float *__restr
     SliverRec S;
     if (j < P.s_hi) S = srec[j];
     else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
+    if (!(S.dmin <= dmax)) S.a = NAN;             // no ray of the launch can pass its DEN test
     const int64_t o = (int64_t)P.slot * n;
     uint32_t n_tests = 0, n_exact = 0;
     for (int64_t w = w0; w < w1; ++w) {

@@ -353,6 +353,7 @@ struct SliverRec {
     float v0x, v0y, v0z, e2x, e2y, e2z, a, b;
     int32_t idx;
     float e1x, e1y, e1z;    // with v0, e2: the exact record (Moller-Trumbore input)
+    float dmin;             // |DEN| >= 1e-6 needs |D| >= dmin (sliver_dmin)
 };
 
 // Bound of one wave's packet of rays (k_packet): every origin lies within ro of
@@ -563,6 +564,35 @@ static inline FiltRec filter_record(
 // The kernel tests x^2 <= (|D|(a + b tmax))^2 with x = D.(E2 x T) in float and
 // tmax = max|T_i| (|T| <= sqrt(3) tmax); a, b carry a factor 2 of slack for the
 // float evaluation of the test itself.
+// Smallest |D| for which Moller-Trumbore's DEN = E1 . (D x E2) (float, .cl:75-79)
+// can reach the 1e-6 threshold.  Per component P_i = (D x E2)_i is a difference
+// of two products: |P^_i - P_i| <= 2.01 u s_i with s_i = |d_j e2_k| + |d_k e2_j|
+// (with or without FMA); the 3-term float dot adds <= 3.01 u sum |e1_i| |P^_i|.
+// With E1 . (D x E2) = D . (E2 x E1):
+//     |DEN^| <= |D| (|E1 x E2| + 5.03 u G),  G = sum_i |e1_i| (|e2_j| + |e2_k|),
+// so |D| < 0.999e-6 / (|E1 x E2| + 5.1 u G) never passes the DEN test.  revolve_curve's
+// pole triangles are collinear (E1 x E2 = 0 exactly): their dmin is ~1e-6 / (5 u |E1||E2|),
+// far above unit directions unless |E1||E2| is large.  Rounded down to float.
+static inline float sliver_dmin(const float *V0, const float *V1, const float *V2)
+{
+    const double u = 1.0 / 16777216.0;
+    double e1[3], e2[3];
+    for (int k = 0; k < 3; ++k) { e1[k] = (double)(V1[k] - V0[k]); e2[k] = (double)(V2[k] - V0[k]); }
+    const double c[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                         e2[0] * e1[1] - e2[1] * e1[0]};
+    const double nc = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    const double n2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+    double G = 0.0;
+    for (int i = 0; i < 3; ++i) G += fabs(e1[i]) * (fabs(e2[(i + 1) % 3]) + fabs(e2[(i + 2) % 3]));
+    const double coef = nc * (1.0 + 1e-9) + 1e-15 * n1 * n2 + 5.1 * u * G;
+    if (!(coef > 0.0)) return INFINITY;                     // zero edge: DEN == 0 exactly
+    const double dmin = 0.999e-6 / coef;
+    float f = (float)dmin;
+    if ((double)f > dmin) f = nextafterf(f, 0.0f);
+    return f;
+}
+
 static inline void sliver_params(const float *V0, const float *V1, const float *V2, float *a_out,
                                  float *b_out)
 {

@@ -50,6 +50,7 @@ struct Pop {
 struct PieceTable {
     DBuf pieces, spieces;              // hierarchy pieces (k_intersect), sliver pieces (k_slivers)
     int32_t npieces = 0, nspieces = 0;
+    std::vector<float> sdmin;          // per sliver piece (ascending): min dmin of its slivers
     int32_t gmax = 0;                  // most fan groups under one piece (k_groups item slots)
 };
 
@@ -70,6 +71,8 @@ struct lpc_handle {
     std::vector<int32_t> run_lo, run_hi;
     std::vector<std::vector<int32_t>> run_levels;    // per run: (first node, count) per level, root first
     std::vector<FiltRec> node_self;                  // each node's own test (piece roots)
+    std::vector<float> sliver_dmin_host;             // SliverRec::dmin, host copy
+    double pop_dmax2 = INFINITY, init_dmax2 = INFINITY;   // max |D|^2 of the trace population / emitted rays
     std::vector<int32_t> node_groups;                // fan groups in each node's subtree
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
@@ -97,6 +100,7 @@ struct lpc_handle {
     DBuf d_misc;                                    // LPC_MISC_WORDS per-launch words
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
+    int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
@@ -255,6 +259,7 @@ static int build_records(lpc_handle *h)
     h->node_self.clear();
     h->node_groups.clear();
     h->run_slo.clear(); h->run_shi.clear();
+    h->sliver_dmin_host.clear();
     h->n_slivers = 0;
     const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 0.0f, INFINITY);
     std::vector<FiltRec> grec;                      // fan-group members, LPC_GROUP_SIZE per group
@@ -290,6 +295,14 @@ static int build_records(lpc_handle *h)
             for (int k = 0; k < 3; ++k) (flat ? fcen : cen).push_back(((double)V0[k] + V1[k] + V2[k]) / 3.0);
         }
         h->run_slo.push_back((int32_t)slivers.size());
+        // slivers ordered by dmin, so a 64-sliver piece holds similar ones
+        std::vector<std::pair<float, int32_t>> sld;
+        for (int32_t t32 : sl) sld.push_back({sliver_dmin(vptr(t32, 0), vptr(t32, 1), vptr(t32, 2)), t32});
+        std::stable_sort(sld.begin(), sld.end(),
+                         [](const std::pair<float, int32_t> &x, const std::pair<float, int32_t> &y) {
+                             return x.first < y.first;
+                         });
+        for (size_t q = 0; q < sld.size(); ++q) sl[q] = sld[q].second;
         for (int32_t t32 : sl) {
             const float *V0 = vptr(t32, 0), *V1 = vptr(t32, 1), *V2 = vptr(t32, 2);
             SliverRec S;
@@ -299,6 +312,7 @@ static int build_records(lpc_handle *h)
             sliver_params(V0, V1, V2, &S.a, &S.b);
             S.e1x = V1[0] - V0[0]; S.e1y = V1[1] - V0[1]; S.e1z = V1[2] - V0[2];
             S.idx = t32;
+            S.dmin = sliver_dmin(V0, V1, V2);
             slivers.push_back(S);
         }
         h->run_shi.push_back((int32_t)slivers.size());
@@ -440,9 +454,10 @@ static int build_records(lpc_handle *h)
     if (slivers.empty()) {
         SliverRec ss;
         memset(&ss, 0, sizeof(ss));
-        ss.a = NAN; ss.idx = -1;
+        ss.a = NAN; ss.idx = -1; ss.dmin = INFINITY;
         slivers.push_back(ss);
     }
+    for (const SliverRec &q : slivers) h->sliver_dmin_host.push_back(q.dmin);
     h->Mpad = n_nodes;
     h->built_w = W;
     RETIF(dalloc(h, h->d_nodes, nodes.size()));
@@ -474,6 +489,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     auto it = h->ptabs.find(g);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
     std::vector<Piece> pcs, spc;
+    std::vector<float> sdm;
     int32_t gmax = 0;
     for (size_t r = 0; r < nr; ++r) {
         if (run_slot[r] < 0) continue;
@@ -501,6 +517,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
             p.s_hi = std::min(a + 64, h->run_shi[r]);
             p.slot = run_slot[r];
             spc.push_back(p);
+            sdm.push_back(h->sliver_dmin_host[(size_t)a]);     // the run's slivers ascend in dmin
         }
     }
     if (pcs.size() > 65535 || spc.size() > 65535) return set_err(h, LPC_E_ARG, "too many triangle pieces");
@@ -508,6 +525,15 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     t.npieces = (int32_t)pcs.size();
     t.nspieces = (int32_t)spc.size();
     t.gmax = gmax;
+    {   // sliver pieces in ascending dmin: a launch takes the prefix its rays can reach
+        std::vector<size_t> o(spc.size());
+        for (size_t i = 0; i < o.size(); ++i) o[i] = i;
+        std::stable_sort(o.begin(), o.end(), [&](size_t x, size_t y) { return sdm[x] < sdm[y]; });
+        std::vector<Piece> s2;
+        t.sdmin.clear();
+        for (size_t i : o) { s2.push_back(spc[i]); t.sdmin.push_back(sdm[i]); }
+        spc.swap(s2);
+    }
     if (!pcs.empty()) {
         RETIF(dalloc(h, t.pieces, pcs.size() * sizeof(Piece)));
         HIPCHK(h, hipMemcpy(t.pieces.p, pcs.data(), pcs.size() * sizeof(Piece), hipMemcpyHostToDevice));
@@ -615,7 +641,8 @@ static void prof_resolve(lpc_handle *h)
 // split: rows [0, split) of `in` are a population's reflected block (key class
 // bit, k_raykey); INT64_MAX when the rows are not a trace population.
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
-                         float *st_user, int32_t *si_user, int32_t *sc_user, int64_t split = INT64_MAX)
+                         float *st_user, int32_t *si_user, int32_t *sc_user, int64_t split = INT64_MAX,
+                         double dmax2 = INFINITY)
 {
     RETIF(ensure_ws(h, n));
     PieceTable *pt;
@@ -728,32 +755,38 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         if (gmax > 0) {
             hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
                                (PacketRec *)h->w_pk64.p);
-            hipLaunchKernelGGL(k_groups, grid, dim3(256), 0, h->stream, in, rs, n, perm, (const FiltRec *)h->d_grec.p,
+            hipLaunchKernelGGL(k_groups, dim3((unsigned)bxw, (unsigned)pt->npieces), dim3(256), 0, h->stream, in, rs, n, perm, (const FiltRec *)h->d_grec.p,
                                (const ExactRec *)h->d_gxrec.p, (const PacketRec *)h->w_pk64.p,
                                (const Piece *)pt->pieces.p, (const GItem *)gitems, (const int32_t *)gcount, gmax,
                                eps, max_ray_len, skey, scnt);
         }
         HIPCHK(h, hipGetLastError());
     }
-    if (pt->nspieces > 0) {
+    // sliver pieces the launch's rays can reach: dmin <= max |D| (sliver_dmin)
+    if (!(dmax2 >= 0.0)) dmax2 = INFINITY;          // NaN bound (a NaN direction): no culling
+    const float dmax = (float)std::min<double>(sqrt(dmax2 * (1.0 + 1e-5)), (double)INFINITY);
+    int32_t nsp = 0;
+    while (nsp < pt->nspieces && (h->sliver_cull == 0 || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
+    const float dmax_k = h->sliver_cull ? dmax : INFINITY;
+    if (nsp > 0) {
         // packets per wave: enough (packet, piece) waves to fill the GPU, no more
         const int rpl = h->sliver_rays == 64 ? 1 : 2;
         const int64_t npkx = (n + 64 * rpl - 1) / (64 * rpl);
         const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
-                                              : std::max<int64_t>(1, npkx * pt->nspieces / h->sliver_waves);
-        const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)pt->nspieces);
+                                              : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
+        const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
         if (rpl == 1) {
             hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
                                (PacketRec *)h->w_pk64.p);
             hipLaunchKernelGGL(k_slivers1, sg, dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk64.p,
                                (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw);
+                               scnt, stats, (int)ppw, dmax_k);
         } else {
             hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
                                (PacketRec *)h->w_pk.p);
             hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
                                (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw);
+                               scnt, stats, (int)ppw, dmax_k);
         }
         HIPCHK(h, hipGetLastError());
     }
@@ -845,6 +878,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
+    h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
@@ -1045,7 +1079,8 @@ int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float 
         return set_err(h, LPC_E_ARG, "bounce_host: missing buffer");
     if (n == 0) return 0;
     HIPCHK(h, hipSetDevice(h->device));
-    RETIF(check_dcap(h, host_dmax2(n, dir4)));
+    const double bdmax2 = host_dmax2(n, dir4);
+    RETIF(check_dcap(h, bdmax2));
     const int64_t C = std::min(n, chunk_rays(h));
     RETIF(ensure_ws(h, C));
     Pop P;
@@ -1058,7 +1093,7 @@ int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float 
         rc = upload_rays(h, P, nc, origin4 + 4 * base, dir4 + 4 * base, pow + base, prev_mid + base);
         if (rc) break;
         if (hipMemcpy(dmeas.p, meas + base, (size_t)nc * 4, hipMemcpyHostToDevice) != hipSuccess) { rc = set_err(h, LPC_E_HIP, "meas upload"); break; }
-        rc = run_intersect(h, P.in(), nc, max_ray_len, nullptr, nullptr, nullptr);
+        rc = run_intersect(h, P.in(), nc, max_ray_len, nullptr, nullptr, nullptr, INT64_MAX, bdmax2);
         if (!rc) rc = run_shade(h, P.in(), (const int32_t *)dmeas.p, nc, max_ray_len, ior_env, true);
         if (rc) break;
         ShadeOutPtrs o = shade_ptrs(h, true);
@@ -1217,7 +1252,8 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
     if (n < 0 || (n > 0 && (!origin4 || !dir4 || !pow))) return set_err(h, LPC_E_ARG, "set_rays: missing buffer");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    RETIF(check_dcap(h, host_dmax2(n, dir4)));
+    h->init_dmax2 = host_dmax2(n, dir4);
+    RETIF(check_dcap(h, h->init_dmax2));
     RETIF(pop_reserve(h, h->I, std::max<int64_t>(n, 1)));
     if (n > 0) RETIF(upload_rays(h, h->I, n, origin4, dir4, pow, nullptr));
     h->n_init = n;
@@ -1238,6 +1274,7 @@ int lpc_trace_reset(lpc_handle *h)
                            h->stream, h->A.out(), h->I.in(0), h->n_init);
     h->n_cur = h->n_init;
     h->split = INT64_MAX;                       // emitted rays: one class
+    h->pop_dmax2 = h->init_dmax2;
     h->m_total = 0;                             // measured record emptied in-stream
     hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p, 0ull);
     HIPCHK(h, hipGetLastError());
@@ -1311,7 +1348,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         const int64_t nc = std::min(C, N - base);
         const RaysIn in = h->A.in(base);
         const int64_t split = h->split == INT64_MAX ? INT64_MAX : std::max<int64_t>(0, h->split - base);
-        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split));
+        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2));
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
         RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
@@ -1365,6 +1402,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     float dm2;
     memcpy(&dm2, &acc.dmax2_bits, 4);
     RETIF(check_dcap(h, (double)dm2));
+    h->pop_dmax2 = (double)dm2;                 // the next population's max |D|^2 (float, see run_intersect)
     if (st) *st = S;
     return 0;
 }

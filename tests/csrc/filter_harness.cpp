@@ -277,3 +277,21 @@ extern "C" void filt_records(int m, const float *V, double dcap, double S, float
         out[5 * j] = r.cx; out[5 * j + 1] = r.cy; out[5 * j + 2] = r.cz; out[5 * j + 3] = r.negB; out[5 * j + 4] = r.negA;
     }
 }
+
+// sliver_dmin (SliverRec::dmin) and Moller-Trumbore's DEN (.cl:75-76) as float,
+// plain and with FMA contraction, for rays D against triangles V.
+extern "C" void sliver_den(int n, const float *D, const float *V, float *dmin_out, float *den_plain,
+                           float *den_fma)
+{
+    for (int i = 0; i < n; ++i) {
+        const float *d = D + 3 * i, *v = V + 9 * i;
+        dmin_out[i] = sliver_dmin(v, v + 3, v + 6);
+        const float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+        const float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        const float px = d[1] * e2[2] - d[2] * e2[1], py = d[2] * e2[0] - d[0] * e2[2], pz = d[0] * e2[1] - d[1] * e2[0];
+        den_plain[i] = px * e1[0] + py * e1[1] + pz * e1[2];
+        const float fx = fmaf(d[1], e2[2], -(d[2] * e2[1])), fy = fmaf(d[2], e2[0], -(d[0] * e2[2])),
+                    fz = fmaf(d[0], e2[1], -(d[1] * e2[0]));
+        den_fma[i] = fmaf(fz, e1[2], fmaf(fy, e1[1], fx * e1[0]));
+    }
+}

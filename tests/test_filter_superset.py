@@ -331,3 +331,36 @@ def test_packet_tests_are_sound(packet_harness, sliver_harness, name, ball, dist
         O, D = _packets(rng, Vs, 60, ball, dist, spread, line=True)
         r = packet_harness(O, D, Vs, 2)
         assert r["violations"] == 0, r
+
+
+@pytest.mark.parametrize("name", ["synthetic", "eye", "lens", "parabolic"])
+def test_sliver_dmin_bounds_den(harness, sliver_harness, name):
+    """SliverRec::dmin: below it |D| is too short for Moller-Trumbore's float DEN
+    (plain or FMA-contracted) to reach the 1e-6 threshold, so a launch whose rays
+    are all shorter skips the sliver (k_slivers).  Random directions scaled to just
+    under dmin never reach it; the bound is within a small factor of the real noise."""
+    V = _scene_slivers(sliver_harness, name)
+    if V.shape[0] == 0:
+        pytest.skip("scene has no slivers")
+    L = ctypes.CDLL(SO)
+    P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    L.sliver_den.argtypes = [ctypes.c_int, P, P, P, P, P]
+    L.sliver_den.restype = None
+    rng = np.random.default_rng(17)
+    n = 300_000
+    j = rng.integers(0, V.shape[0], n)
+    Vj = np.ascontiguousarray(V[j], np.float32)
+    D = rng.normal(size=(n, 3))
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    dmin = np.zeros(n, np.float32)
+    a = np.zeros(n, np.float32)
+    b = np.zeros(n, np.float32)
+    L.sliver_den(n, np.ascontiguousarray(D, np.float32), Vj, dmin, a, b)   # dmin per row
+    fin = np.isfinite(dmin)
+    assert fin.any()
+    Ds = np.ascontiguousarray(D * (np.where(fin, dmin, 1.0) * 0.9999)[:, None], np.float32)
+    L.sliver_den(n, Ds, Vj, dmin, a, b)
+    eps6 = np.float32(0.000001)
+    assert not (fin & ((np.abs(a) >= eps6) | (np.abs(b) >= eps6))).any()
+    # the noise at dmin is a real fraction of the threshold (the bound is not vacuous)
+    assert np.max(np.abs(np.concatenate([a[fin], b[fin]]))) > 1e-3 * eps6
