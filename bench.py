@@ -153,7 +153,8 @@ def main():
 
     M = eng.tri_count
     launches = max(prof["intersect_launches"], 1)
-    avg_ms = prof["intersect_ms"] / launches
+    avg_ms = prof["kernel_ms"] / launches               # k_intersect launches alone
+    stage_ms = prof["intersect_ms"] / launches          # + k_spill levels, k_packet, k_slivers
     rays_per_launch = bounces / launches                 # rank-0 launches
     alg_bytes = rays_per_launch * RAY_BYTES + M * TRI_BYTES
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
@@ -180,7 +181,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_intersect", "avg_launch_ms": avg_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes, "stage_avg_ms": stage_ms,
+                     "note": "achieved = algorithmic bytes per launch / k_intersect's own average "
+                             "launch time (HIP events); traffic = 2*FETCH_SIZE+WRITE_SIZE per "
+                             "k_intersect launch (profiles/pmc_intersect.json)"},
         "roofline_valu": {"bound": "valu", "kernel": "k_intersect",
                           "achieved": mt_tflops, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": mt_tflops / FP32_PEAK_TFLOPS,

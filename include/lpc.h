@@ -186,6 +186,8 @@ typedef struct {
     int64_t tail_nodes;      /* their node visits                               */
     int64_t tail_spread_urad;/* their summed direction spread (micro-radians)   */
     int64_t tail_exact;      /* their exact tests                               */
+    double kernel_ms;        /* k_intersect launches alone (HIP events around each
+                                launch; intersect_ms adds k_spill, k_packet, k_slivers) */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * k_intersect traversal counters (2, diagnostic: adds atomics), timing plus

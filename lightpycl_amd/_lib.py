@@ -35,7 +35,8 @@ class Prof(ctypes.Structure):
                 ("wave_hist", ctypes.c_int64 * 24), ("heavy_piece", ctypes.c_int64),
                 ("heavy_piece_ticks", ctypes.c_int64), ("piece_ticks", ctypes.c_int64),
                 ("tail_waves", ctypes.c_int64), ("tail_nodes", ctypes.c_int64),
-                ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64)]
+                ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64),
+                ("kernel_ms", ctypes.c_double)]
 
 
 _P = ctypes.c_void_p

@@ -135,9 +135,9 @@ struct lpc_handle {
     int64_t wrec_count = 0;
     // profiling
     bool prof = false, prof_stats = false, prof_waves = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
     std::vector<hipEvent_t> ev_pool;
-    double prof_isect_ms = 0.0, prof_rest_ms = 0.0;
+    double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
     int64_t prof_launches = 0, prof_pairs = 0;
 };
 
@@ -627,6 +627,13 @@ static void prof_resolve(lpc_handle *h)
         h->ev_pool.push_back(pr.second);
     }
     h->ev_isect.clear();
+    for (auto &pr : h->ev_kern) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_kern_ms += ms;
+        h->ev_pool.push_back(pr.first);
+        h->ev_pool.push_back(pr.second);
+    }
+    h->ev_kern.clear();
     for (auto &pr : h->ev_rest) {
         float ms = 0.0f;
         if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_rest_ms += ms;
@@ -723,6 +730,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             pgroup = (int)std::max<int64_t>(1, (4 * bxw * pt->npieces) / h->wave_target);
         pgroup = std::max(1, std::min(pgroup, (int)pt->npieces));
         const dim3 grid((unsigned)bxw, (unsigned)((pt->npieces + pgroup - 1) / pgroup));
+        hipEvent_t k0 = nullptr, k1 = nullptr;
+        if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
         if (h->built_w == 8)
             hipLaunchKernelGGL(k_intersect<8>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
                                (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
@@ -733,6 +742,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
                                (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,
                                (int)pt->npieces);
+        if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
         // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and
         // queues what exceeds the budget for level l + 1; the last level finishes
         const int levels = SP.budget > 0 ? std::max(1, std::min(h->spill_levels, 7)) : 0;
@@ -1538,6 +1548,7 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     (void)hipStreamSynchronize(h->stream);
     prof_resolve(h);
     out->intersect_ms = h->prof_isect_ms;
+    out->kernel_ms = h->prof_kern_ms;
     out->shade_ms = h->prof_rest_ms;
     out->intersect_launches = h->prof_launches;
     out->pairs = h->prof_pairs;
@@ -1557,7 +1568,7 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
         if (v > out->heavy_piece_ticks) { out->heavy_piece_ticks = v; out->heavy_piece = p; }
     }
     if (reset) {
-        h->prof_isect_ms = h->prof_rest_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
+        h->prof_isect_ms = h->prof_rest_ms = h->prof_kern_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
         if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
     }
     return 0;

@@ -245,4 +245,4 @@ class Engine:
                     group_tests=p.group_tests, wave_traversals=p.wave_traversals, exact_tests=p.exact_tests,
                     wave_hist=list(p.wave_hist), heavy_piece=p.heavy_piece, heavy_piece_ticks=p.heavy_piece_ticks,
                     piece_ticks=p.piece_ticks, tail_waves=p.tail_waves, tail_nodes=p.tail_nodes,
-                    tail_spread_urad=p.tail_spread_urad, tail_exact=p.tail_exact)
+                    tail_spread_urad=p.tail_spread_urad, tail_exact=p.tail_exact, kernel_ms=p.kernel_ms)
