@@ -395,6 +395,46 @@ __global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__rest
     }
 }
 
+// k_lane: one ray per lane (incoherent populations: a 64-ray packet's union of
+// visited nodes is many times one ray's), grid = (ceil(n/256), pieces).  The lane
+// walks its piece's threaded entry list (LaneEntry, depth-first with skip links,
+// no stack): a node entry that its ray passes is entered (next entry), else
+// skipped; a triangle entry that passes gets the exact test at once.  Same tests,
+// same exact-test superset as k_intersect, same order-independent flush.
+__global__ __launch_bounds__(256) void k_lane(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                              const int32_t *__restrict__ perm, const LaneEntry *__restrict__ E,
+                                              const ExactRec *__restrict__ xrec, const Piece *__restrict__ pieces,
+                                              float eps, float max_ray_len, unsigned long long *__restrict__ skey,
+                                              int32_t *__restrict__ scnt)
+{
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const Piece P = pieces[blockIdx.y];
+    f3 O, D;
+    load_ray(R, rs, n, s, O, D);
+    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
+    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+    float tmin = max_ray_len;
+    int32_t imin = -1, cnt = 0;
+    int32_t i = P.s_lo;
+    const int32_t end = P.s_hi;
+    while (i < end) {
+        const LaneEntry e = E[i];
+        const bool pass = filter_test(e.cx, e.cy, e.cz, e.negB, e.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f;
+        if (e.tri >= 0) {
+            if (pass) {
+                const ExactRec x = xrec[e.tri];
+                mt_accumulate(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z),
+                              e.tri, eps, tmin, imin, cnt);
+            }
+            ++i;
+        } else {
+            i = pass ? i + 1 : e.skip;
+        }
+    }
+    slot_flush(skey, scnt, (int64_t)P.slot * n, perm ? perm[s] : s, tmin, imin, cnt);
+}
+
 // k_spill: the subtrees handed over by the previous level (queue `in`), one item
 // per wave, grid-stride over the queue (its length is read on the device).  An
 // item that again exceeds the budget hands its remaining subtrees to the next

@@ -334,6 +334,15 @@ struct NodeW {
 typedef NodeW<4> Node4;
 typedef NodeW<8> Node8;
 
+// The same hierarchy as a threaded depth-first entry list (k_lane): a node's
+// entry is followed by its children's entries (and their subtrees); skip = the
+// entry after the subtree.  tri >= 0: a triangle (its filter record), else an
+// internal node (its node_record test).  32 B.
+struct LaneEntry {
+    float cx, cy, cz, negB, negA;
+    int32_t skip, tri, pad;
+};
+
 // Leaf children are triangles or "fan groups".  A fan group holds up to
 // LPC_GROUP_SIZE thin triangles whose filter spheres pile up around a common
 // point (revolve_curve's poles): reached through the hierarchy, a wave tests all

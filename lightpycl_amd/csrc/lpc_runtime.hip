@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -72,6 +73,9 @@ struct lpc_handle {
     std::vector<std::vector<int32_t>> run_levels;    // per run: (first node, count) per level, root first
     std::vector<FiltRec> node_self;                  // each node's own test (piece roots)
     std::vector<float> sliver_dmin_host;             // SliverRec::dmin, host copy
+    std::vector<int32_t> node_entry, node_end;       // a node's LaneEntry and the entry after its subtree
+    DBuf d_lane;                                     // LaneEntry list (k_lane)
+    bool lane_ok = false;                            // entry list built (no fan groups)
     double pop_dmax2 = INFINITY, init_dmax2 = INFINITY;   // max |D|^2 of the trace population / emitted rays
     std::vector<int32_t> node_groups;                // fan groups in each node's subtree
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
@@ -101,6 +105,8 @@ struct lpc_handle {
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
     int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
+    int64_t lane_max = 0;                           // populations up to this many rays: k_lane
+    int64_t lane_g = 1;                             // k_lane pieces: nodes per run (1: the run roots)
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
@@ -109,6 +115,8 @@ struct lpc_handle {
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
     int spill_levels = 4;                           // k_spill launches (hand-over depth)
+    int spill_shrink = 1;                           // level l grid = spill_blocks >> (shrink * l) ...
+    int64_t spill_min_blocks = 256;                 // ... but at least this
     int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
     bool piece_loop = false;                        // k_intersect: waves loop over the pieces
     int64_t loop_min_packets = 8192;                //   ... when the population has this many packets
@@ -254,6 +262,9 @@ static int build_records(lpc_handle *h)
     const size_t node_bytes = W == 8 ? sizeof(Node8) : sizeof(Node4);
     std::vector<uint8_t> nodes;                     // NodeW<W> records
     int32_t n_nodes = 0;
+    std::vector<LaneEntry> lane;                    // threaded entry list (k_lane)
+    bool lane_ok = true;
+    h->node_entry.clear(); h->node_end.clear();
     std::vector<SliverRec> slivers;
     h->run_levels.clear();
     h->node_self.clear();
@@ -443,7 +454,57 @@ static int build_records(lpc_handle *h)
             h->run_levels.back().push_back(it->first);
             h->run_levels.back().push_back(it->second);
         }
+        // threaded entry list of this run (k_lane): root entry, then depth first
+        {
+            const int32_t root = levels.back().first;
+            auto rec_at = [&](int32_t node, int k, LaneEntry &e) -> int32_t {
+                const uint32_t *Nw = (const uint32_t *)(nodes.data() + (size_t)node * node_bytes);
+                float f5[5];
+                for (int q = 0; q < 5; ++q) memcpy(&f5[q], &Nw[(size_t)q * W + k], 4);
+                int32_t ref;
+                memcpy(&ref, &Nw[(size_t)5 * W + k], 4);
+                e.cx = f5[0]; e.cy = f5[1]; e.cz = f5[2]; e.negB = f5[3]; e.negA = f5[4]; e.pad = 0;
+                return ref;
+            };
+            std::function<void(int32_t)> emit = [&](int32_t node) {
+                for (int k = 0; k < W; ++k) {
+                    LaneEntry e;
+                    const int32_t ref = rec_at(node, k, e);
+                    if (!(e.negA < INFINITY)) continue;                 // unused child / never
+                    if (ref >= 0) {
+                        const int32_t at = (int32_t)lane.size();
+                        e.tri = -1; e.skip = 0;
+                        lane.push_back(e);
+                        h->node_entry[(size_t)ref] = at;
+                        emit(ref);
+                        lane[(size_t)at].skip = (int32_t)lane.size();
+                        h->node_end[(size_t)ref] = (int32_t)lane.size();
+                    } else if (ref >= LPC_GROUP_REF) {
+                        e.tri = ~ref; e.skip = (int32_t)lane.size() + 1;
+                        lane.push_back(e);
+                    } else {
+                        lane_ok = false;                                // fan group: no lane path
+                    }
+                }
+            };
+            h->node_entry.resize((size_t)n_nodes, -1);
+            h->node_end.resize((size_t)n_nodes, -1);
+            const FiltRec &rs0 = h->node_self[(size_t)root];
+            LaneEntry e0;
+            e0.cx = rs0.cx; e0.cy = rs0.cy; e0.cz = rs0.cz; e0.negB = rs0.negB; e0.negA = rs0.negA;
+            e0.tri = -1; e0.skip = 0; e0.pad = 0;
+            const int32_t at = (int32_t)lane.size();
+            lane.push_back(e0);
+            h->node_entry[(size_t)root] = at;
+            emit(root);
+            lane[(size_t)at].skip = (int32_t)lane.size();
+            h->node_end[(size_t)root] = (int32_t)lane.size();
+        }
     }
+    h->lane_ok = lane_ok && !lane.empty();
+    if (lane.empty()) { LaneEntry z; memset(&z, 0, sizeof(z)); z.negA = INFINITY; z.tri = -1; lane.push_back(z); }
+    RETIF(dalloc(h, h->d_lane, lane.size() * sizeof(LaneEntry)));
+    HIPCHK(h, hipMemcpy(h->d_lane.p, lane.data(), lane.size() * sizeof(LaneEntry), hipMemcpyHostToDevice));
     if (grec.empty()) { grec.assign(LPC_GROUP_SIZE, never); gxrec.assign(LPC_GROUP_SIZE, ExactRec{}); }
     RETIF(dalloc(h, h->d_grec, grec.size() * sizeof(FiltRec)));
     RETIF(dalloc(h, h->d_gxrec, gxrec.size() * sizeof(ExactRec)));
@@ -473,7 +534,7 @@ static int build_records(lpc_handle *h)
 // results are): each run's root, or all nodes of the shallowest level with >= g
 // nodes, g chosen so that blocks_x * pieces fills the GPU.  Sliver pieces = the
 // runs' slivers in blocks of <= 64 (one lane each).
-static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
+static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_force = 0)
 {
     const int64_t bx = std::max<int64_t>(1, (n + 255) / 256);
     const size_t nr = h->run_levels.size();
@@ -486,6 +547,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
     const int64_t target_blocks = h->target_blocks;
     int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (target_blocks + bx * live_runs - 1) /
                                                                         (bx * live_runs)));
+    if (g_force > 0) g = g_force;
     auto it = h->ptabs.find(g);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
     std::vector<Piece> pcs, spc;
@@ -503,7 +565,8 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out)
                 p.root = L[2 * lv] + i;
                 const FiltRec &t = h->node_self[(size_t)p.root];
                 p.cx = t.cx; p.cy = t.cy; p.cz = t.cz; p.negB = t.negB; p.negA = t.negA;
-                p.s_lo = p.s_hi = 0;
+                p.s_lo = h->node_entry.empty() ? 0 : h->node_entry[(size_t)p.root];   // k_lane entry range
+                p.s_hi = h->node_end.empty() ? 0 : h->node_end[(size_t)p.root];
                 p.slot = run_slot[r];
                 pcs.push_back(p);
                 gmax = std::max(gmax, h->node_groups[(size_t)p.root]);
@@ -693,7 +756,17 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
-    if (pt->npieces > 0) {
+    const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
+    if (pt->npieces > 0 && lane_path) {
+        // incoherent (small) populations: one ray per lane, threaded traversal
+        PieceTable *pl;
+        RETIF(piece_table(h, n, &pl, (int32_t)h->lane_g));
+        hipLaunchKernelGGL(k_lane, dim3((unsigned)((n + 255) / 256), (unsigned)pl->npieces), dim3(256), 0, h->stream,
+                           in, rs, n, perm, (const LaneEntry *)h->d_lane.p, (const ExactRec *)h->d_xrec.p,
+                           (const Piece *)pl->pieces.p, eps, max_ray_len, skey, scnt);
+        HIPCHK(h, hipGetLastError());
+    }
+    if (pt->npieces > 0 && !lane_path) {
         uint32_t *wrec = nullptr;
         if (h->prof_waves) {
             h->wrec_count = (int64_t)pt->npieces * ((n + 63) / 64);
@@ -753,12 +826,14 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             O.items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
             O.ctr = misc + LPC_MISC_SPILL + l + 1;
             O.budget = l + 1 < levels ? SP.budget : 0;
+            // later levels hold fewer items (and often none): smaller grids
+            const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
             if (h->built_w == 8)
-                hipLaunchKernelGGL(k_spill<8>, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n,
+                hipLaunchKernelGGL(k_spill<8>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
                                    perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
                                    max_ray_len, skey, scnt, stats, I, O);
             else
-                hipLaunchKernelGGL(k_spill<4>, dim3((unsigned)h->spill_blocks), dim3(256), 0, h->stream, in, rs, n,
+                hipLaunchKernelGGL(k_spill<4>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
                                    perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
                                    max_ray_len, skey, scnt, stats, I, O);
         }
@@ -889,11 +964,15 @@ int lpc_open(int device, lpc_handle **out)
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
+    h->lane_max = env_int("LPC_LANE_MAX", h->lane_max);
+    h->lane_g = std::max<int64_t>(1, env_int("LPC_LANE_G", h->lane_g));
     if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
     h->spill_levels = (int)env_int("LPC_SPILL_LEVELS", h->spill_levels);
+    h->spill_shrink = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_int("LPC_SPILL_SHRINK", h->spill_shrink)));
+    h->spill_min_blocks = std::max<int64_t>(1, env_int("LPC_SPILL_MIN_BLOCKS", h->spill_min_blocks));
     h->spill_pair_shift = (int)std::min<int64_t>(31, std::max<int64_t>(0, env_int("LPC_PAIR_SHIFT", h->spill_pair_shift)));
     h->piece_loop = env_int("LPC_LOOP", h->piece_loop) != 0;
     h->loop_min_packets = env_int("LPC_LOOP_MIN", h->loop_min_packets);
@@ -920,7 +999,7 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos, &h->d_lane};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
