@@ -364,8 +364,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
 
 // k_intersect: grid = (ceil(n/256), pieces), block = 4 waves, one (packet,
 // piece) per wave.
-template <int W>
-__global__ __launch_bounds__(256) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
+template <int W, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                    const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
                                                    const ExactRec *__restrict__ xrec,

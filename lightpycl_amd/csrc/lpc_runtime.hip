@@ -107,6 +107,7 @@ struct lpc_handle {
     int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
     int64_t lane_max = 0;                           // populations up to this many rays: k_lane
     int64_t lane_g = 1;                             // k_lane pieces: nodes per run (1: the run roots)
+    int isect_minb = 6;                             // k_intersect launch bounds: min blocks per CU (1 or 6)
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
@@ -805,16 +806,19 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         const dim3 grid((unsigned)bxw, (unsigned)((pt->npieces + pgroup - 1) / pgroup));
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
-        if (h->built_w == 8)
-            hipLaunchKernelGGL(k_intersect<8>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
-                               (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
-                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,
-                               (int)pt->npieces);
-        else
-            hipLaunchKernelGGL(k_intersect<4>, grid, dim3(256), 0, h->stream, in, rs, n, perm,
-                               (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,
-                               (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,
-                               (int)pt->npieces);
+#define LPC_LAUNCH_ISECT(WW, MB)                                                                               \
+    hipLaunchKernelGGL((k_intersect<WW, MB>), grid, dim3(256), 0, h->stream, in, rs, n, perm,                       \
+                       (const NodeW<WW> *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,        \
+                       (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,         \
+                       (int)pt->npieces)
+        if (h->built_w == 8) {
+            if (h->isect_minb == 6) LPC_LAUNCH_ISECT(8, 6);
+            else LPC_LAUNCH_ISECT(8, 1);
+        } else {
+            if (h->isect_minb == 6) LPC_LAUNCH_ISECT(4, 6);
+            else LPC_LAUNCH_ISECT(4, 1);
+        }
+#undef LPC_LAUNCH_ISECT
         if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
         // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and
         // queues what exceeds the budget for level l + 1; the last level finishes
@@ -966,6 +970,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->lane_max = env_int("LPC_LANE_MAX", h->lane_max);
     h->lane_g = std::max<int64_t>(1, env_int("LPC_LANE_G", h->lane_g));
+    h->isect_minb = env_int("LPC_ISECT_MINB", h->isect_minb) == 1 ? 1 : 6;
     if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
