@@ -141,9 +141,10 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
  * ray is kept (:389), at most max_iter iterations.  per_iter[max_iter]
  * receives each iteration's stats, *n_iter their number.  Same results as
  * calling lpc_trace_iterate from the host loop, without a host round trip
- * through the caller per iteration. */
+ * through the caller per iteration.  measured_count / mesh_power (may be NULL)
+ * receive lpc_trace_measured's outputs at the end. */
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                  int32_t *n_iter);
+                  int32_t *n_iter, int64_t *measured_count, double *mesh_power);
 /* Current population size. */
 int lpc_trace_population(lpc_handle *h, int64_t *n);
 /* Measured record so far: count and per-mesh measured power (double[mesh_count]). */

@@ -63,7 +63,7 @@ _PROTOS = {
     "lpc_trace_set_rays": [_P, _I64, _P, _P, _P, _F32, _F32],
     "lpc_trace_reset": [_P],
     "lpc_trace_iterate": [_P, _P, _P, _P, _P, _P, _P],
-    "lpc_trace_run": [_P, _I32, _F64, _P, _P],
+    "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P],
     "lpc_trace_population": [_P, _P],
     "lpc_trace_measured": [_P, _P, _P],
     "lpc_trace_fetch_measured": [_P, _P, _P, _P],

@@ -821,6 +821,108 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     vals[i] = (int32_t)i;
 }
 
+// Adaptive 16-bit coherence key (LPC_SORT=2): a 5-D Morton code, coarse to fine,
+// of the origin cell (scene box, 256 cells per axis) and the octahedral direction
+// (256 x 256), 40 bits; the key is its 16 most significant bits that vary over
+// the population (k_keymask), so a point source spends them all on direction and
+// a population spread over a small region on its own scale.  Sorted with a
+// 2-pass radix sort; any order is correct (results are order independent).
+static __device__ __forceinline__ uint64_t ray_morton5(float ox, float oy, float oz, float dx, float dy, float dz,
+                                                       float bx0, float by0, float bz0, float sx, float sy, float sz)
+{
+    const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+    float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
+    if (dz < 0.0f) {
+        const float tx = (1.0f - fabsf(py)) * (px >= 0.0f ? 1.0f : -1.0f);
+        const float ty = (1.0f - fabsf(px)) * (py >= 0.0f ? 1.0f : -1.0f);
+        px = tx; py = ty;
+    }
+    uint32_t c[5];
+    c[0] = (uint32_t)fminf(fmaxf((ox - bx0) * sx, 0.0f), 255.0f);
+    c[1] = (uint32_t)fminf(fmaxf((oy - by0) * sy, 0.0f), 255.0f);
+    c[2] = (uint32_t)fminf(fmaxf((oz - bz0) * sz, 0.0f), 255.0f);
+    c[3] = (uint32_t)fminf(fmaxf((px * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
+    c[4] = (uint32_t)fminf(fmaxf((py * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
+    uint64_t k = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b)
+#pragma unroll
+        for (int d = 0; d < 5; ++d) k = (k << 1) | (uint64_t)((c[d] >> b) & 1u);
+    return k;
+}
+
+// Key pass 1: the ray's 32-byte row (k_gather_aos) and the block's OR / AND of
+// the 40-bit codes (part[2 b], part[2 b + 1]).
+__global__ __launch_bounds__(256) void k_raykey16a(RaysIn R, int64_t n, float bx0, float by0, float bz0, float sx,
+                                                   float sy, float sz, float4 *__restrict__ aos,
+                                                   unsigned long long *__restrict__ part)
+{
+    __shared__ unsigned long long s_or[4], s_and[4];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long vo = 0ull, va = ~0ull;
+    if (i < n) {
+        const float ox = R.ox[i], oy = R.oy[i], oz = R.oz[i], dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
+        aos[2 * i] = make_float4(ox, oy, oz, dx);
+        aos[2 * i + 1] = make_float4(dy, dz, 0.0f, 0.0f);
+        vo = va = ray_morton5(ox, oy, oz, dx, dy, dz, bx0, by0, bz0, sx, sy, sz);
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        vo |= __shfl_xor(vo, o, 64);
+        va &= __shfl_xor(va, o, 64);
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_or[wv] = vo; s_and[wv] = va; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s_or[0] | s_or[1] | s_or[2] | s_or[3];
+        part[2 * blockIdx.x + 1] = s_and[0] & s_and[1] & s_and[2] & s_and[3];
+    }
+}
+
+// Key pass 2 (one block): the bits that vary over the population and the 16 most
+// significant of them (sel[0..15], -1 = unused).
+__global__ __launch_bounds__(1024) void k_keymask(const unsigned long long *__restrict__ part, int64_t nb,
+                                                  int32_t *__restrict__ sel)
+{
+    __shared__ unsigned long long s_or[16], s_and[16];
+    unsigned long long vo = 0ull, va = ~0ull;
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) { vo |= part[2 * b]; va &= part[2 * b + 1]; }
+    for (int o = 32; o >= 1; o >>= 1) {
+        vo |= __shfl_xor(vo, o, 64);
+        va &= __shfl_xor(va, o, 64);
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_or[wv] = vo; s_and[wv] = va; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long o = 0ull, a = ~0ull;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { o |= s_or[w]; a &= s_and[w]; }
+        const unsigned long long vary = o & ~a;
+        int j = 0;
+        for (int b = 39; b >= 0 && j < 16; --b)
+            if ((vary >> b) & 1ull) sel[j++] = b;
+        for (; j < 16; ++j) sel[j] = -1;
+    }
+}
+
+// Key pass 3: the 16-bit key of each ray (its code's selected bits).
+__global__ __launch_bounds__(256) void k_keypack(RaysIn R, int64_t n, float bx0, float by0, float bz0, float sx,
+                                                 float sy, float sz, const int32_t *__restrict__ sel,
+                                                 uint32_t *__restrict__ keys, int32_t *__restrict__ vals)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = ray_morton5(R.ox[i], R.oy[i], R.oz[i], R.dx[i], R.dy[i], R.dz[i], bx0, by0, bz0, sx, sy, sz);
+    uint32_t key = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int b = sel[j];
+        key = (key << 1) | (b >= 0 ? (uint32_t)((k >> b) & 1ull) : 0u);
+    }
+    keys[i] = key;
+    vals[i] = (int32_t)i;
+}
+
 // ---------------------------------------------------------------------------
 // k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
 __global__ __launch_bounds__(256) void k_shade(ShadeArgs A)

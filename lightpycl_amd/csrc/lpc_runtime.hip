@@ -96,6 +96,9 @@ struct lpc_handle {
     DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf w_aos;                                     // rays as 32-byte rows for the coherence gather
+    DBuf w_keypart;                                 // per-block OR/AND of the 40-bit codes + selected bits
+    int sort_mode = 1;                              // 1: 32-bit key (rocPRIM default), 2: adaptive 16-bit
+    int64_t onesweep_min = 500000;                  // 32-bit key: onesweep from this many rays
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -615,6 +618,9 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
 // (189 vs 131 us per 1 M-ray iteration incl. k_raykey/k_gather: 4 digit passes +
 // histogram + lookback-state fills, each latency-bound).
 using RaySortCfg = rocprim::default_config;
+// The 16-bit adaptive key (LPC_SORT=2): two 8-bit onesweep passes at every size.
+using RaySortCfg16 = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
 
 static int64_t chunk_rays(const lpc_handle *h)
 {
@@ -647,7 +653,16 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                                         (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)C, 0,
                                                         32, h->stream));
+        size_t tb16 = 0, tb32 = 0;
+        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(nullptr, tb16, (const uint32_t *)nullptr,
+                                                          (uint32_t *)nullptr, (const int32_t *)nullptr,
+                                                          (int32_t *)nullptr, (size_t)C, 0, 16, h->stream));
+        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(nullptr, tb32, (const uint32_t *)nullptr,
+                                                          (uint32_t *)nullptr, (const int32_t *)nullptr,
+                                                          (int32_t *)nullptr, (size_t)C, 0, 32, h->stream));
+        tb = std::max(tb, std::max(tb16, tb32));
         RETIF(dalloc(h, h->w_sort_tmp, tb));
+        RETIF(dalloc(h, h->w_keypart, (size_t)((C + 255) / 256) * 16 + 64 * 4));
         h->sort_tmp_bytes = tb;
         h->ws_rays = C;
     }
@@ -736,6 +751,27 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         // 4 = 3 + refracted-block bit
         const bool pop_box = h->key_mode == 1 || h->key_mode == 2;
         const bool cls = h->key_mode == 2 || h->key_mode == 4;
+        if (h->sort_mode == 2) {
+            // adaptive 16-bit key: 3 small kernels + a 2-pass radix sort
+            const int64_t nb = (n + 255) / 256;
+            unsigned long long *part = (unsigned long long *)h->w_keypart.p;
+            int32_t *sel = (int32_t *)((char *)h->w_keypart.p + (size_t)nb * 16);
+            const float f8 = 8.0f;     // box_scale is for 32 cells per axis
+            hipLaunchKernelGGL(k_raykey16a, dim3((unsigned)nb), dim3(256), 0, h->stream, in, n, h->box_lo[0],
+                               h->box_lo[1], h->box_lo[2], h->box_scale[0] * f8, h->box_scale[1] * f8,
+                               h->box_scale[2] * f8, (float4 *)h->w_aos.p, part);
+            hipLaunchKernelGGL(k_keymask, dim3(1), dim3(1024), 0, h->stream, (const unsigned long long *)part, nb, sel);
+            hipLaunchKernelGGL(k_keypack, dim3((unsigned)nb), dim3(256), 0, h->stream, in, n, h->box_lo[0],
+                               h->box_lo[1], h->box_lo[2], h->box_scale[0] * f8, h->box_scale[1] * f8,
+                               h->box_scale[2] * f8, (const int32_t *)sel, kin, vin);
+            size_t tb = h->sort_tmp_bytes;
+            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
+                                                              0, 16, h->stream));
+            perm = vout;
+            hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
+                               perm, (float *)h->w_rs.p);
+            rs = (const float *)h->w_rs.p;
+        } else {
         if (pop_box)
             hipLaunchKernelGGL(k_bbox, dim3((unsigned)std::min<int64_t>(grid1(n), 1024)), dim3(256), 0, h->stream,
                                in, n, misc);
@@ -744,8 +780,12 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
                            h->key_mode >= 3 ? 1 : 0, kin, vin, h->gather_aos ? (float4 *)h->w_aos.p : nullptr);
         size_t tb = h->sort_tmp_bytes;
-        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, 0, 32,
-                                                        h->stream));
+        if (n >= h->onesweep_min)       // large populations: onesweep (4 digit passes)
+            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
+                                                              0, 32, h->stream));
+        else
+            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, 0,
+                                                            32, h->stream));
         perm = vout;
         if (h->gather_aos)
             hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
@@ -753,6 +793,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         else
             hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
         rs = (const float *)h->w_rs.p;
+        }
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
@@ -965,6 +1006,8 @@ int lpc_open(int device, lpc_handle **out)
     h->key_mode = (int)env_int("LPC_KEY", h->key_mode);
     h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
+    h->sort_mode = env_int("LPC_SORT", h->sort_mode) == 2 ? 2 : 1;
+    h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
@@ -1004,7 +1047,7 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos, &h->d_lane};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos, &h->d_lane, &h->w_keypart};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1376,7 +1419,7 @@ int lpc_trace_reset(lpc_handle *h)
 }
 
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                  int32_t *n_iter)
+                  int32_t *n_iter, int64_t *measured_count, double *mesh_power)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
@@ -1388,6 +1431,11 @@ int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_i
         *n_iter = i + 1;
         if (S.power_next < power_threshold) break;          // :383
         if (S.n_reflect + S.n_refract == 0) break;          // :389
+    }
+    if (measured_count || mesh_power) {                     // the trace's aggregates, same call
+        int64_t c = 0;
+        RETIF(lpc_trace_measured(h, &c, mesh_power));
+        if (measured_count) *measured_count = c;
     }
     return 0;
 }

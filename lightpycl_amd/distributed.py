@@ -77,9 +77,11 @@ class ShardedTrace:
         bounces = 0
         iters = 0
         counts = []
+        measured = None
         if self.comm is None and hasattr(self.engine, "run_local"):
             # one process: the same loop inside the library (lpc_trace_run)
-            for st in self.engine.run_local(int(iterations), thr):
+            stats, measured = self.engine.run_local(int(iterations), thr)
+            for st in stats:
                 bounces += int(st.n_in)
                 iters += 1
                 counts.append(int(st.n_in))
@@ -94,7 +96,7 @@ class ShardedTrace:
                 break
             if tot[2] == 0:
                 break
-        _, mesh_pow = self.engine.measured()
+        _, mesh_pow = measured if measured is not None else self.engine.measured()
         mesh_pow = self._sum(np.asarray(mesh_pow, dtype=np.float64))
         out = dict(bounces=bounces, iterations=iters, global_counts=counts, mesh_power=mesh_pow)
         if hist is not None:

@@ -164,12 +164,16 @@ class Engine:
 
     def run_local(self, iterations, power_threshold):
         """lpc_trace_run: iterate until the next population's power is below
-        power_threshold or no ray is kept (at most `iterations`); per-iteration stats."""
+        power_threshold or no ray is kept (at most `iterations`).  Returns the
+        per-iteration stats and the measured (count, per-mesh power)."""
         cap = max(int(iterations), 0)
         arr = (_lib.IterStats * max(cap, 1))()
         k = ctypes.c_int32(0)
-        self._c(self.L.lpc_trace_run(self.h, cap, float(power_threshold), arr, ctypes.byref(k)))
-        return [arr[i] for i in range(k.value)]
+        c = ctypes.c_int64(0)
+        mp = np.zeros(max(self.mesh_count, 1), np.float64)
+        self._c(self.L.lpc_trace_run(self.h, cap, float(power_threshold), arr, ctypes.byref(k), ctypes.byref(c),
+                                     ptr(mp)))
+        return [arr[i] for i in range(k.value)], (c.value, mp[: self.mesh_count])
 
     def measured(self):
         """(count, per-mesh measured power float64[K])."""
