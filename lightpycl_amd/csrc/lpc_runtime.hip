@@ -119,6 +119,8 @@ struct lpc_handle {
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
     int spill_levels = 4;                           // k_spill launches (hand-over depth)
+    int spill_levels_small = 1;                     // ... for populations below spill_small_n rays
+    int64_t spill_small_n = 262144;
     int spill_shrink = 1;                           // level l grid = spill_blocks >> (shrink * l) ...
     int64_t spill_min_blocks = 256;                 // ... but at least this
     int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
@@ -863,7 +865,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
         // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and
         // queues what exceeds the budget for level l + 1; the last level finishes
-        const int levels = SP.budget > 0 ? std::max(1, std::min(h->spill_levels, 7)) : 0;
+        const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
+        const int levels = SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
         for (int l = 0; l < levels; ++l) {
             SpillArgs I = SP, O = SP;
             I.items = (SpillItem *)h->w_spill.p + (size_t)(l % 2) * (size_t)h->spill_cap;
@@ -1019,6 +1022,7 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
     h->spill_levels = (int)env_int("LPC_SPILL_LEVELS", h->spill_levels);
+    h->spill_levels_small = (int)env_int("LPC_SPILL_LEVELS_SMALL", h->spill_levels_small);
     h->spill_shrink = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_int("LPC_SPILL_SHRINK", h->spill_shrink)));
     h->spill_min_blocks = std::max<int64_t>(1, env_int("LPC_SPILL_MIN_BLOCKS", h->spill_min_blocks));
     h->spill_pair_shift = (int)std::min<int64_t>(31, std::max<int64_t>(0, env_int("LPC_PAIR_SHIFT", h->spill_pair_shift)));
