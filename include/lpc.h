@@ -192,7 +192,9 @@ typedef struct {
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * k_intersect traversal counters (2, diagnostic: adds atomics), timing plus
- * per-wave records of the grid traversal (3, diagnostic), or disable (0). */
+ * per-wave records of the grid traversal (3, diagnostic), only the k_intersect
+ * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs), or
+ * disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
 /* Level 3: the last k_intersect launch's per-(piece, packet) records, 4 uint32

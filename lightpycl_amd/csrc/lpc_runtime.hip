@@ -148,7 +148,7 @@ struct lpc_handle {
     DBuf d_wrec;                                    // per-wave records of the last k_intersect (level 3)
     int64_t wrec_count = 0;
     // profiling
-    bool prof = false, prof_stats = false, prof_waves = false;
+    bool prof = false, prof_stats = false, prof_waves = false, prof_light = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
@@ -798,7 +798,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         }
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+    if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
     const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
     if (pt->npieces > 0 && lane_path) {
@@ -924,8 +924,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         HIPCHK(h, hipGetLastError());
     }
     if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
-        (void)hipEventRecord(e1, h->stream);
-        h->ev_isect.push_back({e0, e1});
+        if (!h->prof_light) {
+            (void)hipEventRecord(e1, h->stream);
+            h->ev_isect.push_back({e0, e1});
+        }
         h->prof_launches += 1;
         h->prof_pairs += n * (int64_t)h->M;
     }
@@ -1496,7 +1498,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         const int64_t split = h->split == INT64_MAX ? INT64_MAX : std::max<int64_t>(0, h->split - base);
         RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2));
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (h->prof) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+        if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
         RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
         ShadeOutPtrs o = shade_ptrs(h, false);
         if (out_origin4 || out_dest4 || out_pow || out_meas) {
@@ -1523,7 +1525,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, h->stream, A);
         hipLaunchKernelGGL(k_scatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         HIPCHK(h, hipGetLastError());
-        if (h->prof) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
+        if (h->prof && !h->prof_light) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
     }
     // refracted block after the reflected one (k_append reads the counts on the
     // device), then the counters to the pinned copy: one host sync per iteration
@@ -1671,6 +1673,7 @@ int lpc_prof_enable(lpc_handle *h, int on)
     h->prof = on != 0;
     h->prof_stats = on == 2;
     h->prof_waves = on == 3;
+    h->prof_light = on == 4;                        // k_intersect events only (bench timed region)
     if (h->prof_stats && !h->d_stats.p) {
         RETIF(dalloc(h, h->d_stats, LPC_STATS_WORDS * 8));
         HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));

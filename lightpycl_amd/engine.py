@@ -227,8 +227,8 @@ class Engine:
         return (H, xe, ye) if not want_xy else (H, xe, ye, x, y, pc)
 
     # -- profiling -------------------------------------------------------------
-    def prof_enable(self, on=True, counters=False, waves=False):
-        level = (3 if waves else 2 if counters else 1) if on else 0
+    def prof_enable(self, on=True, counters=False, waves=False, light=False):
+        level = (4 if light else 3 if waves else 2 if counters else 1) if on else 0
         self._c(self.L.lpc_prof_enable(self.h, level))
 
     def prof_waves(self):
