@@ -115,6 +115,8 @@ struct CompactArgs {
     double *blk_pow;                  // [nb]
     DevAcc *acc;
     RaysOut nR, nT;                   // next population: reflected block, refracted staging
+    int direct_t;                     // single chunk: refracted children go straight after the
+                                      // reflected block (offset acc->nR), no staging / k_append
     float *mx, *my, *mz, *mp;         // measured record
     int32_t *mm;
 };

@@ -1085,6 +1085,7 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
     const int64_t tile = (int64_t)blockIdx.x * 1024;
     const int64_t nb = A.nb;
     int64_t base[3] = {A.blk_off[blockIdx.x], A.blk_off[nb + blockIdx.x], A.blk_off[2 * nb + blockIdx.x]};
+    if (A.direct_t) base[1] += (int64_t)A.acc->nR;          // k_scan wrote the final reflected count
     for (int sub = 0; sub < 4; ++sub) {
         const int64_t r = tile + sub * 256 + threadIdx.x;
         const bool in = r < A.n;

@@ -1519,6 +1519,8 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         A.blk_cnt = (int32_t *)h->w_blk_cnt.p; A.blk_off = (long long *)h->w_blk_off.p;
         A.blk_pow = (double *)h->w_blk_pow.p; A.acc = (DevAcc *)h->d_acc.p;
         A.nR = h->B.out(); A.nT = h->T.out();
+        A.direct_t = (C >= N) ? 1 : 0;                      // one chunk: no refracted staging
+        if (A.direct_t) A.nT = A.nR;
         A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
         A.mm = (int32_t *)(mf + 4 * mc);
         hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
@@ -1529,9 +1531,11 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     }
     // refracted block after the reflected one (k_append reads the counts on the
     // device), then the counters to the pinned copy: one host sync per iteration
-    hipLaunchKernelGGL(k_append, dim3((unsigned)std::min<int64_t>(grid1(N), 8192)), dim3(256), 0, h->stream,
-                       h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
-    HIPCHK(h, hipGetLastError());
+    if (C < N) {
+        hipLaunchKernelGGL(k_append, dim3((unsigned)std::min<int64_t>(grid1(N), 8192)), dim3(256), 0, h->stream,
+                           h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
+        HIPCHK(h, hipGetLastError());
+    }
     HIPCHK(h, hipMemcpyAsync(h->acc_host, h->d_acc.p, sizeof(DevAcc), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     DevAcc acc = *h->acc_host;
