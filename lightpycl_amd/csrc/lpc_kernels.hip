@@ -925,10 +925,8 @@ __global__ __launch_bounds__(256) void k_keypack(RaysIn R, int64_t n, float bx0,
 
 // ---------------------------------------------------------------------------
 // k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
-__global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
+static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t r)
 {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= A.n) return;
     const f3 O = mk3(A.in.ox[r], A.in.oy[r], A.in.oz[r]);
     const f3 D = mk3(A.in.dx[r], A.in.dy[r], A.in.dz[r]);
     const int32_t prev = A.in.pmid[r];
@@ -958,6 +956,14 @@ __global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
     if (A.o.iidx) {
         A.o.iidx[r] = po.hit_idx; A.o.n1[r] = po.n1; A.o.n2[r] = po.n2; A.o.ent[r] = po.entering;
     }
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
+{
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n) return;
+    (void)shade_ray(A, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -1001,6 +1007,55 @@ __global__ __launch_bounds__(256) void k_count(CompactArgs A)
         }
     }
     // wave reductions (fixed order -> deterministic)
+    for (int o = 32; o >= 1; o >>= 1) {
+        cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); cM += __shfl_xor(cM, o, 64);
+    }
+    pk = wave_sum(pk);
+    dm = wave_max(dm);
+    if (lane == 0) {
+        s_cnt[0][wv] = cR; s_cnt[1][wv] = cT; s_cnt[2][wv] = cM; s_pow[wv] = pk; s_dm[wv] = dm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int64_t b = blockIdx.x, nb = A.nb;
+        A.blk_cnt[0 * nb + b] = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+        A.blk_cnt[1 * nb + b] = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+        A.blk_cnt[2 * nb + b] = s_cnt[2][0] + s_cnt[2][1] + s_cnt[2][2] + s_cnt[2][3];
+        A.blk_pow[b] = ((s_pow[0] + s_pow[1]) + s_pow[2]) + s_pow[3];
+        const float m = fmaxf(fmaxf(s_dm[0], s_dm[1]), fmaxf(s_dm[2], s_dm[3]));
+        atomicMax(&A.acc->dmax2_bits, __float_as_uint(m));
+    }
+}
+
+// k_shade + k_count in one pass: a block shades its 1024-ray tile (4 rays per
+// thread, the k_count tile order) and reduces the tile's counts, kept power and
+// max |dir|^2 from registers, in k_count's fixed order (same bits).
+__global__ __launch_bounds__(256) void k_shade_count(ShadeArgs S, CompactArgs A)
+{
+    __shared__ int32_t s_cnt[3][4];
+    __shared__ double s_pow[4];
+    __shared__ float s_dm[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * 1024;
+    int32_t cR = 0, cT = 0, cM = 0;
+    double pk = 0.0;
+    float dm = 0.0f;
+    for (int sub = 0; sub < 4; ++sub) {
+        const int64_t r = tile + sub * 256 + threadIdx.x;
+        if (r < A.n) {
+            const ShadeOut o = shade_ray(S, r);
+            const bool fR = o.r_meas == 0, fT = o.t_meas == 0, fM = o.meas == 1;
+            cR += fR; cT += fT; cM += fM;
+            if (fR) {
+                pk += (double)o.r_pow;
+                dm = fmaxf(dm, o.r_dir.x * o.r_dir.x + o.r_dir.y * o.r_dir.y + o.r_dir.z * o.r_dir.z);
+            }
+            if (fT) {
+                pk += (double)o.t_pow;
+                dm = fmaxf(dm, o.t_dir.x * o.t_dir.x + o.t_dir.y * o.t_dir.y + o.t_dir.z * o.t_dir.z);
+            }
+        }
+    }
     for (int o = 32; o >= 1; o >>= 1) {
         cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); cM += __shfl_xor(cM, o, 64);
     }

@@ -99,6 +99,7 @@ struct lpc_handle {
     DBuf w_keypart;                                 // per-block OR/AND of the 40-bit codes + selected bits
     int sort_mode = 1;                              // 1: 32-bit key (rocPRIM default), 2: adaptive 16-bit
     int64_t onesweep_min = 500000;                  // 32-bit key: onesweep from this many rays
+    bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -940,6 +941,20 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     return 0;
 }
 
+static ShadeArgs shade_args(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, int64_t n, float max_ray_len,
+                            float ior_env, bool extra)
+{
+    ShadeArgs A;
+    A.in = in; A.meas_in = meas_in; A.n = n; A.K = h->K;
+    A.skey = (const unsigned long long *)h->w_key.p; A.sc = (const int32_t *)h->w_sc.p;
+    A.mat_type = (const int32_t *)h->d_mat.p; A.ior = (const float *)h->d_ior.p;
+    A.refl = (const float *)h->d_refl.p; A.diss = (const float *)h->d_diss.p;
+    A.verts = (const float *)h->d_verts.p;
+    A.max_ray_len = max_ray_len; A.ior_env = ior_env;
+    A.o = shade_ptrs(h, extra);
+    return A;
+}
+
 static int run_shade(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, int64_t n,
                      float max_ray_len, float ior_env, bool extra)
 {
@@ -1013,6 +1028,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
     h->sort_mode = env_int("LPC_SORT", h->sort_mode) == 2 ? 2 : 1;
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
+    h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
@@ -1499,8 +1515,24 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2));
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-        RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
         ShadeOutPtrs o = shade_ptrs(h, false);
+        CompactArgs A;
+        A.n = nc; A.nb = (nc + 1023) / 1024; A.o = o;
+        A.blk_cnt = (int32_t *)h->w_blk_cnt.p; A.blk_off = (long long *)h->w_blk_off.p;
+        A.blk_pow = (double *)h->w_blk_pow.p; A.acc = (DevAcc *)h->d_acc.p;
+        A.nR = h->B.out(); A.nT = h->T.out();
+        A.direct_t = (C >= N) ? 1 : 0;                      // one chunk: no refracted staging
+        if (A.direct_t) A.nT = A.nR;
+        A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
+        A.mm = (int32_t *)(mf + 4 * mc);
+        if (h->fuse_shade) {          // postproc + Fresnel + the tile counts in one pass
+            const ShadeArgs SA = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
+            hipLaunchKernelGGL(k_shade_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, SA, A);
+            HIPCHK(h, hipGetLastError());
+        } else {
+            RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
+            hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
+        }
         if (out_origin4 || out_dest4 || out_pow || out_meas) {
             auto pack = [&](float *dst4, const float *x, const float *y, const float *z) -> int {
                 hipLaunchKernelGGL(k_pack4, dim3(grid1(nc)), dim3(256), 0, h->stream, nc, x, y, z,
@@ -1514,16 +1546,6 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             if (out_pow) HIPCHK(h, hipMemcpy(out_pow + base, o.pw, (size_t)nc * 4, hipMemcpyDeviceToHost));
             if (out_meas) HIPCHK(h, hipMemcpy(out_meas + base, o.meas, (size_t)nc * 4, hipMemcpyDeviceToHost));
         }
-        CompactArgs A;
-        A.n = nc; A.nb = (nc + 1023) / 1024; A.o = o;
-        A.blk_cnt = (int32_t *)h->w_blk_cnt.p; A.blk_off = (long long *)h->w_blk_off.p;
-        A.blk_pow = (double *)h->w_blk_pow.p; A.acc = (DevAcc *)h->d_acc.p;
-        A.nR = h->B.out(); A.nT = h->T.out();
-        A.direct_t = (C >= N) ? 1 : 0;                      // one chunk: no refracted staging
-        if (A.direct_t) A.nT = A.nR;
-        A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
-        A.mm = (int32_t *)(mf + 4 * mc);
-        hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, h->stream, A);
         hipLaunchKernelGGL(k_scatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         HIPCHK(h, hipGetLastError());
