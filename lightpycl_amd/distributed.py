@@ -34,10 +34,23 @@ class TorchComm:
         self.device = device
 
     def allreduce_sum(self, values):
-        t = self.torch.tensor(np.asarray(values, dtype=np.float64), dtype=self.torch.float64,
-                              device=self.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return t.cpu().numpy()
+        v = np.asarray(values, dtype=np.float64).reshape(-1)
+        if self.device == "cpu":
+            t = self.torch.from_numpy(v.copy())
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+            return t.numpy()
+        # GPU (RCCL): persistent device and pinned host buffers, no per-call allocation
+        n = v.shape[0]
+        if getattr(self, "_dev", None) is None or self._dev.shape[0] < n:
+            m = max(n, 64)
+            self._dev = self.torch.zeros(m, dtype=self.torch.float64, device=self.device)
+            self._host = self.torch.zeros(m, dtype=self.torch.float64).pin_memory()
+        h, d = self._host[:n], self._dev[:n]
+        h.copy_(self.torch.from_numpy(v))
+        d.copy_(h, non_blocking=True)
+        self.dist.all_reduce(d, op=self.dist.ReduceOp.SUM)
+        h.copy_(d)
+        return h.numpy().copy()
 
     @property
     def rank(self):

@@ -79,3 +79,37 @@ def test_ray_sharded_halves_match(name, n, depth):
     assert counts == r["global_counts"]
     assert cnt == full_cnt
     np.testing.assert_allclose(mp, full_mp, rtol=1e-9, atol=0.0)
+
+
+@pytest.mark.gpu
+def test_rccl_comm_single_rank():
+    """The RCCL code path of TorchComm (device + pinned host buffers) on a
+    one-rank process group: the all-reduced trace equals the local trace."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    from lightpycl_amd.distributed import TorchComm
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        comm = TorchComm(dist, 0)
+        np.testing.assert_array_equal(comm.allreduce_sum([1.0, 2.5, 3.0]), [1.0, 2.5, 3.0])
+        np.testing.assert_array_equal(comm.allreduce_sum(np.arange(100.0)), np.arange(100.0))
+        sc = scenes.BUILDERS["lens"](n=20_000, seed=7, iterations=8)
+        o, d, p = _rays(sc)
+        in_pow = float(np.sum(p, dtype=np.float64))
+        e = _engine(sc, o, d, p)
+        r_comm = ShardedTrace(e, comm).run(8, sc.tau, in_pow)
+        e.reset()
+        r_loc = ShardedTrace(e).run(8, sc.tau, in_pow)
+        e.close()
+        assert r_comm["global_counts"] == r_loc["global_counts"]
+        np.testing.assert_allclose(r_comm["mesh_power"], r_loc["mesh_power"], rtol=1e-12, atol=0.0)
+    finally:
+        dist.destroy_process_group()
