@@ -376,16 +376,26 @@ __global__ __launch_bounds__(256, MINB) void k_intersect(RaysIn R, const float *
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
                                                    uint32_t *__restrict__ wrec, SpillArgs SP, int pgroup,
-                                                   int npieces)
+                                                   int npieces, int xcd_rows)
 {
     __shared__ WaveLds lds[4];
     const int wv = threadIdx.x >> 6;
-    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+    unsigned bx = blockIdx.x, by = blockIdx.y;
+    if (xcd_rows > 0) {
+        // XCD-aware order: blocks are dealt to the 8 XCDs round-robin in launch
+        // order, so XCD k gets rows k, k + 8, ... (grid.y padded to a multiple
+        // of 8; xcd_rows = real rows): each XCD's L2 holds only its pieces' records
+        const unsigned L = blockIdx.y * gridDim.x + blockIdx.x, j = L >> 3;
+        by = (j / gridDim.x) * 8u + (L & 7u);
+        bx = j % gridDim.x;
+        if ((int)by >= xcd_rows) return;
+    }
+    const int64_t w = (int64_t)bx * 4 + wv;
     if (w * 64 >= n) return;                       // whole wave past the end
     // grid.y = ceil(npieces / pgroup): the wave takes pgroup pieces in turn
     // (fewer waves launched only to fail a piece's root test; wave launch
     // rate, ~1 per ns over the chip, bounds a launch of mostly empty waves)
-    const int p0 = (int)blockIdx.y * pgroup;
+    const int p0 = (int)by * pgroup;
     const int p1 = min(p0 + pgroup, npieces);
     for (int p = p0; p < p1; ++p) {
         const Piece P = pieces[p];

@@ -99,6 +99,7 @@ struct lpc_handle {
     DBuf w_keypart;                                 // per-block OR/AND of the 40-bit codes + selected bits
     int sort_mode = 1;                              // 1: 32-bit key (rocPRIM default), 2: adaptive 16-bit
     int64_t onesweep_min = 500000;                  // 32-bit key: onesweep from this many rays
+    int xcd_min_rows = 0;                           // k_intersect XCD-aware order from this many rows (0 off)
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
@@ -847,14 +848,16 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         else if (h->wave_target > 0)
             pgroup = (int)std::max<int64_t>(1, (4 * bxw * pt->npieces) / h->wave_target);
         pgroup = std::max(1, std::min(pgroup, (int)pt->npieces));
-        const dim3 grid((unsigned)bxw, (unsigned)((pt->npieces + pgroup - 1) / pgroup));
+        const int rows = (pt->npieces + pgroup - 1) / pgroup;
+        const int xrows = (h->xcd_min_rows > 0 && rows >= h->xcd_min_rows) ? rows : 0;
+        const dim3 grid((unsigned)bxw, (unsigned)(xrows ? (rows + 7) / 8 * 8 : rows));
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
 #define LPC_LAUNCH_ISECT(WW, MB)                                                                               \
     hipLaunchKernelGGL((k_intersect<WW, MB>), grid, dim3(256), 0, h->stream, in, rs, n, perm,                       \
                        (const NodeW<WW> *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,        \
                        (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,         \
-                       (int)pt->npieces)
+                       (int)pt->npieces, xrows)
         if (h->built_w == 8) {
             if (h->isect_minb == 6) LPC_LAUNCH_ISECT(8, 6);
             else LPC_LAUNCH_ISECT(8, 1);
@@ -1029,6 +1032,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sort_mode = env_int("LPC_SORT", h->sort_mode) == 2 ? 2 : 1;
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
     h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
+    h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
