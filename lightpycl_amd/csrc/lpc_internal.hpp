@@ -107,6 +107,17 @@ struct DevAcc {                       // device-side counters of one iteration
     unsigned int pad;
 };
 
+struct SlotInit {                     // per-mesh slot initial state of a launch (k_slot_init)
+    int32_t K;
+    const int32_t *live;
+    float max_ray_len;
+    unsigned long long *skey;
+    int32_t *scnt;
+    uint32_t *misc;                   // LPC_MISC_WORDS per-launch words (reset), may be NULL
+    DevAcc *acc;                      // iteration counters to reset, may be NULL
+    unsigned long long m_total;
+};
+
 struct CompactArgs {
     int64_t n, nb;                    // rays in chunk, 1024-ray tiles
     ShadeOutPtrs o;

@@ -705,17 +705,26 @@ __global__ __launch_bounds__(256) void k_gather_aos(const float4 *__restrict__ a
 // Slot initial state: slots a run flushes into start at (max_ray_len, idx -1,
 // count 0); slots no run writes keep the reference's initial scratch
 // (max_ray_len, idx 0, count 0).  Also empties the launch's origin box (misc).
-__global__ __launch_bounds__(256) void k_slot_init(int64_t n, int32_t K, const int32_t *__restrict__ live,
-                                                   float max_ray_len, unsigned long long *__restrict__ skey,
-                                                   int32_t *__restrict__ scnt, uint32_t *__restrict__ misc)
+// (also, when SI.acc != NULL, the iteration counters: k_acc_init folded in)
+static __device__ __forceinline__ void slot_init_ray(const SlotInit &SI, int64_t n, int64_t r)
 {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (misc && r < LPC_MISC_WORDS) misc[r] = r < 3 ? 0xffffffffu : 0u;
-    if (r >= n) return;
-    for (int32_t j = 0; j < K; ++j) {
-        skey[(int64_t)j * n + r] = slot_key(max_ray_len, live[j] ? -1 : 0);
-        scnt[(int64_t)j * n + r] = 0;
+    if (SI.misc && r < LPC_MISC_WORDS) SI.misc[r] = r < 3 ? 0xffffffffu : 0u;
+    if (SI.acc && r == 0) {
+        DevAcc z;
+        memset(&z, 0, sizeof(z));
+        z.m_total = SI.m_total;
+        *SI.acc = z;
     }
+    if (r >= n) return;
+    for (int32_t j = 0; j < SI.K; ++j) {
+        SI.skey[(int64_t)j * n + r] = slot_key(SI.max_ray_len, SI.live[j] ? -1 : 0);
+        SI.scnt[(int64_t)j * n + r] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_slot_init(int64_t n, SlotInit SI)
+{
+    slot_init_ray(SI, n, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // Drop-in export of the slots to the reference's scratch buffers
@@ -791,9 +800,11 @@ __global__ __launch_bounds__(256) void k_bbox(RaysIn R, int64_t n, uint32_t *__r
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
                                                 float sx, float sy, float sz, const uint32_t *__restrict__ bb,
                                                 int64_t split, int dir_major, uint32_t *__restrict__ keys,
-                                                int32_t *__restrict__ vals, float4 *__restrict__ aos)
+                                                int32_t *__restrict__ vals, float4 *__restrict__ aos,
+                                                SlotInit SI)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (SI.skey) slot_init_ray(SI, n, i);           // k_slot_init folded in (one launch fewer)
     if (i >= n) return;
     if (aos) {          // the ray as one 32-byte row: k_gather_aos reads it with one line per ray
         aos[2 * i] = make_float4(R.ox[i], R.oy[i], R.oz[i], R.dx[i]);

@@ -100,6 +100,8 @@ struct lpc_handle {
     int sort_mode = 1;                              // 1: 32-bit key (rocPRIM default), 2: adaptive 16-bit
     int64_t onesweep_min = 500000;                  // 32-bit key: onesweep from this many rays
     int xcd_min_rows = 0;                           // k_intersect XCD-aware order from this many rows (0 off)
+    bool acc_pending = false;                       // next slot reset also resets the iteration counters
+    int64_t acc_pending_total = 0;
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
@@ -741,11 +743,23 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     unsigned long long *skey = (unsigned long long *)h->w_key.p;
     int32_t *scnt = (int32_t *)h->w_sc.p;
     uint32_t *misc = (uint32_t *)h->d_misc.p;
-    hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream, n,
-                       h->K, (const int32_t *)h->d_live.p, max_ray_len, skey, scnt, misc);
+    SlotInit SI;
+    SI.K = h->K; SI.live = (const int32_t *)h->d_live.p; SI.max_ray_len = max_ray_len;
+    SI.skey = skey; SI.scnt = scnt; SI.misc = misc;
+    SI.acc = h->acc_pending ? (DevAcc *)h->d_acc.p : nullptr;
+    SI.m_total = (unsigned long long)h->acc_pending_total;
+    h->acc_pending = false;
+    const bool sorted = h->sort_rays && n >= h->sort_min;
+    // the slot reset rides on k_raykey when it runs before everything that reads misc
+    const bool fold_init = sorted && h->sort_mode == 1 && !(h->key_mode == 1 || h->key_mode == 2);
+    if (!fold_init)
+        hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
+                           n, SI);
+    SlotInit SIk = SI;
+    if (!fold_init) SIk.skey = nullptr;
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
-    if (h->sort_rays && n >= h->sort_min) {
+    if (sorted) {
         // coherence order: rays of one wave share origin cell and direction
         const size_t C = (size_t)h->ws_rays;
         uint32_t *kin = (uint32_t *)h->w_sort.p, *kout = kin + C;
@@ -782,7 +796,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                            h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
-                           h->key_mode >= 3 ? 1 : 0, kin, vin, h->gather_aos ? (float4 *)h->w_aos.p : nullptr);
+                           h->key_mode >= 3 ? 1 : 0, kin, vin, h->gather_aos ? (float4 *)h->w_aos.p : nullptr, SIk);
         size_t tb = h->sort_tmp_bytes;
         if (n >= h->onesweep_min)       // large populations: onesweep (4 digit passes)
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
@@ -1508,8 +1522,13 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     RETIF(pop_reserve(h, h->B, 2 * N));
     RETIF(pop_reserve(h, h->T, N));
     RETIF(ensure_measured(h, h->m_total + N));
-    hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p,
-                       (unsigned long long)h->m_total);
+    if (C >= N) {                       // one chunk: the counters reset rides on the slot reset
+        h->acc_pending = true;
+        h->acc_pending_total = h->m_total;
+    } else {
+        hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p,
+                           (unsigned long long)h->m_total);
+    }
     const size_t mc = (size_t)h->m_cap;
     float *mf = (float *)h->m_buf.p;
     for (int64_t base = 0; base < N; base += C) {
