@@ -126,10 +126,26 @@ struct CompactArgs {
     double *blk_pow;                  // [nb]
     DevAcc *acc;
     RaysOut nR, nT;                   // next population: reflected block, refracted staging
+    int32_t *childR, *childT;         // order chaining: each parent's children's positions (or NULL)
     int direct_t;                     // single chunk: refracted children go straight after the
                                       // reflected block (offset acc->nR), no staging / k_append
     float *mx, *my, *mz, *mp;         // measured record
     int32_t *mm;
+};
+
+// Order chaining (k_ocount / k_oscan / k_oscatter): the next population's
+// coherence order = the kept children in their parents' traced order
+// ([reflected ; refracted]), with the rays copied into that order.
+struct OrderArgs {
+    int64_t n, nb;                    // parents, 1024-parent tiles
+    const int32_t *perm;              // traced order of the parents (position -> index)
+    const int32_t *childR, *childT;   // parent index -> child position (-1 none)
+    ShadeOutPtrs o;                   // parents' shade outputs (child rays)
+    int32_t *blk;                     // [2][nb] counts, then offsets
+    long long *totR;                  // reflected children total (device)
+    const DevAcc *acc;                // n_next = acc->nR + acc->nT
+    int32_t *perm_next;               // [n_next]
+    float *rs_next;                   // [6][n_next]
 };
 
 struct PostprocAosArgs {

@@ -1182,6 +1182,10 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
         if (fR || fT || fM) {
             const float dx = A.o.destx[r], dy = A.o.desty[r], dz = A.o.destz[r];
             const int32_t mid = A.o.imid[r];
+            if (A.childR) {
+                A.childR[r] = fR ? (int32_t)(base[0] + wo[0] + pR) : -1;
+                A.childT[r] = fT ? (int32_t)(base[1] + wo[1] + pT) : -1;
+            }
             if (fR) {
                 const int64_t q = base[0] + wo[0] + pR;
                 A.nR.ox[q] = dx; A.nR.oy[q] = dy; A.nR.oz[q] = dz;
@@ -1199,7 +1203,103 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
                 A.mx[q] = dx; A.my[q] = dy; A.mz[q] = dz; A.mp[q] = A.o.pw[r]; A.mm[q] = mid;
             }
         }
+        if (A.childR && in && !(fR || fT || fM)) { A.childR[r] = -1; A.childT[r] = -1; }
         for (int f = 0; f < 3; ++f) base[f] += tot[f];
+        __syncthreads();
+    }
+}
+
+// Order chaining.  Tiles of 1024 parents in their traced order: counts of kept
+// reflected / refracted children, single-block scan, scatter of the children's
+// positions (perm_next) and rays (rs_next) in [reflected ; refracted] order.
+__global__ __launch_bounds__(256) void k_ocount(OrderArgs A)
+{
+    __shared__ int32_t s_c[2][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t cR = 0, cT = 0;
+    for (int sub = 0; sub < 4; ++sub) {
+        const int64_t s = (int64_t)blockIdx.x * 1024 + sub * 256 + threadIdx.x;
+        if (s < A.n) {
+            const int32_t r = A.perm[s];
+            cR += A.childR[r] >= 0;
+            cT += A.childT[r] >= 0;
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) { cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); }
+    if (lane == 0) { s_c[0][wv] = cR; s_c[1][wv] = cT; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        A.blk[blockIdx.x] = s_c[0][0] + s_c[0][1] + s_c[0][2] + s_c[0][3];
+        A.blk[A.nb + blockIdx.x] = s_c[1][0] + s_c[1][1] + s_c[1][2] + s_c[1][3];
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_oscan(OrderArgs A)
+{
+    __shared__ long long s_sc[2][1024];
+    const int t = threadIdx.x;
+    const int64_t nb = A.nb, per = (nb + 1023) / 1024, lo = t * per, hi = min(nb, lo + per);
+    long long loc[2] = {0, 0};
+    for (int64_t i = lo; i < hi; ++i) { loc[0] += A.blk[i]; loc[1] += A.blk[nb + i]; }
+    s_sc[0][t] = loc[0]; s_sc[1][t] = loc[1];
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        long long v0 = 0, v1 = 0;
+        if (t >= off) { v0 = s_sc[0][t - off]; v1 = s_sc[1][t - off]; }
+        __syncthreads();
+        s_sc[0][t] += v0; s_sc[1][t] += v1;
+        __syncthreads();
+    }
+    long long run[2] = {s_sc[0][t] - loc[0], s_sc[1][t] - loc[1]};     // exclusive
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t a = A.blk[i], b = A.blk[nb + i];
+        A.blk[i] = (int32_t)run[0]; A.blk[nb + i] = (int32_t)run[1];
+        run[0] += a; run[1] += b;
+    }
+    if (t == 1023) *A.totR = s_sc[0][1023];
+}
+
+__global__ __launch_bounds__(256) void k_oscatter(OrderArgs A)
+{
+    __shared__ int32_t s_w[2][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nn = (int64_t)A.acc->nR + (int64_t)A.acc->nT;
+    const int64_t totR = *A.totR;
+    int64_t base[2] = {A.blk[blockIdx.x], totR + A.blk[A.nb + blockIdx.x]};
+    for (int sub = 0; sub < 4; ++sub) {
+        const int64_t s = (int64_t)blockIdx.x * 1024 + sub * 256 + threadIdx.x;
+        const bool in = s < A.n;
+        const int32_t r = in ? A.perm[s] : 0;
+        const int32_t qR = in ? A.childR[r] : -1, qT = in ? A.childT[r] : -1;
+        const bool fR = qR >= 0, fT = qT >= 0;
+        const uint64_t bR = __ballot(fR), bT = __ballot(fT);
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        if (lane == 0) { s_w[0][wv] = __popcll(bR); s_w[1][wv] = __popcll(bT); }
+        __syncthreads();
+        int32_t wo[2] = {0, 0}, tot[2] = {0, 0};
+        for (int w = 0; w < 4; ++w)
+            for (int f = 0; f < 2; ++f) {
+                if (w < wv) wo[f] += s_w[f][w];
+                tot[f] += s_w[f][w];
+            }
+        if (fR || fT) {
+            const float ox = A.o.destx[r], oy = A.o.desty[r], oz = A.o.destz[r];
+            if (fR) {
+                const int64_t j = base[0] + wo[0] + __popcll(bR & below);
+                A.perm_next[j] = qR;
+                A.rs_next[j] = ox; A.rs_next[nn + j] = oy; A.rs_next[2 * nn + j] = oz;
+                A.rs_next[3 * nn + j] = A.o.rdx[r]; A.rs_next[4 * nn + j] = A.o.rdy[r];
+                A.rs_next[5 * nn + j] = A.o.rdz[r];
+            }
+            if (fT) {
+                const int64_t j = base[1] + wo[1] + __popcll(bT & below);
+                A.perm_next[j] = qT;
+                A.rs_next[j] = ox; A.rs_next[nn + j] = oy; A.rs_next[2 * nn + j] = oz;
+                A.rs_next[3 * nn + j] = A.o.tdx[r]; A.rs_next[4 * nn + j] = A.o.tdy[r];
+                A.rs_next[5 * nn + j] = A.o.tdz[r];
+            }
+        }
+        for (int f = 0; f < 2; ++f) base[f] += tot[f];
         __syncthreads();
     }
 }

@@ -101,6 +101,13 @@ struct lpc_handle {
     int64_t onesweep_min = 500000;                  // 32-bit key: onesweep from this many rays
     int xcd_min_rows = 0;                           // k_intersect XCD-aware order from this many rows (0 off)
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
+    bool order_chain = false;                       // children inherit their parents' traced order (no sort)
+    bool order_ready = false;                       // w_perm2/w_rs2[order_buf] hold the next launch's order
+    bool order_pending = false;                     // written this iteration; ready once n_next is known
+    int order_buf = 0;
+    int64_t order_n = -1;
+    const int32_t *last_perm = nullptr;             // order of the last intersect launch (NULL: unsorted)
+    DBuf w_chR, w_chT, w_oblk, w_perm2[2], w_rs2[2];
     int64_t acc_pending_total = 0;
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool gather_aos = true;
@@ -751,7 +758,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     h->acc_pending = false;
     const bool sorted = h->sort_rays && n >= h->sort_min;
     // the slot reset rides on k_raykey when it runs before everything that reads misc
-    const bool fold_init = sorted && h->sort_mode == 1 && !(h->key_mode == 1 || h->key_mode == 2);
+    const bool fold_init = sorted && h->sort_mode == 1 && !(h->key_mode == 1 || h->key_mode == 2) &&
+                           !(h->order_ready && n == h->order_n);
     if (!fold_init)
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
                            n, SI);
@@ -759,7 +767,12 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (!fold_init) SIk.skey = nullptr;
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
-    if (sorted) {
+    const bool chained = h->order_ready && n == h->order_n;
+    h->order_ready = false;
+    if (chained) {                      // the previous iteration wrote this order (k_oscatter)
+        perm = (const int32_t *)h->w_perm2[h->order_buf].p;
+        rs = (const float *)h->w_rs2[h->order_buf].p;
+    } else if (sorted) {
         // coherence order: rays of one wave share origin cell and direction
         const size_t C = (size_t)h->ws_rays;
         uint32_t *kin = (uint32_t *)h->w_sort.p, *kout = kin + C;
@@ -813,6 +826,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         rs = (const float *)h->w_rs.p;
         }
     }
+    h->last_perm = perm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
@@ -1047,6 +1061,7 @@ int lpc_open(int device, lpc_handle **out)
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
     h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
     h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
+    h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
@@ -1087,7 +1102,8 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos, &h->d_lane, &h->w_keypart};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
+                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1]};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1450,6 +1466,7 @@ int lpc_trace_reset(lpc_handle *h)
         hipLaunchKernelGGL(k_copy_pop, dim3((unsigned)std::min<int64_t>(grid1(h->n_init), 8192)), dim3(256), 0,
                            h->stream, h->A.out(), h->I.in(0), h->n_init);
     h->n_cur = h->n_init;
+    h->order_ready = h->order_pending = false;
     h->split = INT64_MAX;                       // emitted rays: one class
     h->pop_dmax2 = h->init_dmax2;
     h->m_total = 0;                             // measured record emptied in-stream
@@ -1548,6 +1565,13 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         if (A.direct_t) A.nT = A.nR;
         A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
         A.mm = (int32_t *)(mf + 4 * mc);
+        const bool chain = h->order_chain && A.direct_t && h->last_perm != nullptr;
+        A.childR = A.childT = nullptr;
+        if (chain) {
+            RETIF(dalloc(h, h->w_chR, (size_t)nc * 4));
+            RETIF(dalloc(h, h->w_chT, (size_t)nc * 4));
+            A.childR = (int32_t *)h->w_chR.p; A.childT = (int32_t *)h->w_chT.p;
+        }
         if (h->fuse_shade) {          // postproc + Fresnel + the tile counts in one pass
             const ShadeArgs SA = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
             hipLaunchKernelGGL(k_shade_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, SA, A);
@@ -1572,6 +1596,26 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, h->stream, A);
         hipLaunchKernelGGL(k_scatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         HIPCHK(h, hipGetLastError());
+        if (chain) {                    // the next population's order: children in their parents' order
+            const int tgt = (h->last_perm == (const int32_t *)h->w_perm2[0].p) ? 1 : 0;
+            RETIF(dalloc(h, h->w_perm2[tgt], (size_t)2 * N * 4));
+            RETIF(dalloc(h, h->w_rs2[tgt], (size_t)2 * N * 6 * 4));
+            RETIF(dalloc(h, h->w_oblk, (size_t)2 * A.nb * 4 + 64));
+            OrderArgs Ob;
+            Ob.n = nc; Ob.nb = A.nb; Ob.perm = h->last_perm;
+            Ob.childR = A.childR; Ob.childT = A.childT; Ob.o = o;
+            Ob.blk = (int32_t *)h->w_oblk.p;
+            Ob.totR = (long long *)((char *)h->w_oblk.p + (size_t)2 * A.nb * 4 + 8 - ((size_t)2 * A.nb * 4) % 8);
+            Ob.acc = (const DevAcc *)h->d_acc.p;
+            Ob.perm_next = (int32_t *)h->w_perm2[tgt].p;
+            Ob.rs_next = (float *)h->w_rs2[tgt].p;
+            hipLaunchKernelGGL(k_ocount, dim3((unsigned)A.nb), dim3(256), 0, h->stream, Ob);
+            hipLaunchKernelGGL(k_oscan, dim3(1), dim3(1024), 0, h->stream, Ob);
+            hipLaunchKernelGGL(k_oscatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, Ob);
+            HIPCHK(h, hipGetLastError());
+            h->order_buf = tgt;
+            h->order_pending = true;
+        }
         if (h->prof && !h->prof_light) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
     }
     // refracted block after the reflected one (k_append reads the counts on the
@@ -1592,6 +1636,9 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (h->prof) prof_resolve(h);
     std::swap(h->A, h->B);
     h->n_cur = nR + nT;
+    h->order_ready = h->order_pending;
+    h->order_pending = false;
+    h->order_n = nR + nT;
     h->split = nR;
     h->m_total = (int64_t)acc.m_total;
     S.n_reflect = nR; S.n_refract = nT; S.n_measured = (int64_t)acc.nM_iter;

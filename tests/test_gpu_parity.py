@@ -73,7 +73,7 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
 
 @pytest.mark.parametrize("cfg", [dict(LPC_FLAT="0"), dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"),
                                  dict(LPC_FLAT="20", LPC_KEY="2"), dict(LPC_KEY="3"), dict(LPC_KEY="1"),
-                                 dict(LPC_SORT="0"), dict(LPC_SORT="2"), dict(LPC_GATHER_AOS="0"), dict(LPC_WAVE_TARGET="2000"), dict(LPC_WAVE_TARGET="0"), dict(LPC_SLIVER_CULL="0"), dict(LPC_ISECT_MINB="1"), dict(LPC_FUSE_SHADE="1"), dict(LPC_XCD_ROWS="1"), dict(LPC_XCD_ROWS="1", LPC_WAVE_TARGET="0"), dict(LPC_LANE_MAX="100000000"), dict(LPC_LANE_MAX="100000000", LPC_LANE_G="8"), dict(LPC_BUDGET="0"), dict(LPC_BUDGET="4"),
+                                 dict(LPC_SORT="0"), dict(LPC_SORT="2"), dict(LPC_GATHER_AOS="0"), dict(LPC_WAVE_TARGET="2000"), dict(LPC_WAVE_TARGET="0"), dict(LPC_SLIVER_CULL="0"), dict(LPC_ISECT_MINB="1"), dict(LPC_FUSE_SHADE="1"), dict(LPC_XCD_ROWS="1"), dict(LPC_CHAIN="1"), dict(LPC_XCD_ROWS="1", LPC_WAVE_TARGET="0"), dict(LPC_LANE_MAX="100000000"), dict(LPC_LANE_MAX="100000000", LPC_LANE_G="8"), dict(LPC_BUDGET="0"), dict(LPC_BUDGET="4"),
                                  dict(LPC_BUDGET="6", LPC_SPILL_CAP="100"),
                                  dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
                                  dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"), dict(LPC_LOOP="1", LPC_LOOP_MIN="1"),
