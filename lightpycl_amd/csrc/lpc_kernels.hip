@@ -786,8 +786,20 @@ __global__ __launch_bounds__(256) void k_bbox(RaysIn R, int64_t n, uint32_t *__r
         for (int k = 0; k < 3; ++k) { mn[k] = fminf(mn[k], o[k]); mx[k] = fmaxf(mx[k], o[k]); }
     }
     for (int k = 0; k < 3; ++k) { mn[k] = wave_red(mn[k], 0); mx[k] = wave_red(mx[k], 1); }
-    if ((threadIdx.x & 63) == 0 && mn[0] <= mx[0]) {
-        for (int k = 0; k < 3; ++k) { atomicMin(&bb[k], ord_enc(mn[k])); atomicMax(&bb[3 + k], ord_enc(mx[k])); }
+    // block-level reduction, then one atomic per word per block (device atomics on
+    // one word serialise: the grid is kept small)
+    __shared__ float s_b[6][4];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 3; ++k) { s_b[k][wv] = mn[k]; s_b[3 + k][wv] = mx[k]; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = fminf(fminf(s_b[k][0], s_b[k][1]), fminf(s_b[k][2], s_b[k][3]));
+            mx[k] = fmaxf(fmaxf(s_b[3 + k][0], s_b[3 + k][1]), fmaxf(s_b[3 + k][2], s_b[3 + k][3]));
+        }
+        if (mn[0] <= mx[0])
+            for (int k = 0; k < 3; ++k) { atomicMin(&bb[k], ord_enc(mn[k])); atomicMax(&bb[3 + k], ord_enc(mx[k])); }
     }
 }
 

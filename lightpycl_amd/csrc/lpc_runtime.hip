@@ -758,7 +758,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     h->acc_pending = false;
     const bool sorted = h->sort_rays && n >= h->sort_min;
     // the slot reset rides on k_raykey when it runs before everything that reads misc
-    const bool fold_init = sorted && h->sort_mode == 1 && !(h->key_mode == 1 || h->key_mode == 2) &&
+    const bool fold_init = sorted && h->sort_mode == 1 &&
+                           !(h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX)) &&
                            !(h->order_ready && n == h->order_n);
     if (!fold_init)
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
@@ -780,7 +781,9 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         // key_mode: 0 [scene-box origin cell | direction], 1 population origin box,
         // 2 = 1 + refracted-block bit, 3 [direction | scene-box origin cell],
         // 4 = 3 + refracted-block bit
-        const bool pop_box = h->key_mode == 1 || h->key_mode == 2;
+        // 5: population box for populations that are not a trace's children (the
+        // emitted rays: a collimated beam gets fine origin cells), scene box after
+        const bool pop_box = h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX);
         const bool cls = h->key_mode == 2 || h->key_mode == 4;
         if (h->sort_mode == 2) {
             // adaptive 16-bit key: 3 small kernels + a 2-pass radix sort
@@ -804,12 +807,13 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             rs = (const float *)h->w_rs.p;
         } else {
         if (pop_box)
-            hipLaunchKernelGGL(k_bbox, dim3((unsigned)std::min<int64_t>(grid1(n), 1024)), dim3(256), 0, h->stream,
+            hipLaunchKernelGGL(k_bbox, dim3((unsigned)std::min<int64_t>(grid1(n), 256)), dim3(256), 0, h->stream,
                                in, n, misc);
         hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                            h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
-                           h->key_mode >= 3 ? 1 : 0, kin, vin, h->gather_aos ? (float4 *)h->w_aos.p : nullptr, SIk);
+                           (h->key_mode == 3 || h->key_mode == 4) ? 1 : 0, kin, vin,
+                           h->gather_aos ? (float4 *)h->w_aos.p : nullptr, SIk);
         size_t tb = h->sort_tmp_bytes;
         if (n >= h->onesweep_min)       // large populations: onesweep (4 digit passes)
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
@@ -1062,6 +1066,7 @@ int lpc_open(int device, lpc_handle **out)
     h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
     h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
     h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
+    h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;

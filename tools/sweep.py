@@ -18,12 +18,12 @@ from lightpycl_amd.distributed import ShardedTrace  # noqa: E402
 from lightpycl_amd.engine import Engine  # noqa: E402
 
 KNOBS = ("KEY", "FLAT", "TARGET_BLOCKS", "SORT", "BUDGET", "SPILL_CAP", "SPILL_BLOCKS", "LOOP", "SLIVER_WAVES",
-         "SLIVER_PPW", "NODE_W", "SPILL_LEVELS", "PAIR_SHIFT", "SORT_MIN", "LOOP_MIN", "GATHER_AOS", "SLIVER_RAYS", "WAVE_TARGET", "SLIVER_CULL", "SPILL_SHRINK", "SPILL_MIN_BLOCKS", "LANE_MAX", "LANE_G", "ISECT_MINB", "ONESWEEP_MIN", "SPILL_LEVELS_SMALL", "FUSE_SHADE", "XCD_ROWS", "CHAIN")
+         "SLIVER_PPW", "NODE_W", "SPILL_LEVELS", "PAIR_SHIFT", "SORT_MIN", "LOOP_MIN", "GATHER_AOS", "SLIVER_RAYS", "WAVE_TARGET", "SLIVER_CULL", "SPILL_SHRINK", "SPILL_MIN_BLOCKS", "LANE_MAX", "LANE_G", "ISECT_MINB", "ONESWEEP_MIN", "SPILL_LEVELS_SMALL", "FUSE_SHADE", "XCD_ROWS", "CHAIN", "CHUNK")
 name = sys.argv[1] if len(sys.argv) > 1 else "synthetic"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 configs = sys.argv[4:] or ["KEY=0"]
-steps = 3
+steps = int(os.environ.get("SWEEP_STEPS", "3"))
 sc = scenes.BUILDERS[name](n=n, seed=7)
 o = np.concatenate([np.asarray(s.rays_origin, np.float32) for s in sc.sources])
 d = np.concatenate([np.asarray(s.rays_dir, np.float32) for s in sc.sources])
