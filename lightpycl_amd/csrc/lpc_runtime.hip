@@ -635,9 +635,17 @@ using RaySortCfg = rocprim::default_config;
 using RaySortCfg16 = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                 rocprim::default_config, 0>;
 
+// Rays per chunk.  Default: as many as ~32 GB of per-chunk workspace holds (slots
+// 12 B per mesh + ~200 B of coherence copies, shade outputs and sort buffers per
+// ray), at most 128 Mi: a chunk is also the unit of the coherence sort, and large
+// populations (the eye's grow past 100 M rays) trace up to 1.5x faster in 128 Mi
+// chunks than in 8 Mi ones.
 static int64_t chunk_rays(const lpc_handle *h)
 {
-    return h->chunk > 0 ? h->chunk : (int64_t)8 << 20;
+    if (h->chunk > 0) return h->chunk;
+    const int64_t per_ray = (int64_t)12 * std::max(h->K, 1) + 200;
+    const int64_t c = ((int64_t)32 << 30) / per_ray;
+    return std::max<int64_t>((int64_t)1 << 20, std::min<int64_t>((int64_t)128 << 20, c));
 }
 
 // Workspace for a chunk of `n` rays.
