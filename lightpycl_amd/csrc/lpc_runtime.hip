@@ -125,8 +125,10 @@ struct lpc_handle {
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
-    int64_t target_blocks = 16384;                  // k_intersect: blocks x pieces to fill the GPU
-    int spill_budget = 16;                          // node visits before a wave hands over (0 off)
+    int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
+    int spill_budget = 20;                          // node visits before a wave hands over (0 off)
+    int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
+    int64_t spill_large_n = 1500000;
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
     int spill_levels = 4;                           // k_spill launches (hand-over depth)
@@ -137,7 +139,7 @@ struct lpc_handle {
     int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
     bool piece_loop = false;                        // k_intersect: waves loop over the pieces
     int64_t loop_min_packets = 8192;                //   ... when the population has this many packets
-    int64_t wave_target = 65536;                    // k_intersect: group pieces per wave above this many waves
+    int64_t wave_target = 131072;                   // k_intersect: group pieces per wave above this many waves
     int node_w = 8;                                 // hierarchy width for the next build (4 or 8)
     int built_w = 4;                                // width of the records in d_nodes
     int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
@@ -877,7 +879,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             SP.items = (SpillItem *)h->w_spill.p;
             SP.ctr = misc + LPC_MISC_SPILL;
             SP.cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
-            SP.budget = h->spill_budget;
+            SP.budget = n >= h->spill_large_n ? h->spill_budget_large : h->spill_budget;
             SP.pair_shift = h->spill_pair_shift;
         }
         // pieces per wave: all of them (LPC_LOOP) or enough that the grid has
@@ -1083,6 +1085,8 @@ int lpc_open(int device, lpc_handle **out)
     h->isect_minb = env_int("LPC_ISECT_MINB", h->isect_minb) == 1 ? 1 : 6;
     if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
+    h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
+    h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
     h->spill_levels = (int)env_int("LPC_SPILL_LEVELS", h->spill_levels);
