@@ -79,10 +79,12 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
                                  dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"), dict(LPC_LOOP="1", LPC_LOOP_MIN="1"),
                                  dict(LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1"),
                                  dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_SLIVER_RAYS="64"), dict(LPC_NODE_W="4"),
-                                 dict(LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536")])
+                                 dict(LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536"),
+                                 dict(LPC_LARGE_N="1000"), dict(LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3")])
 def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
     """The launch policies (fan-group threshold, piece granularity, coherence
-    key, no sort, work hand-over budget incl. a queue that overflows) change
+    key, no sort, work hand-over budget incl. a queue that overflows, the
+    population-size budget switch) change
     only speed."""
     from lightpycl_amd.engine import Engine
     for k, v in cfg.items():
