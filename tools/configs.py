@@ -24,7 +24,9 @@ CONFIGS = {   # BASELINE.json configs: rays, depth
     "lens": (10_000_000, 8),
     "eye": (10_000_000, 16),
     "synthetic": (1_000_000, 16),
+    "synthetic_shard": (12_500_000, 16),   # config 5: one GPU's shard of 100 M rays over 8
 }
+SCENE = {"synthetic_shard": "synthetic"}
 
 
 def rays(sc):
@@ -53,7 +55,7 @@ def main():
     for name in names:
         n, depth = CONFIGS[name]
         t0 = time.perf_counter()
-        sc = scenes.BUILDERS[name](n=n, seed=7, iterations=depth)
+        sc = scenes.BUILDERS[SCENE.get(name, name)](n=n, seed=7, iterations=depth)
         o, d, p = rays(sc)
         gen_s = time.perf_counter() - t0
         in_pow = float(np.sum(p, dtype=np.float64))
