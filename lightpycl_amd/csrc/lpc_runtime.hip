@@ -128,7 +128,8 @@ struct lpc_handle {
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 20;                          // node visits before a wave hands over (0 off)
     int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
-    int64_t spill_large_n = 1500000;
+    int64_t spill_large_n = 1500000;                // 0: spill_large_per_tri x triangles
+    int64_t spill_large_per_tri = 64;
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
     int spill_levels = 4;                           // k_spill launches (hand-over depth)
@@ -879,7 +880,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             SP.items = (SpillItem *)h->w_spill.p;
             SP.ctr = misc + LPC_MISC_SPILL;
             SP.cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
-            SP.budget = n >= h->spill_large_n ? h->spill_budget_large : h->spill_budget;
+            const int64_t large_n = h->spill_large_n > 0 ? h->spill_large_n : h->spill_large_per_tri * (int64_t)h->M;
+            SP.budget = n >= large_n ? h->spill_budget_large : h->spill_budget;
             SP.pair_shift = h->spill_pair_shift;
         }
         // pieces per wave: all of them (LPC_LOOP) or enough that the grid has
@@ -1087,6 +1089,7 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
     h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
+    h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
     h->spill_levels = (int)env_int("LPC_SPILL_LEVELS", h->spill_levels);
