@@ -126,7 +126,7 @@ struct lpc_handle {
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int key_mode = 0;                               // coherence key, see run_intersect
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
-    int spill_budget = 20;                          // node visits before a wave hands over (0 off)
+    int spill_budget = 24;                          // node visits before a wave hands over (0 off)
     int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
     int64_t spill_large_n = 1500000;                // 0: spill_large_per_tri x triangles
     int64_t spill_large_per_tri = 64;
