@@ -128,8 +128,8 @@ struct lpc_handle {
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 24;                          // node visits before a wave hands over (0 off)
     int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
-    int64_t spill_large_n = 1500000;                // 0: spill_large_per_tri x triangles
-    int64_t spill_large_per_tri = 64;
+    int64_t spill_large_n = 0;                      // 0: spill_large_per_tri x triangles
+    int64_t spill_large_per_tri = 16;
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
     int spill_levels = 4;                           // k_spill launches (hand-over depth)
