@@ -40,9 +40,60 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 
 // Per-launch device words of the intersect stage (uint32, reset by k_slot_init):
 // [0..5] population origin box (k_bbox, coherence key modes 1-2), [6..13]
-// hand-over queue lengths (k_intersect -> k_spill level 0 -> level 1 ...).
-#define LPC_MISC_WORDS 16
+// hand-over queue lengths (k_intersect -> k_spill level 0 -> level 1 ...),
+// from word 32 the work queue's control words (k_roots / k_trav), every group on
+// a 128-byte line of its own: a device-scope atomic evicts its line from the
+// L2, and one word serialises its atomics (~11 ns each), so counters are sharded.
 #define LPC_MISC_SPILL 6                  // [6 + l]: items queued for hand-over level l (l < 8)
+#define LPC_Q_CSHARDS 8                   // root-item shards (k_roots block b -> b % 8)
+#define LPC_Q_DSHARDS 32                  // hand-over queue shards (k_trav block b -> b % 32)
+#define LPC_Q_NINIT(c) (32 * (1 + (c)))   // root items k_roots wrote into shard c
+#define LPC_Q_CHEAD(c) (32 * (9 + (c)))   // claim head of root shard c
+// Hand-over shard d: a 64-bit word TP = slots reserved (low half) | items
+// handed over and not finished (high half), so one returning atomic reserves
+// slots and counts them before they are published; tickets taken by waiting
+// waves; and, on a line of its own, the shard's waves still in the root phase.
+#define LPC_Q_TP(d) (32 * (17 + 2 * (d)))
+#define LPC_Q_DHEAD(d) (32 * (17 + 2 * (d)) + 2)
+#define LPC_Q_RBUSY(d) (32 * (18 + 2 * (d)))
+#define LPC_MISC_WORDS (32 * (17 + 2 * LPC_Q_DSHARDS))
+
+// Work queue of the intersect stage (k_roots -> k_trav).  An item is one packet
+// (64 rays of the coherence order) against one subtree of a mesh run, packed in
+// 64 bits: packet (24 bits) | node (28 bits) | slot (12 bits).  k_roots writes the
+// (packet, piece root) pairs whose root test some ray passes (the test
+// k_intersect's waves start with); k_trav's waves claim them in batches and walk
+// them, and while waves of their shard wait for work they hand the bottom of
+// their stack over through the shard's queue.  A queue slot holds LPC_QEMPTY
+// until an item is published into it (8-byte agent-scope atomic store: data and
+// flag in one granule); its consumer writes LPC_QEMPTY back, so the queue is
+// empty again between launches.
+#define LPC_QEMPTY 0xffffffffffffffffull
+__host__ __device__ inline uint64_t q_item(uint32_t w, uint32_t node, uint32_t slot)
+{
+    return ((uint64_t)w << 40) | ((uint64_t)node << 12) | (uint64_t)slot;
+}
+__host__ __device__ inline uint32_t q_w(uint64_t it) { return (uint32_t)(it >> 40); }
+__host__ __device__ inline uint32_t q_node(uint64_t it) { return (uint32_t)(it >> 12) & 0x0fffffffu; }
+__host__ __device__ inline uint32_t q_slot(uint64_t it) { return (uint32_t)it & 0xfffu; }
+#define LPC_Q_MAX_PACKETS ((1u << 24) - 1u)
+#define LPC_Q_MAX_NODES ((1u << 28) - 1u)
+#define LPC_Q_MAX_SLOTS 4095
+
+struct QueueArgs {
+    uint64_t *roots;                  // [LPC_Q_CSHARDS][rcap] root items
+    uint64_t *dq;                     // [LPC_Q_DSHARDS][dcap] hand-over slots (LPC_QEMPTY when free)
+    uint32_t *ctl;                    // misc words (LPC_Q_*)
+    uint32_t *err;                    // set when a wave gives up waiting (a bug: never expected)
+    uint32_t rcap, dcap;
+    uint32_t spin_max;                // polls before a waiting wave gives up
+    int32_t batch;                    // root items per claim
+    int32_t hunger;                   // hand work over to waiting waves (0: never, A/B only)
+    int32_t dshard;                   // set per wave by k_trav (-1: no hand-over)
+    uint32_t *irec;                   // per-item records (profiling, lpc_prof_enable(h, 5)) or NULL
+    uint32_t irec_cap;
+};
+#define LPC_Q_IREC_N 16                   // misc word: item records written this launch
 
 // Work hand-over: a k_intersect wave that has visited `budget` nodes with two or
 // more subtrees still on its stack queues each of them as one item; k_spill
@@ -104,7 +155,7 @@ struct DevAcc {                       // device-side counters of one iteration
     unsigned long long nM_iter;       // measured this iteration
     double pow_next;                  // float64 sum of kept children power
     unsigned int dmax2_bits;          // max |dir|^2 of kept children (float bits)
-    unsigned int pad;
+    unsigned int qerr;                // k_trav gave up waiting on its work queue (QueueArgs::err)
 };
 
 struct SlotInit {                     // per-mesh slot initial state of a launch (k_slot_init)

@@ -35,6 +35,11 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 namespace lpck {
 
+// Debug/timing switches (LPC_DBG, read at lpc_open; never set by tests): bit 0 =
+// skip the per-ray result flush of trav_packet (results WRONG; timing of the
+// flush atomics only).
+__constant__ int lpc_dbg = 0;
+
 // ---------------------------------------------------------------------------
 // Intersection.  Rays are processed in the coherence order (k_raykey + radix
 // sort + k_gather); every kernel flushes its per-ray nearest hit and count into
@@ -165,6 +170,26 @@ static __device__ __forceinline__ int select_bit(uint64_t m, int k)
     return pos;
 }
 
+// Publish one item per lane < k into the wave's hand-over shard (k_trav) and
+// return how many fit (lanes [0, fit) were published).  One returning 64-bit
+// atomic reserves the slots and counts the items as pending before any of them
+// is visible; each item is one 8-byte agent-scope store (data = flag).
+static __device__ __forceinline__ int q_publish(const QueueArgs &Q, int k, uint64_t item)
+{
+    const int lane = threadIdx.x & 63;
+    unsigned long long *tp = (unsigned long long *)(Q.ctl + LPC_Q_TP(Q.dshard));
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicAdd(tp, ((unsigned long long)k << 32) | (unsigned long long)k);
+    const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)old);
+    const int fit = base >= Q.dcap ? 0 : (int)min((uint32_t)k, Q.dcap - base);
+    if (fit < k && lane == 0)     // full: the reserved slots beyond it stay empty, uncount them
+        atomicAdd(tp, (unsigned long long)(-(long long)((unsigned long long)(k - fit) << 32)));
+    if (lane < fit)
+        __hip_atomic_store(Q.dq + (size_t)Q.dshard * Q.dcap + base + (uint32_t)lane, item, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return fit;
+}
+
 // LDS of one wave's traversal.
 struct WaveLds {
     int32_t stack[LPC_STACK];
@@ -194,7 +219,10 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
                                                    unsigned long long *__restrict__ stats,
                                                    uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0,
                                                    SpillArgs SP = SpillArgs{nullptr, nullptr, 0u, 0, 31},
-                                                   int32_t start = -1)
+                                                   int32_t start = -1,
+                                                   const QueueArgs &Q = QueueArgs{nullptr, nullptr, nullptr, nullptr,
+                                                                                  0u, 0u, 0u, 1, 0, -1,
+                                                                                  nullptr, 0u})
 {
     const int lane = threadIdx.x & 63;
     const int64_t s = w * 64 + lane;
@@ -262,6 +290,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     };
     int ngr = 0;                                   // fan groups deferred to k_groups
     int budget = SP.budget;
+    uint32_t q_head = 0, q_tail = 0;               // work queue: last read of the shard's counters
     L.stack[top++] = start >= 0 ? start : P.root;
     while (top > 0) {
         // work hand-over: after `budget` nodes the subtrees left on the stack go
@@ -284,6 +313,15 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
             // queue full: void the part of the range inside it, carry on here
             if (lane < top && base + (uint32_t)lane < SP.cap) SP.items[base + lane].node = -1;
             budget = 0;
+        }
+        // work queue (k_trav): every 4th node the shard's waiting waves (tickets
+        // taken beyond the slots reserved) as read 4 nodes ago are acted on, and
+        // a new read is issued (its latency, ~1-2 us, overlaps the next nodes)
+        int waiting = 0;
+        if (Q.hunger && Q.dshard >= 0 && (n_nodes & 3u) == 0u) {
+            waiting = (int)__builtin_amdgcn_readfirstlane((int)(q_head - q_tail));
+            q_tail = __hip_atomic_load(Q.ctl + LPC_Q_TP(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            q_head = __hip_atomic_load(Q.ctl + LPC_Q_DHEAD(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
         const NodeW<W> N = nodes[node];
@@ -322,6 +360,20 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
                 }
             }
         }
+        // hand the bottom of the stack (the largest subtrees) to waiting waves,
+        // at most one entry per waiting wave; keep the top entry
+        if (waiting > 0 && top >= 2) {
+            const int k = min(min(top - 1, waiting), 63);
+            const int32_t ent = lane < k ? L.stack[lane] : 0;
+            const int fit = q_publish(Q, k, q_item((uint32_t)w, (uint32_t)ent, (uint32_t)P.slot));
+            if (fit > 0) {
+                const int32_t keep = lane + fit < top ? L.stack[lane + fit] : 0;
+                __builtin_amdgcn_wave_barrier();
+                if (lane + fit < top) L.stack[lane] = keep;
+                __builtin_amdgcn_wave_barrier();
+                top -= fit;
+            }
+        }
     }
     drain();
     if (stats) {
@@ -353,7 +405,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
             r[0] = (uint32_t)(wall_clock64() - clk0); r[1] = n_nodes; r[2] = n_exact; r[3] = (uint32_t)piece_id;
         }
     }
-    if (s < n) {
+    if (s < n && !(lpc_dbg & 1)) {
         const unsigned long long k = L.lkey[lane];
         const int32_t c = L.lcnt[lane];
         const int64_t o = (int64_t)P.slot * n, q = perm ? perm[s] : s;
@@ -470,6 +522,235 @@ __global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict
         P.root = I.node; P.slot = I.slot;
         trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
                     max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
+    }
+}
+
+// k_roots: the work queue's root items, one wave per packet (64 rays of the
+// coherence order), written into root shard (block % 8): one item per (packet,
+// piece) whose root test some ray of the packet passes -- the test a
+// k_intersect wave starts with, so the items are exactly the (packet, piece)
+// waves that would traverse.  Lanes take 64 pieces at a time and loop over the
+// packet's rays (read from LDS: broadcast), so the tests pipeline without a
+// ballot per test; one claim atomic per block and 64-piece chunk.
+__global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                               const Piece *__restrict__ pieces, int npieces, QueueArgs Q)
+{
+    __shared__ float s_ray[4][6][64];
+    __shared__ uint32_t s_cnt[4];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+    const bool live = w * 64 < n;
+    {
+        const int64_t s = w * 64 + lane;
+        f3 o = mk3(0.0f, 0.0f, 0.0f), d = mk3(0.0f, 0.0f, 1.0f);
+        if (live) load_ray(R, rs, n, s < n ? s : n - 1, o, d);
+        const float u = 1.0f / sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);   // as trav_packet
+        s_ray[wv][0][lane] = o.x; s_ray[wv][1][lane] = o.y; s_ray[wv][2][lane] = o.z;
+        s_ray[wv][3][lane] = d.x * u; s_ray[wv][4][lane] = d.y * u; s_ray[wv][5][lane] = d.z * u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int c0 = 0; c0 < npieces; c0 += 64) {
+        const int p = c0 + lane;
+        const Piece P = pieces[min(p, npieces - 1)];
+        bool pass = false;
+        if (live && p < npieces && P.root >= 0) {
+            for (int r = 0; r < 64; ++r) {
+                const float d = filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, s_ray[wv][0][r], s_ray[wv][1][r],
+                                            s_ray[wv][2][r], s_ray[wv][3][r], s_ray[wv][4][r], s_ray[wv][5][r]);
+                pass = pass || d <= 0.0f;
+            }
+        }
+        const uint64_t m = __builtin_amdgcn_ballot_w64(pass);
+        if (lane == 0) s_cnt[wv] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+            s_base = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(c), tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t off = s_base;
+        for (int k = 0; k < wv; ++k) off += s_cnt[k];
+        if (pass) {
+            const uint32_t pos = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+            if (pos < Q.rcap) Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)P.root, (uint32_t)P.slot);
+        }
+        __syncthreads();                         // s_cnt / s_base reused by the next chunk
+    }
+}
+
+// k_rootwalk: the root items (k_roots), grid-stride, one item per wave at a
+// time -- k_intersect's (packet, piece) waves without the waves whose root test
+// fails.  A wave that exceeds the hand-over budget queues its remaining
+// subtrees for k_spill (`out`), as k_intersect does.
+template <int W>
+__global__ __launch_bounds__(256, 6) void k_rootwalk(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                     const int32_t *__restrict__ perm,
+                                                     const NodeW<W> *__restrict__ nodes,
+                                                     const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
+                                                     unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
+                                                     unsigned long long *__restrict__ stats, QueueArgs Q,
+                                                     SpillArgs out)
+{
+    __shared__ WaveLds lds[4];
+    const int wv = threadIdx.x >> 6;
+    uint32_t pre[LPC_Q_CSHARDS + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int c = 0; c < LPC_Q_CSHARDS; ++c) pre[c + 1] = pre[c] + min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
+    const uint32_t stride = gridDim.x * 4u;
+    for (uint32_t i = blockIdx.x * 4u + (uint32_t)wv; i < pre[LPC_Q_CSHARDS]; i += stride) {
+        int c = 0;
+        while (i >= pre[c + 1]) ++c;
+        const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - pre[c])];
+        Piece P;
+        memset(&P, 0, sizeof(P));
+        P.root = (int32_t)q_node(it);
+        P.slot = (int32_t)q_slot(it);
+        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
+                       eps, max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
+    }
+}
+
+// k_trav: persistent traversal of the work queue, 4 waves per block, every wave
+// on its own.  Root phase: claim `batch` root items at a time, own root shard
+// first, then the others; before each further item of a batch, if waves of the
+// hand-over shard wait, hand the rest of the batch over instead.  Hand-over
+// phase: take a ticket on the shard's queue, wait for its slot, walk the item;
+// leave when no wave of the shard is in its root phase and no handed-over item
+// is unfinished (seen twice in a row), or give up after spin_max polls (sets
+// *err; the host reports it and re-empties the queue).  trav_packet hands the
+// bottom of its stack over while waves of its shard wait.
+template <int W>
+__global__ __launch_bounds__(256, 6) void k_trav(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                 const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
+                                                 const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
+                                                 unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
+                                                 unsigned long long *__restrict__ stats, QueueArgs Q)
+{
+    __shared__ WaveLds lds[4];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    Q.dshard = (int32_t)(blockIdx.x % LPC_Q_DSHARDS);
+    uint32_t *rbusy = Q.ctl + LPC_Q_RBUSY(Q.dshard);
+    unsigned long long *tp = (unsigned long long *)(Q.ctl + LPC_Q_TP(Q.dshard));
+    auto walk = [&](uint64_t it, uint64_t t_claim, uint32_t phase) {
+        Piece P;
+        memset(&P, 0, sizeof(P));
+        P.root = (int32_t)q_node(it);
+        P.slot = (int32_t)q_slot(it);
+        // profiling: one 8-word record per item (trav_packet writes words 0-3:
+        // walk ticks, nodes, exact tests, slot; then claim and walk start times,
+        // the wave's HW_ID and XCC_ID | phase << 8)
+        uint32_t *rec = nullptr;
+        if (Q.irec) {
+            uint32_t ix = 0;
+            if (lane == 0) ix = atomicAdd(Q.ctl + LPC_Q_IREC_N, 1u);
+            ix = (uint32_t)__builtin_amdgcn_readfirstlane((int)ix);
+            if (ix < Q.irec_cap) {
+                rec = Q.irec + 8 * (size_t)ix;
+                if (lane == 0) {
+                    rec[4] = (uint32_t)t_claim;
+                    rec[5] = (uint32_t)wall_clock64();
+                    rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+                    rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (phase << 8);
+                }
+            }
+        }
+        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
+                       eps, max_ray_len, skey, scnt, stats, rec, 0, SpillArgs{nullptr, nullptr, 0u, 0, 31},
+                       P.root, Q);
+    };
+    // root phase (the increment is performed before the first claim)
+    uint32_t r0 = 0;
+    if (lane == 0) r0 = atomicAdd(rbusy, 1u);
+    asm volatile("" ::"v"(r0));                 // wait for the returned value
+    uint32_t exhausted = 0;                     // root shards found empty
+    int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    bool root_phase = true;
+    uint64_t mine = 0;                          // claimed batch, one item per lane < cnt
+    int cnt = 0, next = 0;
+    uint32_t qt = 0, qh = 0;                    // the shard's counters, read one item ahead
+    uint32_t spins = 0;
+    // one walk site (two would double the code in the instruction cache)
+    for (;;) {
+        uint64_t it = LPC_QEMPTY, t_claim = 0;
+        uint32_t phase = 1;
+        if (root_phase) {
+            while (next >= cnt && exhausted != (1u << LPC_Q_CSHARDS) - 1u) {
+                if ((exhausted >> c) & 1u) { c = (c + 1) % LPC_Q_CSHARDS; continue; }
+                const uint32_t nr = min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
+                // look before claiming: every wave finding every shard empty by an
+                // atomic would serialise ~8 atomics per wave on 8 words at the end
+                const uint32_t seen =
+                    __hip_atomic_load(Q.ctl + LPC_Q_CHEAD(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane((int)(seen >= nr))) { exhausted |= 1u << c; continue; }
+                uint32_t t = 0;
+                if (lane == 0) t = atomicAdd(Q.ctl + LPC_Q_CHEAD(c), (uint32_t)Q.batch);
+                t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+                if (t >= nr) { exhausted |= 1u << c; continue; }
+                cnt = (int)min((uint32_t)Q.batch, nr - t);
+                next = 0;
+                mine = lane < cnt ? Q.roots[(size_t)c * Q.rcap + t + (uint32_t)lane] : 0ull;
+            }
+            if (next < cnt && next > 0) {
+                const int waiting = __builtin_amdgcn_readfirstlane((int)(qh - qt));
+                if (waiting > 0) {      // waves wait: hand the rest of the batch over
+                    const uint64_t rest = __shfl(mine, min(lane + next, 63), 64);
+                    next += q_publish(Q, cnt - next, rest);
+                }
+            }
+            if (next < cnt) {
+                it = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), next) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, next);
+                ++next;
+                if (next < cnt && Q.hunger) {
+                    qt = __hip_atomic_load(Q.ctl + LPC_Q_TP(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    qh = __hip_atomic_load(Q.ctl + LPC_Q_DHEAD(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (Q.irec) t_claim = wall_clock64();
+            } else {
+                root_phase = false;
+                if (lane == 0) atomicSub(rbusy, 1u);    // after this wave's publishes (returning atomics)
+                continue;
+            }
+        } else {
+            // hand-over phase: a ticket on the shard's queue, then its slot
+            phase = 2;
+            uint32_t tk = 0;
+            if (lane == 0) tk = atomicAdd(Q.ctl + LPC_Q_DHEAD(Q.dshard), 1u);
+            tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+            if (Q.irec) t_claim = wall_clock64();
+            uint64_t *slot = tk < Q.dcap ? Q.dq + (size_t)Q.dshard * Q.dcap + tk : nullptr;
+            int idle = 0;
+            for (uint32_t poll = 0;; ++poll) {
+                if (slot) {
+                    const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    it = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+                    if (it != LPC_QEMPTY) break;
+                }
+                if ((poll & 3u) == 3u) {
+                    // relaxed: an acquire would invalidate the CU's L1 under the
+                    // traversing waves; the exit needs the state seen twice, polls apart
+                    const uint32_t rb = __hip_atomic_load(rbusy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long v = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const bool done =
+                        __builtin_amdgcn_readfirstlane((int)(rb == 0u && (uint32_t)(v >> 32) == 0u)) != 0;
+                    idle = done ? idle + 1 : 0;
+                    if (idle >= 2) return;       // nothing left in this shard, nothing that could add to it
+                }
+                if (++spins > Q.spin_max) {
+                    if (lane == 0) atomicOr(Q.err, 1u);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (lane == 0) __hip_atomic_store(slot, LPC_QEMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        walk(it, t_claim, phase);
+        // a handed-over item is uncounted when finished (after its own publishes, which returned)
+        if (phase == 2 && lane == 0) atomicAdd(tp, (unsigned long long)(-(long long)(1ull << 32)));
     }
 }
 
@@ -691,8 +972,10 @@ __global__ __launch_bounds__(256) void k_gather(RaysIn R, int64_t n, const int32
 
 // k_gather from the 32-byte rows k_raykey wrote: one cache line per ray instead
 // of one per component (the permutation is random with respect to memory).
+// full: also the power and previous mesh (the rows' last two words, k_raykey),
+// so the copy is a whole population in coherence order (traced mode).
 __global__ __launch_bounds__(256) void k_gather_aos(const float4 *__restrict__ aos, int64_t n,
-                                                    const int32_t *__restrict__ perm, float *__restrict__ rs)
+                                                    const int32_t *__restrict__ perm, float *__restrict__ rs, int full)
 {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
@@ -700,6 +983,7 @@ __global__ __launch_bounds__(256) void k_gather_aos(const float4 *__restrict__ a
     const float4 a = aos[2 * q], b = aos[2 * q + 1];
     rs[s] = a.x; rs[n + s] = a.y; rs[2 * n + s] = a.z;
     rs[3 * n + s] = a.w; rs[4 * n + s] = b.x; rs[5 * n + s] = b.y;
+    if (full) { rs[6 * n + s] = b.z; rs[7 * n + s] = b.w; }
 }
 
 // Slot initial state: slots a run flushes into start at (max_ray_len, idx -1,
@@ -820,7 +1104,8 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     if (i >= n) return;
     if (aos) {          // the ray as one 32-byte row: k_gather_aos reads it with one line per ray
         aos[2 * i] = make_float4(R.ox[i], R.oy[i], R.oz[i], R.dx[i]);
-        aos[2 * i + 1] = make_float4(R.dy[i], R.dz[i], 0.0f, 0.0f);
+        aos[2 * i + 1] = make_float4(R.dy[i], R.dz[i], R.pw ? R.pw[i] : 0.0f,
+                                     R.pmid ? __int_as_float(R.pmid[i]) : 0.0f);
     }
     if (bb) {
         const float lo[3] = {ord_dec(bb[0]), ord_dec(bb[1]), ord_dec(bb[2])};
@@ -896,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_raykey16a(RaysIn R, int64_t n, float bx
     if (i < n) {
         const float ox = R.ox[i], oy = R.oy[i], oz = R.oz[i], dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
         aos[2 * i] = make_float4(ox, oy, oz, dx);
-        aos[2 * i + 1] = make_float4(dy, dz, 0.0f, 0.0f);
+        aos[2 * i + 1] = make_float4(dy, dz, R.pw ? R.pw[i] : 0.0f, R.pmid ? __int_as_float(R.pmid[i]) : 0.0f);
         vo = va = ray_morton5(ox, oy, oz, dx, dy, dz, bx0, by0, bz0, sx, sy, sz);
     }
     for (int o = 32; o >= 1; o >>= 1) {

@@ -147,6 +147,20 @@ struct lpc_handle {
     int64_t sliver_ppw = 0;                         // k_slivers: packets per wave (0: from sliver_waves)
     int sliver_rays = 128;                          // k_slivers packet size (64 or 128 rays)
     DBuf w_spill;                                   // k_spill queue
+    // work queue (k_roots + persistent k_trav) instead of k_intersect + k_spill
+    bool traced = true;                             // LPC_TRACED: aggregate iterations in coherence order
+    bool traced_resort = false;                     // LPC_TRACED_SORT: sort the children again
+    bool pop_traced = false;                        // the population is in its parents' traced order
+    int queue = 2;                                  // LPC_QUEUE: 0 k_intersect, 1 persistent k_trav, 2 k_rootwalk
+    int64_t q_walk_blocks = 4096;                   // k_rootwalk grid (4 waves each, grid-stride)
+    int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
+    int q_batch = 2;                                // root items per claim
+    int q_hunger = 1;                               // hand work over to waiting waves
+    int64_t q_blocks = 0;                           // k_trav grid (0: CUs x resident blocks per CU)
+    int q_per_cu = 6;                               // ... at most this many per CU
+    int64_t q_dcap = 1 << 16;                       // hand-over slots per shard
+    int64_t q_spin = 1 << 22;                       // polls before a waiting wave gives up
+    DBuf w_qroots, d_qdq;                           // root items, hand-over slots (kept LPC_QEMPTY)
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     // trace
@@ -162,7 +176,7 @@ struct lpc_handle {
     DBuf d_wrec;                                    // per-wave records of the last k_intersect (level 3)
     int64_t wrec_count = 0;
     // profiling
-    bool prof = false, prof_stats = false, prof_waves = false, prof_light = false;
+    bool prof = false, prof_stats = false, prof_waves = false, prof_light = false, prof_items = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
@@ -659,7 +673,7 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         const int64_t C = n;
         RETIF(dalloc(h, h->w_key, (size_t)h->K * C * 8));
         RETIF(dalloc(h, h->w_sc, (size_t)h->K * C * 4));
-        RETIF(dalloc(h, h->w_rs, (size_t)6 * C * 4));
+        RETIF(dalloc(h, h->w_rs, (size_t)8 * C * 4));
         RETIF(dalloc(h, h->w_pk, (size_t)((C + 127) / 128) * sizeof(PacketRec)));
         RETIF(dalloc(h, h->w_pk64, (size_t)((C + 63) / 64) * sizeof(PacketRec)));
         RETIF(dalloc(h, h->d_misc, LPC_MISC_WORDS * 4));
@@ -746,13 +760,182 @@ static void prof_resolve(lpc_handle *h)
     h->ev_rest.clear();
 }
 
+// Work hand-over (k_spill levels): queue, budget by population size.
+static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
+{
+    *SP = SpillArgs{nullptr, nullptr, 0u, 0, 31};
+    if (h->spill_budget <= 0) return 0;
+    RETIF(dalloc(h, h->w_spill, (size_t)2 * h->spill_cap * sizeof(SpillItem)));
+    SP->items = (SpillItem *)h->w_spill.p;
+    SP->ctr = (uint32_t *)h->d_misc.p + LPC_MISC_SPILL;
+    SP->cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
+    const int64_t large_n = h->spill_large_n > 0 ? h->spill_large_n : h->spill_large_per_tri * (int64_t)h->M;
+    SP->budget = n >= large_n ? h->spill_budget_large : h->spill_budget;
+    SP->pair_shift = h->spill_pair_shift;
+    return 0;
+}
+
+// hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
+// what exceeds the budget for level l + 1; the last level finishes
+static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
+                            float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
+                            unsigned long long *stats, const SpillArgs &SP)
+{
+    uint32_t *misc = (uint32_t *)h->d_misc.p;
+    const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
+    const int levels = SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
+    for (int l = 0; l < levels; ++l) {
+        SpillArgs I = SP, O = SP;
+        I.items = (SpillItem *)h->w_spill.p + (size_t)(l % 2) * (size_t)h->spill_cap;
+        I.ctr = misc + LPC_MISC_SPILL + l;
+        O.items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
+        O.ctr = misc + LPC_MISC_SPILL + l + 1;
+        O.budget = l + 1 < levels ? SP.budget : 0;
+        // later levels hold fewer items (and often none): smaller grids
+        const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
+        if (h->built_w == 8)
+            hipLaunchKernelGGL(k_spill<8>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
+                               perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
+                               max_ray_len, skey, scnt, stats, I, O);
+        else
+            hipLaunchKernelGGL(k_spill<4>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
+                               perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
+                               max_ray_len, skey, scnt, stats, I, O);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+// Piece level of the work queue: pieces per run so that (packets x pieces) root
+// tests reach q_target (mesh run roots for large populations, finer pieces for
+// small ones, whose few packets would otherwise be few items).
+static int32_t q_level(const lpc_handle *h, int64_t n)
+{
+    int64_t live_runs = 0;
+    for (int32_t j = 0; j < h->K; ++j) live_runs += h->slot_run[(size_t)j] >= 0;
+    live_runs = std::max<int64_t>(live_runs, 1);
+    const int64_t npk = (n + 63) / 64;
+    return (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (h->q_target + npk * live_runs - 1) /
+                                                                      (npk * live_runs)));
+}
+
+// k_trav grid: every block resident at once (CUs x blocks per CU from the
+// occupancy query) unless LPC_Q_BLOCKS says otherwise.  Correctness does not
+// depend on residency (a block that starts late finds no root item left).
+template <int W>
+static int q_grid(lpc_handle *h, unsigned *grid)
+{
+    if (h->q_blocks > 0) { *grid = (unsigned)h->q_blocks; return 0; }
+    int per_cu = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trav<W>, 256, 0));
+    // the hardware admits fewer 256-thread blocks than the API says when the
+    // kernel uses ~100 SGPRs (MI355X_MICROARCH.md, residency): k_trav's launch
+    // bounds ask for 6 per CU; a block that is not resident starts only when
+    // another exits, at the end of the launch
+    per_cu = std::min(per_cu, h->q_per_cu);
+    *grid = (unsigned)std::max(1, per_cu) * (unsigned)std::max(1, h->cus);
+    return 0;
+}
+
+// A k_trav wave gave up waiting (QueueArgs::err, kept in DevAcc::qerr): the
+// launch's results are incomplete.  Re-empty the hand-over slots, clear the flag
+// and report.  Never expected; the bound only keeps a logic error from hanging
+// the GPU.
+static int q_failed(lpc_handle *h)
+{
+    (void)hipStreamSynchronize(h->stream);
+    if (h->d_qdq.p) (void)hipMemset(h->d_qdq.p, 0xff, h->d_qdq.bytes);
+    (void)hipMemset((char *)h->d_acc.p + offsetof(DevAcc, qerr), 0, sizeof(uint32_t));
+    return set_err(h, LPC_E_HIP, "intersect work queue: a wave gave up waiting (results incomplete)");
+}
+
+static int check_qerr(lpc_handle *h)
+{
+    uint32_t e = 0;
+    HIPCHK(h, hipMemcpy(&e, (char *)h->d_acc.p + offsetof(DevAcc, qerr), sizeof(e), hipMemcpyDeviceToHost));
+    return e ? q_failed(h) : 0;
+}
+
+// The work-queue form of the hierarchy stage: k_roots writes the (packet, piece)
+// items whose root test passes, the persistent k_trav walks them.
+static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
+                     const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
+                     unsigned long long *stats)
+{
+    const int64_t npk = (n + 63) / 64;
+    const int64_t rblocks = (npk + 3) / 4;
+    const int64_t rcap = ((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces;
+    if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "work queue: too many root items per shard");
+    RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
+    const size_t dq_bytes = (size_t)LPC_Q_DSHARDS * (size_t)h->q_dcap * 8;
+    if (h->d_qdq.bytes < dq_bytes) {
+        RETIF(dalloc(h, h->d_qdq, dq_bytes));
+        HIPCHK(h, hipMemsetAsync(h->d_qdq.p, 0xff, h->d_qdq.bytes, h->stream));
+    }
+    QueueArgs Q;
+    Q.roots = (uint64_t *)h->w_qroots.p;
+    Q.dq = (uint64_t *)h->d_qdq.p;
+    Q.ctl = (uint32_t *)h->d_misc.p;
+    Q.err = (uint32_t *)((char *)h->d_acc.p + offsetof(DevAcc, qerr));
+    Q.rcap = (uint32_t)rcap;
+    Q.dcap = (uint32_t)(h->d_qdq.bytes / 8 / LPC_Q_DSHARDS);
+    Q.spin_max = (uint32_t)h->q_spin;
+    Q.batch = h->q_batch;
+    Q.hunger = h->q_hunger;
+    Q.dshard = -1;
+    Q.irec = nullptr;
+    Q.irec_cap = 0;
+    if (h->prof_items) {              // per-item records of this launch (the last one is kept)
+        const int64_t cap = (int64_t)1 << 21;
+        RETIF(dalloc(h, h->d_wrec, (size_t)cap * 32));
+        HIPCHK(h, hipMemsetAsync(h->d_wrec.p, 0, (size_t)cap * 32, h->stream));
+        h->wrec_count = 2 * cap;      // lpc_prof_waves hands them out as 4-word halves
+        Q.irec = (uint32_t *)h->d_wrec.p;
+        Q.irec_cap = (uint32_t)cap;
+    }
+    hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
+                       (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
+    hipEvent_t k0 = nullptr, k1 = nullptr;
+    if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
+        SpillArgs SP;
+        RETIF(spill_setup(h, n, &SP));
+        const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks);
+        if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
+        if (h->built_w == 8)
+            hipLaunchKernelGGL(k_rootwalk<8>, dim3(grid), dim3(256), 0, h->stream, in, rs, n, perm,
+                               (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
+                               scnt, stats, Q, SP);
+        else
+            hipLaunchKernelGGL(k_rootwalk<4>, dim3(grid), dim3(256), 0, h->stream, in, rs, n, perm,
+                               (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
+                               scnt, stats, Q, SP);
+        if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
+        return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP);
+    }
+    unsigned grid = 0;
+    if (h->built_w == 8) RETIF(q_grid<8>(h, &grid));
+    else RETIF(q_grid<4>(h, &grid));
+    if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
+    if (h->built_w == 8)
+        hipLaunchKernelGGL(k_trav<8>, dim3(grid), dim3(256), 0, h->stream, in, rs, n, perm,
+                           (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
+                           stats, Q);
+    else
+        hipLaunchKernelGGL(k_trav<4>, dim3(grid), dim3(256), 0, h->stream, in, rs, n, perm,
+                           (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
+                           stats, Q);
+    if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
 // intersect for n rays of `in` into the slot arrays, and optionally into a
 // caller's [ray][mesh] buffers (st_user != NULL, the reference's scratch layout).
 // split: rows [0, split) of `in` are a population's reflected block (key class
 // bit, k_raykey); INT64_MAX when the rows are not a trace population.
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
                          float *st_user, int32_t *si_user, int32_t *sc_user, int64_t split = INT64_MAX,
-                         double dmax2 = INFINITY)
+                         double dmax2 = INFINITY, RaysIn *traced = nullptr)
 {
     RETIF(ensure_ws(h, n));
     PieceTable *pt;
@@ -767,9 +950,14 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     SI.acc = h->acc_pending ? (DevAcc *)h->d_acc.p : nullptr;
     SI.m_total = (unsigned long long)h->acc_pending_total;
     h->acc_pending = false;
-    const bool sorted = h->sort_rays && n >= h->sort_min;
+    // traced mode (trace_iterate without per-ray exports): the slots, shading and
+    // compaction work in the launch's coherence order, so the children come out
+    // in their parents' traced order and need no sort of their own (unless
+    // LPC_TRACED_SORT); *traced receives the rays in that order
+    const bool chained_pop = traced && h->pop_traced && !h->traced_resort;
+    const bool sorted = h->sort_rays && n >= h->sort_min && !chained_pop;
     // the slot reset rides on k_raykey when it runs before everything that reads misc
-    const bool fold_init = sorted && h->sort_mode == 1 &&
+    const bool fold_init = sorted && h->sort_mode == 1 && n >= LPC_MISC_WORDS &&
                            !(h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX)) &&
                            !(h->order_ready && n == h->order_n);
     if (!fold_init)
@@ -779,7 +967,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (!fold_init) SIk.skey = nullptr;
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
-    const bool chained = h->order_ready && n == h->order_n;
+    const bool chained = !traced && h->order_ready && n == h->order_n;
     h->order_ready = false;
     if (chained) {                      // the previous iteration wrote this order (k_oscatter)
         perm = (const int32_t *)h->w_perm2[h->order_buf].p;
@@ -814,7 +1002,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                                               0, 16, h->stream));
             perm = vout;
             hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
-                               perm, (float *)h->w_rs.p);
+                               perm, (float *)h->w_rs.p, traced ? 1 : 0);
             rs = (const float *)h->w_rs.p;
         } else {
         if (pop_box)
@@ -824,7 +1012,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                            h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
                            (h->key_mode == 3 || h->key_mode == 4) ? 1 : 0, kin, vin,
-                           h->gather_aos ? (float4 *)h->w_aos.p : nullptr, SIk);
+                           (h->gather_aos || traced) ? (float4 *)h->w_aos.p : nullptr, SIk);
         size_t tb = h->sort_tmp_bytes;
         if (n >= h->onesweep_min)       // large populations: onesweep (4 digit passes)
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
@@ -833,19 +1021,44 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, 0,
                                                             32, h->stream));
         perm = vout;
-        if (h->gather_aos)
+        if (h->gather_aos || traced)
             hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
-                               perm, (float *)h->w_rs.p);
+                               perm, (float *)h->w_rs.p, traced ? 1 : 0);
         else
             hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
         rs = (const float *)h->w_rs.p;
         }
+    }
+    if (traced) {
+        // positions of the coherence order are the rays' indices from here on
+        if (rs) {
+            const float *f = rs;
+            RaysIn t;
+            t.ox = f; t.oy = f + n; t.oz = f + 2 * n; t.dx = f + 3 * n; t.dy = f + 4 * n; t.dz = f + 5 * n;
+            t.pw = f + 6 * n; t.pmid = (const int32_t *)(f + 7 * n);
+            *traced = t;
+        } else {
+            *traced = in;
+        }
+        perm = nullptr;
     }
     h->last_perm = perm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
     const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
+    // work queue (default): needs no fan groups and the item encoding's bounds
+    bool qpath = false;
+    if (h->queue && !h->prof_waves && !lane_path) {
+        PieceTable *ptq;
+        RETIF(piece_table(h, n, &ptq, q_level(h, n)));
+        qpath = ptq->gmax == 0 && (n + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
+                (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES && h->K <= LPC_Q_MAX_SLOTS;
+        if (qpath) {
+            pt = ptq;                   // same sliver pieces at every level
+            if (pt->npieces > 0) RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats));
+        }
+    }
     if (pt->npieces > 0 && lane_path) {
         // incoherent (small) populations: one ray per lane, threaded traversal
         PieceTable *pl;
@@ -855,7 +1068,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                            (const Piece *)pl->pieces.p, eps, max_ray_len, skey, scnt);
         HIPCHK(h, hipGetLastError());
     }
-    if (pt->npieces > 0 && !lane_path) {
+    if (pt->npieces > 0 && !lane_path && !qpath) {
         uint32_t *wrec = nullptr;
         if (h->prof_waves) {
             h->wrec_count = (int64_t)pt->npieces * ((n + 63) / 64);
@@ -875,15 +1088,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         }
         // work hand-over (not with fan groups: a k_spill item has no group slots)
         SpillArgs SP{nullptr, nullptr, 0u, 0, 31};
-        if (h->spill_budget > 0 && gmax == 0 && !wrec) {
-            RETIF(dalloc(h, h->w_spill, (size_t)2 * h->spill_cap * sizeof(SpillItem)));
-            SP.items = (SpillItem *)h->w_spill.p;
-            SP.ctr = misc + LPC_MISC_SPILL;
-            SP.cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
-            const int64_t large_n = h->spill_large_n > 0 ? h->spill_large_n : h->spill_large_per_tri * (int64_t)h->M;
-            SP.budget = n >= large_n ? h->spill_budget_large : h->spill_budget;
-            SP.pair_shift = h->spill_pair_shift;
-        }
+        if (gmax == 0 && !wrec) RETIF(spill_setup(h, n, &SP));
         // pieces per wave: all of them (LPC_LOOP) or enough that the grid has
         // about wave_target waves
         const int64_t bxw = (n + 255) / 256;
@@ -911,28 +1116,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         }
 #undef LPC_LAUNCH_ISECT
         if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
-        // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and
-        // queues what exceeds the budget for level l + 1; the last level finishes
-        const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
-        const int levels = SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
-        for (int l = 0; l < levels; ++l) {
-            SpillArgs I = SP, O = SP;
-            I.items = (SpillItem *)h->w_spill.p + (size_t)(l % 2) * (size_t)h->spill_cap;
-            I.ctr = misc + LPC_MISC_SPILL + l;
-            O.items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
-            O.ctr = misc + LPC_MISC_SPILL + l + 1;
-            O.budget = l + 1 < levels ? SP.budget : 0;
-            // later levels hold fewer items (and often none): smaller grids
-            const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
-            if (h->built_w == 8)
-                hipLaunchKernelGGL(k_spill<8>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
-                                   perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
-                                   max_ray_len, skey, scnt, stats, I, O);
-            else
-                hipLaunchKernelGGL(k_spill<4>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
-                                   perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
-                                   max_ray_len, skey, scnt, stats, I, O);
-        }
+        RETIF(run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP));
         if (gmax > 0) {
             hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
                                (PacketRec *)h->w_pk64.p);
@@ -1104,6 +1288,21 @@ int lpc_open(int device, lpc_handle **out)
     h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
     h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
     h->sliver_rays = env_int("LPC_SLIVER_RAYS", h->sliver_rays) == 64 ? 64 : 128;
+    h->queue = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_QUEUE", h->queue)));
+    h->traced = env_int("LPC_TRACED", h->traced) != 0;
+    h->traced_resort = env_int("LPC_TRACED_SORT", h->traced_resort) != 0;
+    h->q_walk_blocks = env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks);
+    {
+        const int dbg = (int)env_int("LPC_DBG", 0);
+        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
+    }
+    h->q_target = std::max<int64_t>(1, env_int("LPC_Q_TARGET", h->q_target));
+    h->q_batch = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_int("LPC_Q_BATCH", h->q_batch)));
+    h->q_hunger = env_int("LPC_Q_HUNGER", h->q_hunger) != 0;
+    h->q_blocks = std::max<int64_t>(0, env_int("LPC_Q_BLOCKS", h->q_blocks));
+    h->q_per_cu = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_int("LPC_Q_PER_CU", h->q_per_cu)));
+    h->q_dcap = std::min<int64_t>((int64_t)1 << 26, std::max<int64_t>(64, env_int("LPC_Q_DCAP", h->q_dcap)));
+    h->q_spin = std::min<int64_t>(0xffffffffLL, std::max<int64_t>(1024, env_int("LPC_Q_SPIN", h->q_spin)));
     if (hipHostMalloc((void **)&h->acc_host, sizeof(DevAcc), hipHostMallocDefault) != hipSuccess) {
         g_open_err = "pinned host buffer";
         lpc_close(h);
@@ -1122,7 +1321,7 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_qroots, &h->d_qdq, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
                     &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1]};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
@@ -1312,6 +1511,7 @@ int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float 
         ShadeOutPtrs o = shade_ptrs(h, true);
         hipError_t e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) { rc = set_err(h, LPC_E_HIP, std::string("bounce: ") + hipGetErrorString(e)); break; }
+        if ((rc = check_qerr(h)) != 0) break;
         auto d2h = [&](void *dst, const void *src, size_t bytes) {
             if (!rc && dst && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
                 rc = set_err(h, LPC_E_HIP, "bounce: D2H");
@@ -1371,6 +1571,7 @@ int lpc_intersect(lpc_handle *h, int64_t n, const float *dev_origin4, const floa
                             dev_cnt + base * h->K));
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    RETIF(check_qerr(h));
     if (h->prof) prof_resolve(h);
     return 0;
 }
@@ -1486,6 +1687,7 @@ int lpc_trace_reset(lpc_handle *h)
         hipLaunchKernelGGL(k_copy_pop, dim3((unsigned)std::min<int64_t>(grid1(h->n_init), 8192)), dim3(256), 0,
                            h->stream, h->A.out(), h->I.in(0), h->n_init);
     h->n_cur = h->n_init;
+    h->pop_traced = false;
     h->order_ready = h->order_pending = false;
     h->split = INT64_MAX;                       // emitted rays: one class
     h->pop_dmax2 = h->init_dmax2;
@@ -1568,11 +1770,18 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     }
     const size_t mc = (size_t)h->m_cap;
     float *mf = (float *)h->m_buf.p;
+    // traced mode: one chunk, no per-ray export (the population then comes out in
+    // its parents' coherence order; measured rays per iteration likewise)
+    const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow;
+    const bool traced = h->traced && C >= N && !exports && !h->order_chain;
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
-        const RaysIn in = h->A.in(base);
+        RaysIn in = h->A.in(base);
         const int64_t split = h->split == INT64_MAX ? INT64_MAX : std::max<int64_t>(0, h->split - base);
-        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2));
+        RaysIn tin;
+        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2,
+                            traced ? &tin : nullptr));
+        if (traced) in = tin;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
         ShadeOutPtrs o = shade_ptrs(h, false);
@@ -1648,6 +1857,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     HIPCHK(h, hipMemcpyAsync(h->acc_host, h->d_acc.p, sizeof(DevAcc), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     DevAcc acc = *h->acc_host;
+    if (acc.qerr) return q_failed(h);
     const int64_t nR = (int64_t)acc.nR, nT = (int64_t)acc.nT;
     if (out_next_pow && nR + nT > 0) {
         HIPCHK(h, hipMemcpyAsync(out_next_pow, h->B.f(6), (size_t)(nR + nT) * 4, hipMemcpyDeviceToHost, h->stream));
@@ -1655,6 +1865,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     }
     if (h->prof) prof_resolve(h);
     std::swap(h->A, h->B);
+    h->pop_traced = traced;
     h->n_cur = nR + nT;
     h->order_ready = h->order_pending;
     h->order_pending = false;
@@ -1790,6 +2001,7 @@ int lpc_prof_enable(lpc_handle *h, int on)
     h->prof_stats = on == 2;
     h->prof_waves = on == 3;
     h->prof_light = on == 4;                        // k_intersect events only (bench timed region)
+    h->prof_items = on == 5;                        // k_trav per-item records (lpc_prof_waves, 8 words each)
     if (h->prof_stats && !h->d_stats.p) {
         RETIF(dalloc(h, h->d_stats, LPC_STATS_WORDS * 8));
         HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));

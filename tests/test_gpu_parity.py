@@ -71,21 +71,37 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
     _cmp_bounce(g2, r2, diss)
 
 
-@pytest.mark.parametrize("cfg", [dict(LPC_FLAT="0"), dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"),
-                                 dict(LPC_FLAT="20", LPC_KEY="2"), dict(LPC_KEY="3"), dict(LPC_KEY="1"),
-                                 dict(LPC_SORT="0"), dict(LPC_SORT="2"), dict(LPC_GATHER_AOS="0"), dict(LPC_WAVE_TARGET="2000"), dict(LPC_WAVE_TARGET="0"), dict(LPC_SLIVER_CULL="0"), dict(LPC_ISECT_MINB="1"), dict(LPC_FUSE_SHADE="1"), dict(LPC_XCD_ROWS="1"), dict(LPC_CHAIN="1"), dict(LPC_XCD_ROWS="1", LPC_WAVE_TARGET="0"), dict(LPC_LANE_MAX="100000000"), dict(LPC_LANE_MAX="100000000", LPC_LANE_G="8"), dict(LPC_BUDGET="0"), dict(LPC_BUDGET="4"),
-                                 dict(LPC_BUDGET="6", LPC_SPILL_CAP="100"),
-                                 dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
-                                 dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"), dict(LPC_LOOP="1", LPC_LOOP_MIN="1"),
-                                 dict(LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1"),
-                                 dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_SLIVER_RAYS="64"), dict(LPC_NODE_W="4"),
-                                 dict(LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536"),
-                                 dict(LPC_LARGE_N="1000"), dict(LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3")])
+_OLD = dict(LPC_QUEUE="0")          # k_intersect + k_spill levels instead of the work queue
+_POLICIES = [
+    # both paths
+    dict(LPC_FLAT="0"), dict(LPC_KEY="3"), dict(LPC_KEY="1"), dict(LPC_SORT="0"), dict(LPC_SORT="2"),
+    dict(LPC_GATHER_AOS="0"), dict(LPC_SLIVER_CULL="0"), dict(LPC_FUSE_SHADE="1"), dict(LPC_CHAIN="1"),
+    dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_SLIVER_RAYS="64"), dict(LPC_NODE_W="4"),
+    # work queue (k_roots + k_trav): claim batch, piece level, hand-over queue that
+    # overflows, grids of one block, of a few blocks and far beyond residency
+    dict(LPC_Q_BATCH="1"), dict(LPC_Q_BATCH="7"), dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"),
+    dict(LPC_Q_DCAP="64"), dict(LPC_Q_BLOCKS="1"), dict(LPC_Q_BLOCKS="3", LPC_Q_DCAP="64"),
+    dict(LPC_Q_BLOCKS="20000"), dict(LPC_Q_BLOCKS="37", LPC_Q_BATCH="3", LPC_NODE_W="4"),
+    # fan groups fall back to k_intersect
+    dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"), dict(LPC_FLAT="20", LPC_KEY="2"),
+    # the k_intersect path's own knobs
+    dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"), dict(_OLD, LPC_ISECT_MINB="1"),
+    dict(_OLD, LPC_XCD_ROWS="1"), dict(_OLD, LPC_XCD_ROWS="1", LPC_WAVE_TARGET="0"),
+    dict(LPC_LANE_MAX="100000000"), dict(LPC_LANE_MAX="100000000", LPC_LANE_G="8"),
+    dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="4"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
+    dict(_OLD, LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
+    dict(_OLD, LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"),
+    dict(_OLD, LPC_LOOP="1", LPC_LOOP_MIN="1"), dict(_OLD, LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1"),
+    dict(_OLD, LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536"),
+    dict(_OLD, LPC_LARGE_N="1000"), dict(_OLD, LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3"),
+]
+
+
+@pytest.mark.parametrize("cfg", _POLICIES)
 def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
-    """The launch policies (fan-group threshold, piece granularity, coherence
-    key, no sort, work hand-over budget incl. a queue that overflows, the
-    population-size budget switch) change
-    only speed."""
+    """The launch policies (work queue or k_intersect, fan-group threshold,
+    piece granularity, coherence key, no sort, hand-over budgets and queues
+    that overflow, grid sizes) change only speed."""
     from lightpycl_amd.engine import Engine
     for k, v in cfg.items():
         monkeypatch.setenv(k, v)
@@ -143,8 +159,14 @@ def test_aggregate_mode_and_histogram(oracle_mod, name, n):
     assert tr.iteration_counts == info["counts"]
     pos, pwr = tr.get_measured_rays()
     rpos, rpwr = oracle_mod.measured_rays(ref)
-    np.testing.assert_array_equal(pos[:, :3], rpos[:, :3])          # same order: iteration, then ray
-    np.testing.assert_array_equal(pwr, np.asarray(rpwr).reshape(-1))
+    # aggregate mode keeps each iteration's rays in the launch's coherence order
+    # (DESIGN.md "traced order"): the same measured rays, bit for bit, as a set
+    rpwr = np.asarray(rpwr).reshape(-1)
+
+    def rows(p, w):
+        r = np.concatenate([p[:, :3], w.reshape(-1, 1)], axis=1)
+        return r[np.lexsort(r.T[::-1])]
+    np.testing.assert_array_equal(rows(pos, pwr), rows(np.asarray(rpos), rpwr))
     np.testing.assert_allclose(tr.measured_power(), info["mesh_power"], rtol=1e-12)
     H, xe, ye = tr.get_binned_data_angular(limits=sc.hist_limits, points=sc.hist_points)
     Hr, xr, yr = oracle_mod.binned_angular(rpos, rpwr, limits=sc.hist_limits, points=sc.hist_points)
