@@ -32,6 +32,8 @@ FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector (packed) peak
 RAY_BYTES = 156                # algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # per triangle per bounce-iteration
 MT_FLOPS = 46                  # Moller-Trumbore flops per ray-triangle test
+# the hierarchy-traversal kernel timed for the roofline, by LPC_QUEUE launch policy
+HIER_KERNEL = {"0": "k_intersect", "1": "k_trav", "2": "k_rootwalk"}
 
 
 def parse():
@@ -46,7 +48,7 @@ def parse():
 
 
 def load_pmc_traffic():
-    """HBM bytes per k_intersect launch from the committed rocprofv3 --pmc summary
+    """HBM bytes per launch of the hierarchy kernel from the committed rocprofv3 --pmc summary
     (profiles/pmc_intersect.json, written by tools/pmc_summary.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_intersect.json")
     if os.path.exists(p):
@@ -124,7 +126,7 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    eng.prof_enable(True, light=True)        # HIP events around the k_intersect launches only
+    eng.prof_enable(True, light=True)        # HIP events around the hierarchy kernel launches only
     eng.prof_read(reset=True)
     sync()
     t0 = time.perf_counter()
@@ -153,7 +155,8 @@ def main():
 
     M = eng.tri_count
     launches = max(prof["intersect_launches"], 1)
-    avg_ms = prof["kernel_ms"] / launches               # k_intersect launches alone
+    avg_ms = prof["kernel_ms"] / launches               # the hierarchy kernel's launches alone
+    kernel = HIER_KERNEL.get(os.environ.get("LPC_QUEUE", "2"), "k_rootwalk")
     rays_per_launch = bounces / launches                 # rank-0 launches
     alg_bytes = rays_per_launch * RAY_BYTES + M * TRI_BYTES
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
@@ -179,11 +182,11 @@ def main():
                    "parallelism": f"ray-sharded x{world}", "iterations_per_step": iters / a.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_intersect", "avg_launch_ms": avg_ms,
+                     "kernel": kernel, "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "note": "achieved = algorithmic bytes per launch / k_intersect's own average "
-                             "launch time (HIP events); traffic = 2*FETCH_SIZE+WRITE_SIZE per "
-                             "k_intersect launch (profiles/pmc_intersect.json)"},
+                     "note": f"achieved = algorithmic bytes per launch / {kernel}'s own average "
+                             "launch time (HIP events on its stream); traffic = 2*FETCH_SIZE+WRITE_SIZE per "
+                             f"{kernel} launch (profiles/pmc_intersect.json)"},
         "roofline_valu": {"bound": "valu", "kernel": "whole trace",
                           "achieved": mt_tflops, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": mt_tflops / FP32_PEAK_TFLOPS,

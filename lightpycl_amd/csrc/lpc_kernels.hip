@@ -580,6 +580,47 @@ __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict
     }
 }
 
+// k_roots for few pieces (<= 64): lanes are the packet's rays and the wave
+// loops over the pieces (one test and a ballot each); lane-per-piece would
+// leave most lanes idle through 64 ray iterations.  Same tests, same items.
+__global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                 const Piece *__restrict__ pieces, int npieces, QueueArgs Q)
+{
+    __shared__ uint32_t s_cnt[4];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+    const bool live = w * 64 < n;
+    const int64_t s = w * 64 + lane;
+    f3 O = mk3(0.0f, 0.0f, 0.0f), D = mk3(0.0f, 0.0f, 1.0f);
+    if (live) load_ray(R, rs, n, s < n ? s : n - 1, O, D);
+    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);   // as trav_packet
+    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+    const Piece Pl = pieces[min(lane, npieces - 1)];
+    uint64_t m = 0;
+    if (live)
+        for (int p = 0; p < npieces; ++p) {
+            if (bcasti(Pl.root, p) < 0) continue;
+            const float d = filter_test(bcast(Pl.cx, p), bcast(Pl.cy, p), bcast(Pl.cz, p), bcast(Pl.negB, p),
+                                        bcast(Pl.negA, p), O.x, O.y, O.z, nx, ny, nz);
+            if (any_lane(d <= 0.0f)) m |= 1ull << p;
+        }
+    if (lane == 0) s_cnt[wv] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        s_base = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(c), tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t off = s_base;
+    for (int k = 0; k < wv; ++k) off += s_cnt[k];
+    if ((m >> lane) & 1ull) {
+        const uint32_t pos = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (pos < Q.rcap) Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)Pl.root, (uint32_t)Pl.slot);
+    }
+}
+
 // k_rootwalk: the root items (k_roots), grid-stride, one item per wave at a
 // time -- k_intersect's (packet, piece) waves without the waves whose root test
 // fails.  A wave that exceeds the hand-over budget queues its remaining

@@ -151,8 +151,10 @@ struct lpc_handle {
     bool traced = true;                             // LPC_TRACED: aggregate iterations in coherence order
     bool traced_resort = false;                     // LPC_TRACED_SORT: sort the children again
     bool pop_traced = false;                        // the population is in its parents' traced order
+    bool pop_emitted = false;                       // the population is the emitted rays (set_rays)
+    int init_key_lo = 0, init_key_hi = 32;          // key bits that vary over the emitted rays (set_rays)
     int queue = 2;                                  // LPC_QUEUE: 0 k_intersect, 1 persistent k_trav, 2 k_rootwalk
-    int64_t q_walk_blocks = 4096;                   // k_rootwalk grid (4 waves each, grid-stride)
+    int64_t q_walk_blocks = 8192;                   // k_rootwalk grid (4 waves each, grid-stride)
     int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
     int q_batch = 2;                                // root items per claim
     int q_hunger = 1;                               // hand work over to waiting waves
@@ -893,8 +895,12 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         Q.irec = (uint32_t *)h->d_wrec.p;
         Q.irec_cap = (uint32_t)cap;
     }
-    hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
-                       (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
+    if (pt->npieces <= 64)
+        hipLaunchKernelGGL(k_roots_r, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
+                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
+    else
+        hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
+                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
         SpillArgs SP;
@@ -1014,12 +1020,15 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                            (h->key_mode == 3 || h->key_mode == 4) ? 1 : 0, kin, vin,
                            (h->gather_aos || traced) ? (float4 *)h->w_aos.p : nullptr, SIk);
         size_t tb = h->sort_tmp_bytes;
-        if (n >= h->onesweep_min)       // large populations: onesweep (4 digit passes)
+        // the emitted rays' varying key bits (set_rays) under key mode 0
+        int b0 = 0, b1 = 32;
+        if (traced && h->pop_emitted && h->key_mode == 0 && !cls) { b0 = h->init_key_lo; b1 = h->init_key_hi; }
+        if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
-                                                              0, 32, h->stream));
+                                                              b0, b1, h->stream));
         else
-            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, 0,
-                                                            32, h->stream));
+            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, b0,
+                                                            b1, h->stream));
         perm = vout;
         if (h->gather_aos || traced)
             hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
@@ -1667,6 +1676,22 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->init_dmax2 = host_dmax2(n, dir4);
+    {   // coherence key bits that can vary over these rays (k_raykey, key mode 0:
+        // [class | origin cell 15 | direction 16]): a point source has one origin
+        // cell, a collimated beam one direction, and the sort skips the rest
+        bool same_o = true, same_d = true;
+        for (int64_t i = 1; i < n && (same_o || same_d); ++i) {
+            for (int k = 0; k < 3; ++k) {
+                if (origin4[4 * i + k] != origin4[k]) same_o = false;
+                if (dir4[4 * i + k] != dir4[k]) same_d = false;
+            }
+        }
+        h->init_key_lo = 0;
+        h->init_key_hi = 31;
+        if (same_o) h->init_key_hi = 16;
+        if (same_d) h->init_key_lo = 16;
+        if (same_o && same_d) { h->init_key_lo = 0; h->init_key_hi = 8; }   // one digit pass
+    }
     RETIF(check_dcap(h, h->init_dmax2));
     RETIF(pop_reserve(h, h->I, std::max<int64_t>(n, 1)));
     if (n > 0) RETIF(upload_rays(h, h->I, n, origin4, dir4, pow, nullptr));
@@ -1688,6 +1713,7 @@ int lpc_trace_reset(lpc_handle *h)
                            h->stream, h->A.out(), h->I.in(0), h->n_init);
     h->n_cur = h->n_init;
     h->pop_traced = false;
+    h->pop_emitted = true;
     h->order_ready = h->order_pending = false;
     h->split = INT64_MAX;                       // emitted rays: one class
     h->pop_dmax2 = h->init_dmax2;
@@ -1866,6 +1892,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (h->prof) prof_resolve(h);
     std::swap(h->A, h->B);
     h->pop_traced = traced;
+    h->pop_emitted = false;
     h->n_cur = nR + nT;
     h->order_ready = h->order_pending;
     h->order_pending = false;

@@ -4,7 +4,7 @@
 
 writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats), profiles/<tag>_pmc.json
 (per-kernel averages of every PMC pass) and profiles/pmc_intersect.json, which
-bench.py reads for roofline.traffic: HBM bytes per k_intersect launch =
+bench.py reads for roofline.traffic: HBM bytes per launch of the hierarchy kernel (argv[3]) =
 (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of
 MI355X_MICROARCH.md section HBM (FETCH_SIZE reads half of a wide streaming read).
 """
@@ -16,6 +16,7 @@ import shutil
 import sys
 
 src, tag = sys.argv[1], sys.argv[2]
+kname = sys.argv[3] if len(sys.argv) > 3 else "k_rootwalk"     # the bench roofline's kernel
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "profiles")
 os.makedirs(out, exist_ok=True)
@@ -30,13 +31,13 @@ for d in sorted(os.listdir(src)):
 summary = {k: {c: {"launches": len(v), "mean": sum(v) / len(v), "values": v} for c, v in cs.items()}
            for k, cs in per.items()}
 json.dump(summary, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
-ki = next((v for k, v in summary.items() if "k_intersect" in k), {})
+ki = next((v for k, v in summary.items() if kname in k), {})
 if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
     fetch, write = ki["FETCH_SIZE"]["mean"], ki["WRITE_SIZE"]["mean"]
-    rec = {"source": f"profiles/{tag}_pmc.json", "kernel": "k_intersect",
+    rec = {"source": f"profiles/{tag}_pmc.json", "kernel": kname,
            "fetch_size_kb_mean": fetch, "write_size_kb_mean": write,
            "hbm_bytes_per_launch": (2.0 * fetch + write) * 1024.0,
-           "note": "mean over the k_intersect launches of one bench step (all iterations)"}
+           "note": f"mean over the {kname} launches of one bench step (all iterations)"}
     for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
         if c in ki:
             rec[c.lower() + "_mean"] = ki[c]["mean"]
