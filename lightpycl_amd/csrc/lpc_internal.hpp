@@ -156,6 +156,8 @@ struct DevAcc {                       // device-side counters of one iteration
     double pow_next;                  // float64 sum of kept children power
     unsigned int dmax2_bits;          // max |dir|^2 of kept children (float bits)
     unsigned int qerr;                // k_trav gave up waiting on its work queue (QueueArgs::err)
+    unsigned int seq;                 // host copy only: iteration number, written last (k_scan)
+    unsigned int pad;
 };
 
 struct SlotInit {                     // per-mesh slot initial state of a launch (k_slot_init)
@@ -182,6 +184,8 @@ struct CompactArgs {
                                       // reflected block (offset acc->nR), no staging / k_append
     float *mx, *my, *mz, *mp;         // measured record
     int32_t *mm;
+    DevAcc *host_acc;                 // mapped pinned host copy k_scan publishes (or NULL)
+    unsigned int seq;                 // ... with this sequence number, written last
 };
 
 // Order chaining (k_ocount / k_oscan / k_oscatter): the next population's

@@ -336,6 +336,15 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
             d[k] = r.x;
             d[k + 1] = r.y;
         }
+        if (lpc_dbg & 2) {      // TIMING EXPERIMENT ONLY (results wrong): cull children behind the origin
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                const float wx = N.cx[k] - O.x, wy = N.cy[k] - O.y, wz = N.cz[k] - O.z;
+                const float wn = wx * nx + wy * ny + wz * nz, ww = wx * wx + wy * wy + wz * wz;
+                const float R2 = fmaxf(0.0f, -(N.negA[k] + N.negB[k] * ww));
+                if (wn < 0.0f && wn * wn > R2 * 1.02f + 1e-6f) d[k] = 1.0f;
+            }
+        }
         if (N.ref[0] >= 0) {                       // internal node: children are nodes
 #pragma unroll
             for (int k = 0; k < W; ++k)
@@ -1490,6 +1499,27 @@ __global__ __launch_bounds__(1024) void k_scan(CompactArgs A)
         A.acc->nM_iter += (unsigned long long)mt;
     }
     if (t == 0) A.acc->pow_next += pow_next;
+    if (A.host_acc) {
+        // publish the iteration's counters to the mapped host copy, the sequence
+        // number last: the host reads them while k_scatter still runs
+        __syncthreads();
+        if (t == 0) {
+            const DevAcc a = *A.acc;
+            DevAcc *o = A.host_acc;
+            __hip_atomic_store(&o->nR, a.nR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&o->nT, a.nT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&o->m_total, a.m_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&o->nM_iter, a.nM_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store((unsigned long long *)&o->pow_next, __double_as_longlong(a.pow_next),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&o->dmax2_bits, a.dmax2_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&o->qerr, a.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // every counter store acknowledged before the sequence number is sent
+            // (a release fence would also write back the whole L2)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&o->seq, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)

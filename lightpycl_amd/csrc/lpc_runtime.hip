@@ -9,6 +9,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -164,6 +165,13 @@ struct lpc_handle {
     int64_t q_spin = 1 << 22;                       // polls before a waiting wave gives up
     DBuf w_qroots, d_qdq;                           // root items, hand-over slots (kept LPC_QEMPTY)
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
+    DevAcc *acc_map = nullptr, *acc_map_dev = nullptr;   // mapped pinned copy k_scan publishes (+ device address)
+    unsigned int acc_seq = 0;
+    bool early_acc = true;                          // LPC_EARLY_ACC: read the counters before k_scatter ends
+    bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
+    hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
+    hipEvent_t ev_side[2] = {nullptr, nullptr};     // rays ready (main -> side), slivers done (side -> main)
+    double host_last = 0.0;
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     // trace
     Pop A, B, T, I;
@@ -211,6 +219,9 @@ static int dalloc(lpc_handle *h, DBuf &b, size_t bytes, bool keep = false)
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return 0;
     void *p = nullptr;
+    // the stream may still use the old buffer (iterations return before their
+    // last kernel ends): let it finish before the buffer goes
+    if (b.p && h && h->stream) (void)hipStreamSynchronize(h->stream);
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess)
         return set_err(h, LPC_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
@@ -235,6 +246,7 @@ static int pop_reserve(lpc_handle *h, Pop &P, int64_t n)
 {
     if (P.cap >= n && P.buf.p) return 0;
     int64_t cap = std::max<int64_t>(n, 1024);
+    if (P.buf.p && h->stream) (void)hipStreamSynchronize(h->stream);   // see dalloc
     dfree(P.buf);
     RETIF(dalloc(h, P.buf, (size_t)cap * 8 * 4));
     P.cap = cap;
@@ -1052,9 +1064,47 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         perm = nullptr;
     }
     h->last_perm = perm;
+    unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
+    // sliver pieces the launch's rays can reach: dmin <= max |D| (sliver_dmin)
+    if (!(dmax2 >= 0.0)) dmax2 = INFINITY;          // NaN bound (a NaN direction): no culling
+    const float dmax = (float)std::min<double>(sqrt(dmax2 * (1.0 + 1e-5)), (double)INFINITY);
+    int32_t nsp = 0;
+    while (nsp < pt->nspieces && (h->sliver_cull == 0 || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
+    const float dmax_k = h->sliver_cull ? dmax : INFINITY;
+    // the slivers run beside the hierarchy stage on a second stream (both only
+    // add to the slots with order-independent atomics); joined at the end
+    hipStream_t ss = h->stream;
+    const bool side = nsp > 0 && h->stream2 && h->ev_side[0];
+    if (side) {
+        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
+        ss = h->stream2;
+    }
+    if (nsp > 0) {
+        // packets per wave: enough (packet, piece) waves to fill the GPU, no more
+        const int rpl = h->sliver_rays == 64 ? 1 : 2;
+        const int64_t npkx = (n + 64 * rpl - 1) / (64 * rpl);
+        const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
+                                              : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
+        const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
+        if (rpl == 1) {
+            hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
+                               (PacketRec *)h->w_pk64.p);
+            hipLaunchKernelGGL(k_slivers1, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk64.p,
+                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
+                               scnt, stats, (int)ppw, dmax_k);
+        } else {
+            hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
+                               (PacketRec *)h->w_pk.p);
+            hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
+                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
+                               scnt, stats, (int)ppw, dmax_k);
+        }
+        HIPCHK(h, hipGetLastError());
+    }
+    if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-    unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
     const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
     // work queue (default): needs no fan groups and the item encoding's bounds
     bool qpath = false;
@@ -1136,34 +1186,6 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         }
         HIPCHK(h, hipGetLastError());
     }
-    // sliver pieces the launch's rays can reach: dmin <= max |D| (sliver_dmin)
-    if (!(dmax2 >= 0.0)) dmax2 = INFINITY;          // NaN bound (a NaN direction): no culling
-    const float dmax = (float)std::min<double>(sqrt(dmax2 * (1.0 + 1e-5)), (double)INFINITY);
-    int32_t nsp = 0;
-    while (nsp < pt->nspieces && (h->sliver_cull == 0 || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
-    const float dmax_k = h->sliver_cull ? dmax : INFINITY;
-    if (nsp > 0) {
-        // packets per wave: enough (packet, piece) waves to fill the GPU, no more
-        const int rpl = h->sliver_rays == 64 ? 1 : 2;
-        const int64_t npkx = (n + 64 * rpl - 1) / (64 * rpl);
-        const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
-                                              : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
-        const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
-        if (rpl == 1) {
-            hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
-                               (PacketRec *)h->w_pk64.p);
-            hipLaunchKernelGGL(k_slivers1, sg, dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk64.p,
-                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw, dmax_k);
-        } else {
-            hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
-                               (PacketRec *)h->w_pk.p);
-            hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, h->stream, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
-                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw, dmax_k);
-        }
-        HIPCHK(h, hipGetLastError());
-    }
     if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
         if (!h->prof_light) {
             (void)hipEventRecord(e1, h->stream);
@@ -1172,6 +1194,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         h->prof_launches += 1;
         h->prof_pairs += n * (int64_t)h->M;
     }
+    if (side) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
     if (st_user) {
         hipLaunchKernelGGL(k_slot_export, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
                            (const int32_t *)h->d_live.p, (const unsigned long long *)skey,
@@ -1312,6 +1335,24 @@ int lpc_open(int device, lpc_handle **out)
     h->q_per_cu = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_int("LPC_Q_PER_CU", h->q_per_cu)));
     h->q_dcap = std::min<int64_t>((int64_t)1 << 26, std::max<int64_t>(64, env_int("LPC_Q_DCAP", h->q_dcap)));
     h->q_spin = std::min<int64_t>(0xffffffffLL, std::max<int64_t>(1024, env_int("LPC_Q_SPIN", h->q_spin)));
+    h->early_acc = env_int("LPC_EARLY_ACC", h->early_acc) != 0;
+    h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
+    if (env_int("LPC_SIDE_STREAM", 1) != 0) {
+        if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_side[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_side[1], hipEventDisableTiming) != hipSuccess) {
+            h->stream2 = nullptr;       // all on the main stream
+            h->ev_side[0] = h->ev_side[1] = nullptr;
+        }
+    }
+    if (hipHostMalloc((void **)&h->acc_map, sizeof(DevAcc), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&h->acc_map_dev, h->acc_map, 0) != hipSuccess) {
+        h->acc_map = h->acc_map_dev = nullptr;       // counters then come by copy + stream sync
+        h->early_acc = false;
+    } else {
+        memset(h->acc_map, 0, sizeof(DevAcc));
+    }
     if (hipHostMalloc((void **)&h->acc_host, sizeof(DevAcc), hipHostMallocDefault) != hipSuccess) {
         g_open_err = "pinned host buffer";
         lpc_close(h);
@@ -1335,9 +1376,13 @@ int lpc_close(lpc_handle *h)
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
+    if (h->acc_map) (void)hipHostFree(h->acc_map);
+    h->acc_map = h->acc_map_dev = nullptr;
     for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
     prof_resolve(h);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->stream2) { (void)hipStreamSynchronize(h->stream2); (void)hipStreamDestroy(h->stream2); }
+    for (hipEvent_t e : h->ev_side) if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return 0;
@@ -1742,6 +1787,7 @@ int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_i
         RETIF(lpc_trace_measured(h, &c, mesh_power));
         if (measured_count) *measured_count = c;
     }
+    HIPCHK(h, hipStreamSynchronize(h->stream));             // the trace's last kernels too
     return 0;
 }
 
@@ -1771,9 +1817,39 @@ static int ensure_measured(lpc_handle *h, int64_t need)
     return 0;
 }
 
+// Wait (spinning) until k_scan has published this iteration's counters
+// (sequence number h->acc_seq) in the mapped host copy; the stream keeps running.
+// A stream that fails or finishes without publishing is reported.
+static int wait_mapped_acc(lpc_handle *h, DevAcc *out)
+{
+    volatile DevAcc *m = h->acc_map;
+    for (uint64_t i = 1;; ++i) {
+        if (__atomic_load_n(&h->acc_map->seq, __ATOMIC_ACQUIRE) == h->acc_seq) break;
+        if ((i & 255u) == 0u) {
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(&h->acc_map->seq, __ATOMIC_ACQUIRE) == h->acc_seq) break;
+                return set_err(h, LPC_E_HIP, "iteration counters were not published");
+            }
+            if (e != hipErrorNotReady) return set_err(h, LPC_E_HIP, std::string("trace: ") + hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+    out->nR = m->nR; out->nT = m->nT; out->m_total = m->m_total; out->nM_iter = m->nM_iter;
+    out->pow_next = m->pow_next; out->dmax2_bits = m->dmax2_bits; out->qerr = m->qerr;
+    out->seq = m->seq; out->pad = 0;
+    return 0;
+}
+
+static double host_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
                       int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st)
 {
+    const double t_enter = h && h->host_prof ? host_us() : 0.0;
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_iterate before trace_set_rays");
     HIPCHK(h, hipSetDevice(h->device));
@@ -1800,6 +1876,10 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     // its parents' coherence order; measured rays per iteration likewise)
     const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow;
     const bool traced = h->traced && C >= N && !exports && !h->order_chain;
+    // the counters come back through the mapped host copy k_scan writes, so the
+    // host decides and launches the next iteration while k_scatter still runs
+    const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && !h->prof && !h->order_chain;
+    if (early) ++h->acc_seq;
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         RaysIn in = h->A.in(base);
@@ -1820,6 +1900,8 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         if (A.direct_t) A.nT = A.nR;
         A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
         A.mm = (int32_t *)(mf + 4 * mc);
+        A.host_acc = early ? h->acc_map_dev : nullptr;
+        A.seq = h->acc_seq;
         const bool chain = h->order_chain && A.direct_t && h->last_perm != nullptr;
         A.childR = A.childT = nullptr;
         if (chain) {
@@ -1880,10 +1962,22 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
                            h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
         HIPCHK(h, hipGetLastError());
     }
-    HIPCHK(h, hipMemcpyAsync(h->acc_host, h->d_acc.p, sizeof(DevAcc), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    DevAcc acc = *h->acc_host;
+    DevAcc acc;
+    const double t_wait = h->host_prof ? host_us() : 0.0;
+    if (early) {
+        RETIF(wait_mapped_acc(h, &acc));
+    } else {
+        HIPCHK(h, hipMemcpyAsync(h->acc_host, h->d_acc.p, sizeof(DevAcc), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        acc = *h->acc_host;
+    }
     if (acc.qerr) return q_failed(h);
+    if (h->host_prof) {
+        const double t_got = host_us();
+        fprintf(stderr, "[lpc host] n %lld  since last %.1f us  launch %.1f us  wait %.1f us\n", (long long)N,
+                t_enter - h->host_last, t_wait - t_enter, t_got - t_wait);
+        h->host_last = t_got;
+    }
     const int64_t nR = (int64_t)acc.nR, nT = (int64_t)acc.nT;
     if (out_next_pow && nR + nT > 0) {
         HIPCHK(h, hipMemcpyAsync(out_next_pow, h->B.f(6), (size_t)(nR + nT) * 4, hipMemcpyDeviceToHost, h->stream));
