@@ -20,6 +20,11 @@
 
 using namespace lpck;
 
+static double host_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 namespace {
 
 struct DBuf {
@@ -171,7 +176,7 @@ struct lpc_handle {
     bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
     hipEvent_t ev_side[2] = {nullptr, nullptr};     // rays ready (main -> side), slivers done (side -> main)
-    double host_last = 0.0;
+    double host_last = 0.0, t_first = 0.0;
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     // trace
     Pop A, B, T, I;
@@ -981,6 +986,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (!fold_init)
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
                            n, SI);
+    if (h->host_prof && h->t_first == 0.0) h->t_first = host_us();
     SlotInit SIk = SI;
     if (!fold_init) SIk.skey = nullptr;
     const int32_t *perm = nullptr;
@@ -1841,11 +1847,6 @@ static int wait_mapped_acc(lpc_handle *h, DevAcc *out)
     return 0;
 }
 
-static double host_us()
-{
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
                       int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st)
 {
@@ -1878,7 +1879,9 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     const bool traced = h->traced && C >= N && !exports && !h->order_chain;
     // the counters come back through the mapped host copy k_scan writes, so the
     // host decides and launches the next iteration while k_scatter still runs
-    const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && !h->prof && !h->order_chain;
+    // (profiling: only the light level, whose events end before k_scan)
+    const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && (!h->prof || h->prof_light) &&
+                       !h->order_chain;
     if (early) ++h->acc_seq;
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
@@ -1974,8 +1977,10 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (acc.qerr) return q_failed(h);
     if (h->host_prof) {
         const double t_got = host_us();
-        fprintf(stderr, "[lpc host] n %lld  since last %.1f us  launch %.1f us  wait %.1f us\n", (long long)N,
-                t_enter - h->host_last, t_wait - t_enter, t_got - t_wait);
+        fprintf(stderr, "[lpc host] n %lld  since last %.1f us  first launch %.1f us  launch %.1f us  wait %.1f us\n",
+                (long long)N, t_enter - h->host_last, h->t_first > 0.0 ? h->t_first - t_enter : -1.0,
+                t_wait - t_enter, t_got - t_wait);
+        h->t_first = 0.0;
         h->host_last = t_got;
     }
     const int64_t nR = (int64_t)acc.nR, nT = (int64_t)acc.nT;
