@@ -132,7 +132,13 @@ int lpc_trace_reset(lpc_handle *h);
  * st->n_in = current population (known from the previous call / set_rays):
  *   out_origin4/out_dest4 (n_in,4), out_pow (n_in) post-dissipation,
  *   out_meas (n_in)                                    -> the results tuple :355
- *   out_next_pow (n_reflect + n_refract, capacity 2*n_in) -> termination sum :372 */
+ *   out_next_pow (n_reflect + n_refract, capacity 2*n_in) -> termination sum :372
+ * Without any export (and one chunk) the iteration runs in its coherence order:
+ * the same per-ray results, but the next population and this iteration's part
+ * of the measured record come in the parents' traced order instead of the
+ * reference's (LPC_TRACED=0 keeps the reference order).  The call may return
+ * while the iteration's last kernel still runs; the next call, lpc_trace_run
+ * and every copy to the host wait for it. */
 int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
                       int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st);
 /* The reference's iteration loop on one device (iterative_tracer.py:241-391):
@@ -191,10 +197,11 @@ typedef struct {
                                 launch; intersect_ms adds k_spill, k_packet, k_slivers) */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
- * k_intersect traversal counters (2, diagnostic: adds atomics), timing plus
- * per-wave records of the grid traversal (3, diagnostic), only the k_intersect
- * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs), or
- * disable (0). */
+ * traversal counters (2, diagnostic: adds atomics), timing plus per-wave
+ * records of the k_intersect grid (3, diagnostic), only the hierarchy kernel's
+ * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs),
+ * per-item records of the work-queue kernel k_trav (5, diagnostic; read with
+ * lpc_prof_waves as pairs of 4-word records), or disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
 /* Level 3: the last k_intersect launch's per-(piece, packet) records, 4 uint32
