@@ -35,9 +35,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 namespace lpck {
 
-// Debug/timing switches (LPC_DBG, read at lpc_open; never set by tests): bit 0 =
-// skip the per-ray result flush of trav_packet (results WRONG; timing of the
-// flush atomics only).
+// Debug/timing switches (LPC_DBG, read at lpc_open; never set by tests; every
+// one makes results WRONG, timing experiments only): bit 0 = skip trav_packet's
+// per-ray result flush, bit 1 = cull children behind the ray origin, bit 2 =
+// skip the exact tests (drains).
 __constant__ int lpc_dbg = 0;
 
 // ---------------------------------------------------------------------------
@@ -255,6 +256,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
     auto drain = [&]() {
         if (nq == 0) return;
+        if (lpc_dbg & 4) { nq = 0; return; }     // TIMING EXPERIMENT ONLY (results wrong): no exact tests
         const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
         int incl = pc;
         for (int o = 1; o < 64; o <<= 1) {
@@ -511,19 +513,20 @@ __global__ __launch_bounds__(256) void k_lane(RaysIn R, const float *__restrict_
 // item that again exceeds the budget hands its remaining subtrees to the next
 // level's queue (`out`; budget 0 on the last level).  Only used without fan
 // groups (the host checks).
-template <int W>
-__global__ __launch_bounds__(256) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
+// WPB waves per block (1: a wave's slot frees when its items end, see k_rootwalk).
+template <int W, int WPB>
+__global__ __launch_bounds__(64 * WPB, 6) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                unsigned long long *__restrict__ stats, SpillArgs SP,
                                                SpillArgs out)
 {
-    __shared__ WaveLds lds[4];
-    const int wv = threadIdx.x >> 6;
+    __shared__ WaveLds lds[WPB];
+    const int wv = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
     const uint32_t total = min(*SP.ctr, SP.cap);
-    const uint32_t stride = gridDim.x * 4u;
-    for (uint32_t it = blockIdx.x * 4u + (uint32_t)wv; it < total; it += stride) {
+    const uint32_t stride = gridDim.x * (uint32_t)WPB;
+    for (uint32_t it = blockIdx.x * (uint32_t)WPB + (uint32_t)wv; it < total; it += stride) {
         const SpillItem I = SP.items[it];
         if (I.node < 0) continue;
         Piece P;
@@ -634,8 +637,11 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
 // time -- k_intersect's (packet, piece) waves without the waves whose root test
 // fails.  A wave that exceeds the hand-over budget queues its remaining
 // subtrees for k_spill (`out`), as k_intersect does.
-template <int W>
-__global__ __launch_bounds__(256, 6) void k_rootwalk(RaysIn R, const float *__restrict__ rs, int64_t n,
+// WPB waves per block: 1 by default -- a block's slots free as soon as its one
+// item ends, where a 4-wave block holds its LDS until its slowest item ends
+// (per-item records: ~2 800 of 6 144 wave slots walking on average with 4).
+template <int W, int WPB>
+__global__ __launch_bounds__(64 * WPB, 6) void k_rootwalk(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -643,14 +649,14 @@ __global__ __launch_bounds__(256, 6) void k_rootwalk(RaysIn R, const float *__re
                                                      unsigned long long *__restrict__ stats, QueueArgs Q,
                                                      SpillArgs out)
 {
-    __shared__ WaveLds lds[4];
-    const int wv = threadIdx.x >> 6;
+    __shared__ WaveLds lds[WPB];
+    const int wv = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
     uint32_t pre[LPC_Q_CSHARDS + 1];
     pre[0] = 0;
 #pragma unroll
     for (int c = 0; c < LPC_Q_CSHARDS; ++c) pre[c + 1] = pre[c] + min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-    const uint32_t stride = gridDim.x * 4u;
-    for (uint32_t i = blockIdx.x * 4u + (uint32_t)wv; i < pre[LPC_Q_CSHARDS]; i += stride) {
+    const uint32_t stride = gridDim.x * (uint32_t)WPB;
+    for (uint32_t i = blockIdx.x * (uint32_t)WPB + (uint32_t)wv; i < pre[LPC_Q_CSHARDS]; i += stride) {
         int c = 0;
         while (i >= pre[c + 1]) ++c;
         const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - pre[c])];
@@ -658,8 +664,16 @@ __global__ __launch_bounds__(256, 6) void k_rootwalk(RaysIn R, const float *__re
         memset(&P, 0, sizeof(P));
         P.root = (int32_t)q_node(it);
         P.slot = (int32_t)q_slot(it);
+        // profiling (lpc_prof_enable(h, 5)): an 8-word record per item, by item
+        // index (no atomics): walk ticks, nodes, exact tests, slot, start time, 0, HW_ID, XCC_ID
+        uint32_t *rec = (Q.irec && i < Q.irec_cap) ? Q.irec + 8 * (size_t)i : nullptr;
+        if (rec && (threadIdx.x & 63) == 0) {
+            rec[4] = (uint32_t)wall_clock64(); rec[5] = rec[4];
+            rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+            rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (1u << 8);
+        }
         trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
-                       eps, max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
+                       eps, max_ray_len, skey, scnt, stats, rec, 0, out, P.root);
     }
 }
 

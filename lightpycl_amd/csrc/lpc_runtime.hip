@@ -160,7 +160,9 @@ struct lpc_handle {
     bool pop_emitted = false;                       // the population is the emitted rays (set_rays)
     int init_key_lo = 0, init_key_hi = 32;          // key bits that vary over the emitted rays (set_rays)
     int queue = 2;                                  // LPC_QUEUE: 0 k_intersect, 1 persistent k_trav, 2 k_rootwalk
-    int64_t q_walk_blocks = 8192;                   // k_rootwalk grid (4 waves each, grid-stride)
+    int64_t q_walk_blocks = 16384;                  // k_rootwalk grid in 4-wave units (grid-stride)
+    int q_walk_wpb = 1;                             // LPC_Q_WALK_WPB: waves per k_rootwalk block (1 or 4)
+    int spill_wpb = 1;                              // LPC_SPILL_WPB: waves per k_spill block (1 or 4)
     int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
     int q_batch = 2;                                // root items per claim
     int q_hunger = 1;                               // hand work over to waiting waves
@@ -811,15 +813,22 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
         O.ctr = misc + LPC_MISC_SPILL + l + 1;
         O.budget = l + 1 < levels ? SP.budget : 0;
         // later levels hold fewer items (and often none): smaller grids
+        // grid in 4-wave units, launched as single-wave blocks unless LPC_SPILL_WPB=4
         const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
-        if (h->built_w == 8)
-            hipLaunchKernelGGL(k_spill<8>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
-                               perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
-                               max_ray_len, skey, scnt, stats, I, O);
-        else
-            hipLaunchKernelGGL(k_spill<4>, dim3(sb), dim3(256), 0, h->stream, in, rs, n,
-                               perm, (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps,
-                               max_ray_len, skey, scnt, stats, I, O);
+        const int wpb = h->spill_wpb;
+        const unsigned g = sb * 4u / (unsigned)wpb;
+#define LPC_LAUNCH_SPILL(WW, PB, NT)                                                                             \
+    hipLaunchKernelGGL((k_spill<WW, PB>), dim3(g), dim3(64 * PB), 0, h->stream, in, rs, n, perm,                 \
+                       (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
+                       I, O)
+        if (h->built_w == 8) {
+            if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8);
+            else LPC_LAUNCH_SPILL(8, 1, Node8);
+        } else {
+            if (wpb == 4) LPC_LAUNCH_SPILL(4, 4, Node4);
+            else LPC_LAUNCH_SPILL(4, 1, Node4);
+        }
+#undef LPC_LAUNCH_SPILL
     }
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -922,16 +931,22 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
         SpillArgs SP;
         RETIF(spill_setup(h, n, &SP));
-        const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks);
+        // the grid in waves (LPC_Q_WALK_BLOCKS x 4), in blocks of q_walk_wpb waves
+        const int wpb = h->q_walk_wpb;
+        const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4 / wpb);
         if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
-        if (h->built_w == 8)
-            hipLaunchKernelGGL(k_rootwalk<8>, dim3(grid), dim3(256), 0, h->stream, in, rs, n, perm,
-                               (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
-                               scnt, stats, Q, SP);
-        else
-            hipLaunchKernelGGL(k_rootwalk<4>, dim3(grid), dim3(256), 0, h->stream, in, rs, n, perm,
-                               (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
-                               scnt, stats, Q, SP);
+#define LPC_LAUNCH_WALK(WW, PB, NT)                                                                              \
+    hipLaunchKernelGGL((k_rootwalk<WW, PB>), dim3(grid), dim3(64 * PB), 0, h->stream, in, rs, n, perm,            \
+                       (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
+                       Q, SP)
+        if (h->built_w == 8) {
+            if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8);
+            else LPC_LAUNCH_WALK(8, 1, Node8);
+        } else {
+            if (wpb == 4) LPC_LAUNCH_WALK(4, 4, Node4);
+            else LPC_LAUNCH_WALK(4, 1, Node4);
+        }
+#undef LPC_LAUNCH_WALK
         if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
         return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP);
     }
@@ -1330,6 +1345,8 @@ int lpc_open(int device, lpc_handle **out)
     h->traced = env_int("LPC_TRACED", h->traced) != 0;
     h->traced_resort = env_int("LPC_TRACED_SORT", h->traced_resort) != 0;
     h->q_walk_blocks = env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks);
+    h->q_walk_wpb = env_int("LPC_Q_WALK_WPB", h->q_walk_wpb) == 4 ? 4 : 1;
+    h->spill_wpb = env_int("LPC_SPILL_WPB", h->spill_wpb) == 4 ? 4 : 1;
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
