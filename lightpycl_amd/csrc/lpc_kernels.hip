@@ -686,15 +686,15 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_rootwalk(RaysIn R, const float 
 // is unfinished (seen twice in a row), or give up after spin_max polls (sets
 // *err; the host reports it and re-empties the queue).  trav_packet hands the
 // bottom of its stack over while waves of its shard wait.
-template <int W>
-__global__ __launch_bounds__(256, 6) void k_trav(RaysIn R, const float *__restrict__ rs, int64_t n,
+template <int W, int WPB>
+__global__ __launch_bounds__(64 * WPB, 6) void k_trav(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                  const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                  const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                  unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                  unsigned long long *__restrict__ stats, QueueArgs Q)
 {
-    __shared__ WaveLds lds[4];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ WaveLds lds[WPB];
+    const int wv = WPB == 1 ? 0 : (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
     Q.dshard = (int32_t)(blockIdx.x % LPC_Q_DSHARDS);
     uint32_t *rbusy = Q.ctl + LPC_Q_RBUSY(Q.dshard);
     unsigned long long *tp = (unsigned long long *)(Q.ctl + LPC_Q_TP(Q.dshard));

@@ -71,17 +71,22 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
     _cmp_bounce(g2, r2, diss)
 
 
-_OLD = dict(LPC_QUEUE="0")          # k_intersect + k_spill levels instead of the work queue
+_OLD = dict(LPC_QUEUE="0")          # k_intersect + k_spill levels instead of the root items
+_TRAV = dict(LPC_QUEUE="1")         # the persistent work-queue kernel
 _POLICIES = [
     # both paths
     dict(LPC_FLAT="0"), dict(LPC_KEY="3"), dict(LPC_KEY="1"), dict(LPC_SORT="0"), dict(LPC_SORT="2"),
     dict(LPC_GATHER_AOS="0"), dict(LPC_SLIVER_CULL="0"), dict(LPC_FUSE_SHADE="1"), dict(LPC_CHAIN="1"),
     dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_SLIVER_RAYS="64"), dict(LPC_NODE_W="4"),
-    # work queue (k_roots + k_trav): claim batch, piece level, hand-over queue that
-    # overflows, grids of one block, of a few blocks and far beyond residency
-    dict(LPC_Q_BATCH="1"), dict(LPC_Q_BATCH="7"), dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"),
-    dict(LPC_Q_DCAP="64"), dict(LPC_Q_BLOCKS="1"), dict(LPC_Q_BLOCKS="3", LPC_Q_DCAP="64"),
-    dict(LPC_Q_BLOCKS="20000"), dict(LPC_Q_BLOCKS="37", LPC_Q_BATCH="3", LPC_NODE_W="4"),
+    # root items walked by k_rootwalk (default): piece level, grid, block shape
+    dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"), dict(LPC_Q_WALK_BLOCKS="1"),
+    dict(LPC_Q_WALK_WPB="4", LPC_SPILL_WPB="4"), dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"),
+    # persistent work queue (k_roots + k_trav): claim batch, piece level, hand-over
+    # queue that overflows, grids of one block, of a few blocks and far beyond residency
+    dict(_TRAV, LPC_Q_BATCH="1"), dict(_TRAV, LPC_Q_BATCH="7"), dict(_TRAV, LPC_Q_TARGET="1"),
+    dict(_TRAV, LPC_Q_TARGET="10000000"), dict(_TRAV, LPC_Q_DCAP="64"), dict(_TRAV, LPC_Q_BLOCKS="1"),
+    dict(_TRAV, LPC_Q_BLOCKS="3", LPC_Q_DCAP="64"), dict(_TRAV, LPC_Q_BLOCKS="20000"),
+    dict(_TRAV, LPC_Q_BLOCKS="37", LPC_Q_BATCH="3", LPC_NODE_W="4"), dict(_TRAV, LPC_Q_HUNGER="0"),
     # fan groups fall back to k_intersect
     dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"), dict(LPC_FLAT="20", LPC_KEY="2"),
     # the k_intersect path's own knobs
