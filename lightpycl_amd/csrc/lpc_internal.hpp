@@ -188,6 +188,40 @@ struct CompactArgs {
     unsigned int seq;                 // ... with this sequence number, written last
 };
 
+// Two-kernel compaction of a traced single-chunk iteration (k_shade_stage ->
+// k_stage_move, see lpc_kernels.hip).  Tile counts are packed in one word:
+// reflected | refracted << 9 | measured << 18 (each <= LPC_ST_TILE).
+#define LPC_ST_TILE 256                   // rays per staging tile (k_shade_stage / k_stage_move block)
+struct StageArgs {
+    ShadeArgs S;                      // shading inputs (S.o unused)
+    float *stR, *stT;                 // staged kept children: 8 arrays each (ox..pw | pmid), stride cst
+    float *stM;                       // staged measured rays: x y z pw | mesh, stride cst
+    int64_t cst;
+    uint32_t *tcnt;                   // [ntiles] packed counts
+    double *tpow;                     // [ntiles] kept children power
+    uint32_t *tdm;                    // [ntiles] max |dir|^2 (float bits) of kept children
+};
+struct MoveArgs {
+    int64_t ntiles;
+    const float *stR, *stT, *stM;
+    int64_t cst;
+    const uint32_t *tcnt;
+    const double *tpow;
+    const uint32_t *tdm;
+    float *popR;                      // next population: 8 arrays, stride capR
+    int64_t capR;
+    float *mrec;                      // measured record: x y z pw | mesh, stride capM
+    int64_t capM;
+    unsigned long long m_base;        // measured record length before this iteration
+    DevAcc *acc;
+    DevAcc *host_acc;                 // mapped pinned host copy (or NULL)
+    unsigned int seq;
+    // the next population's slots and launch words, reset here (k_slot_init's
+    // work) when it fits the slot arrays (n_next <= slot_cap)
+    SlotInit SI;
+    int64_t slot_cap;
+};
+
 // Order chaining (k_ocount / k_oscan / k_oscatter): the next population's
 // coherence order = the kept children in their parents' traced order
 // ([reflected ; refracted]), with the rays copied into that order.

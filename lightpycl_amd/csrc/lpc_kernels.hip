@@ -1307,7 +1307,7 @@ __global__ __launch_bounds__(256) void k_keypack(RaysIn R, int64_t n, float bx0,
 
 // ---------------------------------------------------------------------------
 // k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
-static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t r)
+static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_t r, PostOut &po, f3 &dest)
 {
     const f3 O = mk3(A.in.ox[r], A.in.oy[r], A.in.oz[r]);
     const f3 D = mk3(A.in.dx[r], A.in.dy[r], A.in.dz[r]);
@@ -1318,15 +1318,22 @@ static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t
         const unsigned long long k = A.skey[a];
         t = slot_key_t(k); i = slot_key_idx(k); c = A.sc[a];
     };
-    const PostOut po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
-    const f3 dest = ray_dest(O, D, po.t_min);
+    po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
+    dest = ray_dest(O, D, po.t_min);
     const int32_t meas_in = A.meas_in ? A.meas_in[r] : 0;
     auto tri = [&](int32_t idx, f3 &v0, f3 &v1, f3 &v2) {
         const float *v = A.verts + (int64_t)idx * 9;
         v0 = mk3(v[0], v[1], v[2]); v1 = mk3(v[3], v[4], v[5]); v2 = mk3(v[6], v[7], v[8]);
     };
-    const ShadeOut s = shade(O, D, dest, A.in.pw[r], meas_in, po.hit_mesh, po.hit_idx, po.n1,
-                             po.n2, A.mat_type, A.ior, A.refl, A.diss, A.ior_env, tri);
+    return shade(O, D, dest, A.in.pw[r], meas_in, po.hit_mesh, po.hit_idx, po.n1, po.n2, A.mat_type, A.ior,
+                 A.refl, A.diss, A.ior_env, tri);
+}
+
+static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t r)
+{
+    PostOut po;
+    f3 dest;
+    const ShadeOut s = shade_eval(A, r, po, dest);
     A.o.destx[r] = dest.x; A.o.desty[r] = dest.y; A.o.destz[r] = dest.z;
     A.o.imid[r] = po.hit_mesh;
     A.o.pw[r] = s.pow;
@@ -1591,6 +1598,202 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two-kernel compaction of a traced single-chunk iteration (StageArgs /
+// MoveArgs), replacing k_shade + k_count + k_scan + k_scatter + k_append:
+//   k_shade_stage  shading, one ray per thread; a 256-ray tile's kept children
+//                  and measured rays are written compacted into the tile's own
+//                  staging rows, with the tile's counts, kept power and max |dir|^2;
+//   k_stage_move   every block sums the tile counts (its tiles' prefixes and the
+//                  totals, so the refracted block goes straight after the
+//                  reflected one) and moves its tiles' staged rows into place;
+//                  block 0 also writes the iteration counters (fixed-order power
+//                  sum) and publishes them to the host.
+// Children and measured rays land at the same positions as with the four
+// kernels ([reflected ; refracted], each in parent order).
+__global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
+{
+    __shared__ int32_t s_w[3][LPC_ST_TILE / 64];
+    __shared__ double s_pow[LPC_ST_TILE / 64];
+    __shared__ float s_dm[LPC_ST_TILE / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t tile = blockIdx.x;
+    const int64_t r = tile * LPC_ST_TILE + threadIdx.x;
+    const bool in = r < A.S.n;
+    PostOut po;
+    po.hit_mesh = -1;
+    f3 dest = mk3(0.0f, 0.0f, 0.0f);
+    ShadeOut s;
+    memset(&s, 0, sizeof(s));
+    s.r_meas = -1; s.t_meas = -1;
+    if (in) s = shade_eval(A.S, r, po, dest);
+    const bool fR = in && s.r_meas == 0, fT = in && s.t_meas == 0, fM = in && s.meas == 1;
+    const uint64_t bR = __ballot(fR), bT = __ballot(fT), bM = __ballot(fM);
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // kept power and max |dir|^2 (k_count's per-ray order: reflected, then refracted)
+    double pk = 0.0;
+    float dm = 0.0f;
+    if (fR) {
+        pk += (double)s.r_pow;
+        dm = fmaxf(dm, s.r_dir.x * s.r_dir.x + s.r_dir.y * s.r_dir.y + s.r_dir.z * s.r_dir.z);
+    }
+    if (fT) {
+        pk += (double)s.t_pow;
+        dm = fmaxf(dm, s.t_dir.x * s.t_dir.x + s.t_dir.y * s.t_dir.y + s.t_dir.z * s.t_dir.z);
+    }
+    pk = wave_sum(pk);
+    dm = wave_max(dm);
+    if (lane == 0) {
+        s_w[0][wv] = __popcll(bR); s_w[1][wv] = __popcll(bT); s_w[2][wv] = __popcll(bM);
+        s_pow[wv] = pk; s_dm[wv] = dm;
+    }
+    __syncthreads();
+    int32_t wo[3] = {0, 0, 0};
+    for (int w = 0; w < wv; ++w)
+        for (int f = 0; f < 3; ++f) wo[f] += s_w[f][w];
+    const int64_t c = A.cst, t0 = tile * LPC_ST_TILE;
+    auto put = [&](float *b, int64_t q, f3 d, float pw) {
+        b[q] = dest.x; b[c + q] = dest.y; b[2 * c + q] = dest.z;
+        b[3 * c + q] = d.x; b[4 * c + q] = d.y; b[5 * c + q] = d.z;
+        b[6 * c + q] = pw; ((int32_t *)b)[7 * c + q] = po.hit_mesh;
+    };
+    if (fR) put(A.stR, t0 + wo[0] + __popcll(bR & below), s.r_dir, s.r_pow);
+    if (fT) put(A.stT, t0 + wo[1] + __popcll(bT & below), s.t_dir, s.t_pow);
+    if (fM) {
+        const int64_t q = t0 + wo[2] + __popcll(bM & below);
+        A.stM[q] = dest.x; A.stM[c + q] = dest.y; A.stM[2 * c + q] = dest.z; A.stM[3 * c + q] = s.pow;
+        ((int32_t *)A.stM)[4 * c + q] = po.hit_mesh;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t cR = 0, cT = 0, cM = 0;
+        double tp = 0.0;                      // fixed order over the tile's waves
+        float td = 0.0f;
+        for (int k = 0; k < LPC_ST_TILE / 64; ++k) {
+            cR += s_w[0][k]; cT += s_w[1][k]; cM += s_w[2][k];
+            tp += s_pow[k]; td = fmaxf(td, s_dm[k]);
+        }
+        A.tcnt[tile] = cR | (cT << 9) | (cM << 18);
+        A.tpow[tile] = tp;
+        A.tdm[tile] = __float_as_uint(td);
+    }
+}
+
+__global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
+{
+    __shared__ long long s_red[LPC_ST_TILE / 64][6];
+    __shared__ long long s_pre[3], s_tot[3];
+    __shared__ double s_p[LPC_ST_TILE];
+    __shared__ float s_d[LPC_ST_TILE];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t tile = blockIdx.x;
+    // this tile's prefix and the totals, from all tile counts (4 B each)
+    long long pre[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
+    for (int64_t j = t; j < A.ntiles; j += LPC_ST_TILE) {
+        const uint32_t v = A.tcnt[j];
+        const long long c[3] = {(long long)(v & 511u), (long long)((v >> 9) & 511u), (long long)((v >> 18) & 511u)};
+        for (int f = 0; f < 3; ++f) {
+            tot[f] += c[f];
+            if (j < tile) pre[f] += c[f];
+        }
+    }
+    for (int f = 0; f < 3; ++f) {
+        long long a = pre[f], b = tot[f];
+        for (int o = 32; o >= 1; o >>= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+        pre[f] = a; tot[f] = b;
+    }
+    if (lane == 0)
+        for (int f = 0; f < 3; ++f) { s_red[wv][f] = pre[f]; s_red[wv][3 + f] = tot[f]; }
+    __syncthreads();
+    if (t < 6) {
+        long long v = 0;
+        for (int k = 0; k < LPC_ST_TILE / 64; ++k) v += s_red[k][t];
+        if (t < 3) s_pre[t] = v; else s_tot[t - 3] = v;
+    }
+    __syncthreads();
+    const int64_t nn = s_tot[0] + s_tot[1];                         // next population
+    const bool reset = A.SI.skey && nn <= A.slot_cap;
+    if (tile == 0) {
+        // iteration counters: fixed-order power sum, max |dir|^2
+        double lp = 0.0;
+        float ld = 0.0f;
+        for (int64_t j = t; j < A.ntiles; j += LPC_ST_TILE) { lp += A.tpow[j]; ld = fmaxf(ld, __uint_as_float(A.tdm[j])); }
+        s_p[t] = lp;
+        s_d[t] = ld;
+        for (int off = LPC_ST_TILE / 2; off >= 1; off >>= 1) {
+            __syncthreads();
+            if (t < off) { s_p[t] += s_p[t + off]; s_d[t] = fmaxf(s_d[t], s_d[t + off]); }
+        }
+        __syncthreads();
+        if (t == 0) {
+            DevAcc a;
+            memset(&a, 0, sizeof(a));
+            a.nR = (unsigned long long)s_tot[0]; a.nT = (unsigned long long)s_tot[1];
+            a.m_total = A.m_base + (unsigned long long)s_tot[2];
+            a.nM_iter = (unsigned long long)s_tot[2];
+            a.pow_next = s_p[0];
+            a.dmax2_bits = __float_as_uint(s_d[0]);
+            a.qerr = A.acc->qerr;
+            *A.acc = a;
+            if (A.host_acc) {
+                // publish to the mapped host copy, the sequence number last: the
+                // host launches the next iteration while the rows still move
+                DevAcc *o = A.host_acc;
+                __hip_atomic_store(&o->nR, a.nR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&o->nT, a.nT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&o->m_total, a.m_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&o->nM_iter, a.nM_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store((unsigned long long *)&o->pow_next, __double_as_longlong(a.pow_next),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&o->dmax2_bits, a.dmax2_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&o->qerr, a.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&o->seq, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        // the next launch's words (k_slot_init's misc reset)
+        if (reset && A.SI.misc)
+            for (int i = t; i < LPC_MISC_WORDS; i += LPC_ST_TILE) A.SI.misc[i] = i < 3 ? 0xffffffffu : 0u;
+    }
+    // this tile's staged rows into place: kept children (two per thread at most,
+    // loads of both issued before the stores), then measured rays
+    const uint32_t v = A.tcnt[tile];
+    const int cR = (int)(v & 511u), cT = (int)((v >> 9) & 511u), cM = (int)((v >> 18) & 511u);
+    const int64_t c = A.cst, cb = A.capR, cm = A.capM, s0 = tile * LPC_ST_TILE;
+    float row[2][8];
+    int64_t dst[2] = {-1, -1};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = t + h * LPC_ST_TILE;
+        if (i < cR + cT) {
+            const bool isR = i < cR;
+            const float *src = isR ? A.stR : A.stT;
+            const int64_t q = s0 + (isR ? i : i - cR);
+            dst[h] = isR ? s_pre[0] + i : s_tot[0] + s_pre[1] + (i - cR);
+#pragma unroll
+            for (int a = 0; a < 8; ++a) row[h][a] = src[a * c + q];
+        }
+    }
+    float mrow[5];
+    const bool hasM = t < cM;
+    if (hasM)
+#pragma unroll
+        for (int a = 0; a < 5; ++a) mrow[a] = A.stM[a * c + s0 + t];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (dst[h] < 0) continue;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) A.popR[a * cb + dst[h]] = row[h][a];
+        if (reset)                            // the child's slots for the next launch (stride nn)
+            slot_init_ray(SlotInit{A.SI.K, A.SI.live, A.SI.max_ray_len, A.SI.skey, A.SI.scnt, nullptr, nullptr, 0ull},
+                          nn, dst[h]);
+    }
+    if (hasM) {
+        const int64_t d = (int64_t)A.m_base + s_pre[2] + t;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) A.mrec[a * cm + d] = mrow[a];
+    }
+}
+
 // Order chaining.  Tiles of 1024 parents in their traced order: counts of kept
 // reflected / refracted children, single-block scan, scatter of the children's
 // positions (perm_next) and rays (rs_next) in [reflected ; refracted] order.
@@ -1687,9 +1890,11 @@ __global__ __launch_bounds__(256) void k_oscatter(OrderArgs A)
 }
 
 // Append the refracted block after the reflected one (next population).
-__global__ __launch_bounds__(256) void k_append(RaysOut dst, RaysIn src, const DevAcc *acc)
+__global__ __launch_bounds__(256) void k_append(RaysOut dst, RaysIn src, const DevAcc *acc, int64_t cap_dst,
+                                                int64_t cap_src)
 {
     const int64_t nR = (int64_t)acc->nR, nT = (int64_t)acc->nT;
+    if (nR < 0 || nT < 0 || nT > cap_src || nR + nT > cap_dst) return;   // broken counts (reported by the host)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nT;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t q = nR + i;

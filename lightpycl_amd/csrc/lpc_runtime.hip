@@ -5,6 +5,7 @@
 // population of a trace.  All launches go to the handle's stream.
 #include "lpc_kernels.hip"
 #include "lpc.h"
+#include <hip/hip_ext.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -116,6 +117,9 @@ struct lpc_handle {
     DBuf w_chR, w_chT, w_oblk, w_perm2[2], w_rs2[2];
     int64_t acc_pending_total = 0;
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
+    bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
+    DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
+    int64_t slots_reset_n = -1;                     // k_stage_move reset the slots for a population of this size
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -180,6 +184,7 @@ struct lpc_handle {
     hipEvent_t ev_side[2] = {nullptr, nullptr};     // rays ready (main -> side), slivers done (side -> main)
     double host_last = 0.0, t_first = 0.0;
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
+    bool pop_init = false;                          // the population is I (the emitted rays, set_rays)
     // trace
     Pop A, B, T, I;
     int64_t n_cur = 0, n_init = 0;
@@ -722,6 +727,9 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         tb = std::max(tb, std::max(tb16, tb32));
         RETIF(dalloc(h, h->w_sort_tmp, tb));
         RETIF(dalloc(h, h->w_keypart, (size_t)((C + 255) / 256) * 16 + 64 * 4));
+        const int64_t nt = (C + LPC_ST_TILE - 1) / LPC_ST_TILE;
+        RETIF(dalloc(h, h->w_fc, (size_t)nt * (8 + 4 + 4) + 64));       // staging tiles' power, counts, max |dir|^2
+        h->slots_reset_n = -1;                          // fresh slot arrays: not reset
         h->sort_tmp_bytes = tb;
         h->ws_rays = C;
     }
@@ -874,7 +882,8 @@ static int q_failed(lpc_handle *h)
     (void)hipStreamSynchronize(h->stream);
     if (h->d_qdq.p) (void)hipMemset(h->d_qdq.p, 0xff, h->d_qdq.bytes);
     (void)hipMemset((char *)h->d_acc.p + offsetof(DevAcc, qerr), 0, sizeof(uint32_t));
-    return set_err(h, LPC_E_HIP, "intersect work queue: a wave gave up waiting (results incomplete)");
+    return set_err(h, LPC_E_HIP, "device-side consistency check failed (work queue wait or compaction prefix): "
+                                 "results incomplete");
 }
 
 static int check_qerr(lpc_handle *h)
@@ -934,11 +943,13 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         // the grid in waves (LPC_Q_WALK_BLOCKS x 4), in blocks of q_walk_wpb waves
         const int wpb = h->q_walk_wpb;
         const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4 / wpb);
-        if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
+        // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
+        // event packets between the kernels
+        if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
 #define LPC_LAUNCH_WALK(WW, PB, NT)                                                                              \
-    hipLaunchKernelGGL((k_rootwalk<WW, PB>), dim3(grid), dim3(64 * PB), 0, h->stream, in, rs, n, perm,            \
-                       (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
-                       Q, SP)
+    hipExtLaunchKernelGGL((k_rootwalk<WW, PB>), dim3(grid), dim3(64 * PB), 0, h->stream, k0, k1, 0, in, rs, n,    \
+                          perm, (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,   \
+                          scnt, stats, Q, SP)
         if (h->built_w == 8) {
             if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8);
             else LPC_LAUNCH_WALK(8, 1, Node8);
@@ -947,7 +958,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
             else LPC_LAUNCH_WALK(4, 1, Node4);
         }
 #undef LPC_LAUNCH_WALK
-        if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
+        if (h->prof) h->ev_kern.push_back({k0, k1});
         return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP);
     }
     unsigned grid = 0;
@@ -998,9 +1009,16 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     const bool fold_init = sorted && h->sort_mode == 1 && n >= LPC_MISC_WORDS &&
                            !(h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX)) &&
                            !(h->order_ready && n == h->order_n);
-    if (!fold_init)
+    // the previous iteration's k_stage_move already reset the slots and launch
+    // words for exactly this population (the counters need no reset either)
+    const bool clean = traced && h->fuse_compact && h->slots_reset_n == n;
+    h->slots_reset_n = -1;
+    if (clean) {
+        h->acc_pending = false;
+    } else if (!fold_init) {
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
                            n, SI);
+    }
     if (h->host_prof && h->t_first == 0.0) h->t_first = host_us();
     SlotInit SIk = SI;
     if (!fold_init) SIk.skey = nullptr;
@@ -1098,9 +1116,13 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     const bool side = nsp > 0 && h->stream2 && h->ev_side[0];
     if (side) {
         HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
-        HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
         ss = h->stream2;
     }
+    // on the side stream the sliver kernels are launched after the hierarchy
+    // stage's (the host reaches k_roots / k_rootwalk sooner; the slivers still
+    // run beside k_rootwalk)
+    auto launch_slivers = [&]() -> int {
+    if (side) HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
     if (nsp > 0) {
         // packets per wave: enough (packet, piece) waves to fill the GPU, no more
         const int rpl = h->sliver_rays == 64 ? 1 : 2;
@@ -1124,6 +1146,9 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         HIPCHK(h, hipGetLastError());
     }
     if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
+    return 0;
+    };
+    if (!side) RETIF(launch_slivers());
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
@@ -1215,7 +1240,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         h->prof_launches += 1;
         h->prof_pairs += n * (int64_t)h->M;
     }
-    if (side) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
+    if (side) {
+        RETIF(launch_slivers());
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
+    }
     if (st_user) {
         hipLaunchKernelGGL(k_slot_export, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
                            (const int32_t *)h->d_live.p, (const unsigned long long *)skey,
@@ -1313,6 +1341,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sort_mode = env_int("LPC_SORT", h->sort_mode) == 2 ? 2 : 1;
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
     h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
+    h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
     h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
     h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
@@ -1395,7 +1424,7 @@ int lpc_close(lpc_handle *h)
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_qroots, &h->d_qdq, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
-                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1]};
+                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1], &h->w_fc};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1775,10 +1804,10 @@ int lpc_trace_reset(lpc_handle *h)
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_reset before trace_set_rays");
     HIPCHK(h, hipSetDevice(h->device));
-    RETIF(pop_reserve(h, h->A, std::max<int64_t>(h->n_init, 1)));
-    if (h->n_init > 0)
-        hipLaunchKernelGGL(k_copy_pop, dim3((unsigned)std::min<int64_t>(grid1(h->n_init), 8192)), dim3(256), 0,
-                           h->stream, h->A.out(), h->I.in(0), h->n_init);
+    // the first iteration reads the emitted rays where set_rays put them (I is
+    // never written by an iteration: no copy)
+    h->pop_init = true;
+    h->slots_reset_n = -1;
     h->n_cur = h->n_init;
     h->pop_traced = false;
     h->pop_emitted = true;
@@ -1900,9 +1929,12 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && (!h->prof || h->prof_light) &&
                        !h->order_chain;
     if (early) ++h->acc_seq;
+    // traced single chunk: k_shade_stage + k_stage_move
+    const bool fused = traced && h->fuse_compact && C >= N;
+    int64_t fused_slot_cap = -1;
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
-        RaysIn in = h->A.in(base);
+        RaysIn in = (h->pop_init ? h->I : h->A).in(base);
         const int64_t split = h->split == INT64_MAX ? INT64_MAX : std::max<int64_t>(0, h->split - base);
         RaysIn tin;
         RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2,
@@ -1928,6 +1960,40 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             RETIF(dalloc(h, h->w_chR, (size_t)nc * 4));
             RETIF(dalloc(h, h->w_chT, (size_t)nc * 4));
             A.childR = (int32_t *)h->w_chR.p; A.childT = (int32_t *)h->w_chT.p;
+        }
+        if (fused) {                  // shade + staged compaction, two kernels (k_shade_stage, k_stage_move)
+            const int64_t nt = (nc + LPC_ST_TILE - 1) / LPC_ST_TILE;
+            const size_t Cs = (size_t)h->ws_rays;
+            StageArgs G;
+            G.S = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
+            G.stR = (float *)h->w_shf.p;                // the 20 shade-output arrays hold the staging rows
+            G.stT = (float *)h->w_shi.p;
+            G.stM = (float *)h->w_soa.p;
+            G.cst = (int64_t)Cs;
+            G.tpow = (double *)h->w_fc.p;
+            G.tcnt = (uint32_t *)(G.tpow + nt);
+            G.tdm = G.tcnt + nt;
+            hipLaunchKernelGGL(k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, G);
+            MoveArgs M;
+            M.ntiles = nt;
+            M.stR = G.stR; M.stT = G.stT; M.stM = G.stM; M.cst = G.cst;
+            M.tcnt = G.tcnt; M.tpow = G.tpow; M.tdm = G.tdm;
+            M.popR = h->B.f(0); M.capR = h->B.cap;
+            M.mrec = mf; M.capM = (int64_t)mc;
+            M.m_base = (unsigned long long)h->m_total;
+            M.acc = (DevAcc *)h->d_acc.p;
+            M.host_acc = A.host_acc;
+            M.seq = A.seq;
+            // the next population's slots are reset here (k_slot_init skipped next time)
+            M.SI.K = h->K; M.SI.live = (const int32_t *)h->d_live.p; M.SI.max_ray_len = h->max_ray_len;
+            M.SI.skey = (unsigned long long *)h->w_key.p; M.SI.scnt = (int32_t *)h->w_sc.p;
+            M.SI.misc = (uint32_t *)h->d_misc.p; M.SI.acc = nullptr; M.SI.m_total = 0;
+            M.slot_cap = h->ws_rays;
+            hipLaunchKernelGGL(k_stage_move, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
+            fused_slot_cap = h->ws_rays;        // k_stage_move resets the next population's slots if it fits
+            HIPCHK(h, hipGetLastError());
+            if (h->prof && !h->prof_light) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
+            continue;
         }
         if (h->fuse_shade) {          // postproc + Fresnel + the tile counts in one pass
             const ShadeArgs SA = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
@@ -1979,7 +2045,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     // device), then the counters to the pinned copy: one host sync per iteration
     if (C < N) {
         hipLaunchKernelGGL(k_append, dim3((unsigned)std::min<int64_t>(grid1(N), 8192)), dim3(256), 0, h->stream,
-                           h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p);
+                           h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p, h->B.cap, h->T.cap);
         HIPCHK(h, hipGetLastError());
     }
     DevAcc acc;
@@ -2007,9 +2073,11 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     }
     if (h->prof) prof_resolve(h);
     std::swap(h->A, h->B);
+    h->pop_init = false;
     h->pop_traced = traced;
     h->pop_emitted = false;
     h->n_cur = nR + nT;
+    h->slots_reset_n = (fused_slot_cap >= nR + nT) ? nR + nT : -1;
     h->order_ready = h->order_pending;
     h->order_pending = false;
     h->order_n = nR + nT;

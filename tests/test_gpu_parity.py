@@ -351,3 +351,37 @@ def test_traced_order_equals_reference_order(monkeypatch, name, n, chunk):
         r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
         return r[np.lexsort(r.T[::-1])]
     np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n", [("synthetic", 100000), ("lens", 50000), ("eye", 4000), ("cube", 3000)])
+def test_fused_compaction_equals_four_kernels(monkeypatch, name, n):
+    """k_shade_compact (shade, counts, look-back scan and scatter in one pass)
+    against k_shade + k_count + k_scan + k_scatter (LPC_FUSE_COMPACT=0): the same
+    children at the same positions, so identical per-iteration counts and the
+    identical measured record, element for element."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.BUILDERS[name](n=n, seed=23)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("LPC_FUSE_COMPACT", fused)
+        e = Engine(0)
+        try:
+            e.upload_meshes(sc.meshes)
+            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+            for rep in range(2):            # the tile words of the first trace must not leak into the second
+                e.reset()
+                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+            pos, p, mm = e.fetch_measured()
+            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm,
+                        [s.power_next for s in stats]))
+        finally:
+            e.close()
+    a, b = out
+    assert a[0] == b[0] and a[1] == b[1]
+    np.testing.assert_array_equal(a[2], b[2])
+    for x, y in zip(a[3:6], b[3:6]):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_allclose(a[6], b[6], rtol=1e-12)
