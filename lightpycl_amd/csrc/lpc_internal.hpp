@@ -169,6 +169,7 @@ struct SlotInit {                     // per-mesh slot initial state of a launch
     uint32_t *misc;                   // LPC_MISC_WORDS per-launch words (reset), may be NULL
     DevAcc *acc;                      // iteration counters to reset, may be NULL
     unsigned long long m_total;
+    int uniform;                      // every slot (max_ray_len, idx -1): the traced path's clean state
 };
 
 struct CompactArgs {
@@ -200,6 +201,8 @@ struct StageArgs {
     uint32_t *tcnt;                   // [ntiles] packed counts
     double *tpow;                     // [ntiles] kept children power
     uint32_t *tdm;                    // [ntiles] max |dir|^2 (float bits) of kept children
+    unsigned long long *skey;         // the slots read by the shading, restored to the clean state
+    int32_t *scnt;                    //   (key slot_key(max_ray_len, -1), count 0) after the read
 };
 struct MoveArgs {
     int64_t ntiles;
@@ -216,10 +219,7 @@ struct MoveArgs {
     DevAcc *acc;
     DevAcc *host_acc;                 // mapped pinned host copy (or NULL)
     unsigned int seq;
-    // the next population's slots and launch words, reset here (k_slot_init's
-    // work) when it fits the slot arrays (n_next <= slot_cap)
-    SlotInit SI;
-    int64_t slot_cap;
+    uint32_t *misc;                   // the next launch's words (LPC_MISC_WORDS), reset here
 };
 
 // Order chaining (k_ocount / k_oscan / k_oscatter): the next population's

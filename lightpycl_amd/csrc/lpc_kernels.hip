@@ -1063,9 +1063,9 @@ static __device__ __forceinline__ void slot_init_ray(const SlotInit &SI, int64_t
         z.m_total = SI.m_total;
         *SI.acc = z;
     }
-    if (r >= n) return;
+    if (r >= n || !SI.skey) return;
     for (int32_t j = 0; j < SI.K; ++j) {
-        SI.skey[(int64_t)j * n + r] = slot_key(SI.max_ray_len, SI.live[j] ? -1 : 0);
+        SI.skey[(int64_t)j * n + r] = slot_key(SI.max_ray_len, (SI.uniform || SI.live[j]) ? -1 : 0);
         SI.scnt[(int64_t)j * n + r] = 0;
     }
 }
@@ -1157,15 +1157,10 @@ __global__ __launch_bounds__(256) void k_bbox(RaysIn R, int64_t n, uint32_t *__r
 // leave one small object still spread over the 32^3 cells (otherwise the scene
 // box bx0.., sx..).  class = (i >= split): the refracted block of a population
 // ([reflected ; refracted], k_append) sorts apart from the reflected one.
-__global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
-                                                float sx, float sy, float sz, const uint32_t *__restrict__ bb,
-                                                int64_t split, int dir_major, uint32_t *__restrict__ keys,
-                                                int32_t *__restrict__ vals, float4 *__restrict__ aos,
-                                                SlotInit SI)
+static __device__ __forceinline__ uint32_t raykey_ray(const RaysIn &R, int64_t i, float bx0, float by0, float bz0,
+                                                      float sx, float sy, float sz, const uint32_t *__restrict__ bb,
+                                                      int64_t split, int dir_major, float4 *__restrict__ aos)
 {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (SI.skey) slot_init_ray(SI, n, i);           // k_slot_init folded in (one launch fewer)
-    if (i >= n) return;
     if (aos) {          // the ray as one 32-byte row: k_gather_aos reads it with one line per ray
         aos[2 * i] = make_float4(R.ox[i], R.oy[i], R.oz[i], R.dx[i]);
         aos[2 * i + 1] = make_float4(R.dy[i], R.dz[i], R.pw ? R.pw[i] : 0.0f,
@@ -1199,7 +1194,19 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     const uint32_t oz = (uint32_t)fminf(fmaxf((R.oz[i] - bz0) * sz, 0.0f), 31.0f);
     const uint32_t okey = spread3(ox) | (spread3(oy) << 1) | (spread3(oz) << 2);
     const uint32_t dkey = spread2(du) | (spread2(dv) << 1);
-    keys[i] = (i >= split ? 0x80000000u : 0u) | (dir_major ? (dkey << 15) | okey : (okey << 16) | dkey);
+    return (i >= split ? 0x80000000u : 0u) | (dir_major ? (dkey << 15) | okey : (okey << 16) | dkey);
+}
+
+__global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
+                                                float sx, float sy, float sz, const uint32_t *__restrict__ bb,
+                                                int64_t split, int dir_major, uint32_t *__restrict__ keys,
+                                                int32_t *__restrict__ vals, float4 *__restrict__ aos,
+                                                SlotInit SI)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (SI.skey || SI.misc || SI.acc) slot_init_ray(SI, n, i);     // k_slot_init folded in (one launch fewer)
+    if (i >= n) return;
+    keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, bb, split, dir_major, aos);
     vals[i] = (int32_t)i;
 }
 
@@ -1307,16 +1314,21 @@ __global__ __launch_bounds__(256) void k_keypack(RaysIn R, int64_t n, float bx0,
 
 // ---------------------------------------------------------------------------
 // k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
-static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_t r, PostOut &po, f3 &dest)
+// touched (optional): bit j set for slots j < 64 that hold anything but the clean
+// state (max_ray_len, idx -1, count 0), noted as postproc reads them
+static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_t r, PostOut &po, f3 &dest,
+                                                      uint64_t *touched = nullptr)
 {
     const f3 O = mk3(A.in.ox[r], A.in.oy[r], A.in.oz[r]);
     const f3 D = mk3(A.in.dx[r], A.in.dy[r], A.in.dz[r]);
     const int32_t prev = A.in.pmid[r];
     const int64_t n = A.n;
+    const unsigned long long k0 = slot_key(A.max_ray_len, -1);
     auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
         const int64_t a = (int64_t)j * n + r;
         const unsigned long long k = A.skey[a];
         t = slot_key_t(k); i = slot_key_idx(k); c = A.sc[a];
+        if (touched && j < 64 && (k != k0 || c != 0)) *touched |= 1ull << j;
     };
     po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
     dest = ray_dest(O, D, po.t_min);
@@ -1604,9 +1616,9 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
 //   k_shade_stage  shading, one ray per thread; a 256-ray tile's kept children
 //                  and measured rays are written compacted into the tile's own
 //                  staging rows, with the tile's counts, kept power and max |dir|^2;
-//   k_stage_move   every block sums the tile counts (its tiles' prefixes and the
+//   k_stage_move   every block sums the tile counts (its tile's prefix and the
 //                  totals, so the refracted block goes straight after the
-//                  reflected one) and moves its tiles' staged rows into place;
+//                  reflected one) and moves its tile's staged rows into place;
 //                  block 0 also writes the iteration counters (fixed-order power
 //                  sum) and publishes them to the host.
 // Children and measured rays land at the same positions as with the four
@@ -1626,7 +1638,25 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     ShadeOut s;
     memset(&s, 0, sizeof(s));
     s.r_meas = -1; s.t_meas = -1;
-    if (in) s = shade_eval(A.S, r, po, dest);
+    if (in) {
+        uint64_t touched = 0;
+        s = shade_eval(A.S, r, po, dest, &touched);
+        // the slots just read back to the clean state: those a flush wrote (noted
+        // while postproc read them; slots 64 and up are read again)
+        const unsigned long long k0 = slot_key(A.S.max_ray_len, -1);
+        while (touched) {
+            const int j = __builtin_ctzll(touched);
+            touched &= touched - 1;
+            const int64_t a = (int64_t)j * A.S.n + r;
+            A.skey[a] = k0;
+            A.scnt[a] = 0;
+        }
+        for (int32_t j = 64; j < A.S.K; ++j) {
+            const int64_t a = (int64_t)j * A.S.n + r;
+            if (A.skey[a] != k0) A.skey[a] = k0;
+            if (A.scnt[a] != 0) A.scnt[a] = 0;
+        }
+    }
     const bool fR = in && s.r_meas == 0, fT = in && s.t_meas == 0, fM = in && s.meas == 1;
     const uint64_t bR = __ballot(fR), bT = __ballot(fT), bM = __ballot(fM);
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1710,8 +1740,6 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         if (t < 3) s_pre[t] = v; else s_tot[t - 3] = v;
     }
     __syncthreads();
-    const int64_t nn = s_tot[0] + s_tot[1];                         // next population
-    const bool reset = A.SI.skey && nn <= A.slot_cap;
     if (tile == 0) {
         // iteration counters: fixed-order power sum, max |dir|^2
         double lp = 0.0;
@@ -1751,8 +1779,8 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
             }
         }
         // the next launch's words (k_slot_init's misc reset)
-        if (reset && A.SI.misc)
-            for (int i = t; i < LPC_MISC_WORDS; i += LPC_ST_TILE) A.SI.misc[i] = i < 3 ? 0xffffffffu : 0u;
+        if (A.misc)
+            for (int i = t; i < LPC_MISC_WORDS; i += LPC_ST_TILE) A.misc[i] = i < 3 ? 0xffffffffu : 0u;
     }
     // this tile's staged rows into place: kept children (two per thread at most,
     // loads of both issued before the stores), then measured rays
@@ -1783,9 +1811,6 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         if (dst[h] < 0) continue;
 #pragma unroll
         for (int a = 0; a < 8; ++a) A.popR[a * cb + dst[h]] = row[h][a];
-        if (reset)                            // the child's slots for the next launch (stride nn)
-            slot_init_ray(SlotInit{A.SI.K, A.SI.live, A.SI.max_ray_len, A.SI.skey, A.SI.scnt, nullptr, nullptr, 0ull},
-                          nn, dst[h]);
     }
     if (hasM) {
         const int64_t d = (int64_t)A.m_base + s_pre[2] + t;

@@ -119,7 +119,10 @@ struct lpc_handle {
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
-    int64_t slots_reset_n = -1;                     // k_stage_move reset the slots for a population of this size
+    bool slots_clean = false;                       // every slot (max_ray_len slots_mrl, idx -1, count 0)
+    float slots_mrl = 0.0f;
+    bool misc_clean = false;                        // the launch words were reset for the next launch
+    bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -729,7 +732,8 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_keypart, (size_t)((C + 255) / 256) * 16 + 64 * 4));
         const int64_t nt = (C + LPC_ST_TILE - 1) / LPC_ST_TILE;
         RETIF(dalloc(h, h->w_fc, (size_t)nt * (8 + 4 + 4) + 64));       // staging tiles' power, counts, max |dir|^2
-        h->slots_reset_n = -1;                          // fresh slot arrays: not reset
+
+        h->slots_clean = h->misc_clean = false;         // fresh slot arrays
         h->sort_tmp_bytes = tb;
         h->ws_rays = C;
     }
@@ -998,6 +1002,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     SI.skey = skey; SI.scnt = scnt; SI.misc = misc;
     SI.acc = h->acc_pending ? (DevAcc *)h->d_acc.p : nullptr;
     SI.m_total = (unsigned long long)h->acc_pending_total;
+    SI.uniform = 0;
     h->acc_pending = false;
     // traced mode (trace_iterate without per-ray exports): the slots, shading and
     // compaction work in the launch's coherence order, so the children come out
@@ -1009,19 +1014,34 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     const bool fold_init = sorted && h->sort_mode == 1 && n >= LPC_MISC_WORDS &&
                            !(h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX)) &&
                            !(h->order_ready && n == h->order_n);
-    // the previous iteration's k_stage_move already reset the slots and launch
-    // words for exactly this population (the counters need no reset either)
-    const bool clean = traced && h->fuse_compact && h->slots_reset_n == n;
-    h->slots_reset_n = -1;
-    if (clean) {
-        h->acc_pending = false;
-    } else if (!fold_init) {
+    // Traced single-chunk iterations (k_shade_stage) leave every slot they read in
+    // the clean state (max_ray_len, idx -1, count 0), so once the whole slot array
+    // is clean no slot needs a reset; only the launch words do (k_stage_move
+    // reset them for the next launch; the emitted rays' k_raykey does).
+    const bool restore = traced && h->fuse_compact;
+    const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
+    const bool misc_clean = restore && h->misc_clean;
+    h->slots_clean = h->misc_clean = false;
+    SlotInit SIk = SI;
+    SIk.skey = nullptr; SIk.misc = nullptr; SIk.acc = nullptr;
+    if (restore && !clean) {            // the whole array to the clean state (stride-independent)
+        SI.uniform = 1;
+        const int64_t all = h->ws_rays;
+        hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(all, LPC_MISC_WORDS))), dim3(256), 0,
+                           h->stream, all, SI);
+    } else if (restore) {               // slots clean: the launch words only (k_stage_move writes all counters)
+        SI.skey = nullptr;
+        SI.acc = nullptr;
+        if (fold_init) SIk = SI;
+        else if (!misc_clean)
+            hipLaunchKernelGGL(k_slot_init, dim3(grid1(LPC_MISC_WORDS)), dim3(256), 0, h->stream, (int64_t)0, SI);
+    } else if (fold_init) {
+        SIk = SI;
+    } else {
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
                            n, SI);
     }
     if (h->host_prof && h->t_first == 0.0) h->t_first = host_us();
-    SlotInit SIk = SI;
-    if (!fold_init) SIk.skey = nullptr;
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
     const bool chained = !traced && h->order_ready && n == h->order_n;
@@ -1065,15 +1085,15 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         if (pop_box)
             hipLaunchKernelGGL(k_bbox, dim3((unsigned)std::min<int64_t>(grid1(n), 256)), dim3(256), 0, h->stream,
                                in, n, misc);
+        // the emitted rays' varying key bits (set_rays) under key mode 0
+        int b0 = 0, b1 = 32;
+        if (traced && h->pop_emitted && h->key_mode == 0 && !cls) { b0 = h->init_key_lo; b1 = h->init_key_hi; }
         hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                            h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
                            pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
                            (h->key_mode == 3 || h->key_mode == 4) ? 1 : 0, kin, vin,
                            (h->gather_aos || traced) ? (float4 *)h->w_aos.p : nullptr, SIk);
         size_t tb = h->sort_tmp_bytes;
-        // the emitted rays' varying key bits (set_rays) under key mode 0
-        int b0 = 0, b1 = 32;
-        if (traced && h->pop_emitted && h->key_mode == 0 && !cls) { b0 = h->init_key_lo; b1 = h->init_key_hi; }
         if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
                                                               b0, b1, h->stream));
@@ -1148,7 +1168,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
     return 0;
     };
-    if (!side) RETIF(launch_slivers());
+    const bool late = side && h->sliver_late;
+    if (!late) RETIF(launch_slivers());
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
@@ -1240,10 +1261,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         h->prof_launches += 1;
         h->prof_pairs += n * (int64_t)h->M;
     }
-    if (side) {
-        RETIF(launch_slivers());
-        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
-    }
+    if (late) RETIF(launch_slivers());
+    if (side) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
     if (st_user) {
         hipLaunchKernelGGL(k_slot_export, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
                            (const int32_t *)h->d_live.p, (const unsigned long long *)skey,
@@ -1342,6 +1361,7 @@ int lpc_open(int device, lpc_handle **out)
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
     h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
     h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
+    h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
     h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
     h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
@@ -1807,16 +1827,13 @@ int lpc_trace_reset(lpc_handle *h)
     // the first iteration reads the emitted rays where set_rays put them (I is
     // never written by an iteration: no copy)
     h->pop_init = true;
-    h->slots_reset_n = -1;
     h->n_cur = h->n_init;
     h->pop_traced = false;
     h->pop_emitted = true;
     h->order_ready = h->order_pending = false;
     h->split = INT64_MAX;                       // emitted rays: one class
     h->pop_dmax2 = h->init_dmax2;
-    h->m_total = 0;                             // measured record emptied in-stream
-    hipLaunchKernelGGL(k_acc_init, dim3(1), dim3(64), 0, h->stream, (DevAcc *)h->d_acc.p, 0ull);
-    HIPCHK(h, hipGetLastError());
+    h->m_total = 0;                             // measured record emptied (the first iteration resets the counters)
     return 0;
 }
 
@@ -1931,7 +1948,6 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (early) ++h->acc_seq;
     // traced single chunk: k_shade_stage + k_stage_move
     const bool fused = traced && h->fuse_compact && C >= N;
-    int64_t fused_slot_cap = -1;
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         RaysIn in = (h->pop_init ? h->I : h->A).in(base);
@@ -1973,6 +1989,9 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             G.tpow = (double *)h->w_fc.p;
             G.tcnt = (uint32_t *)(G.tpow + nt);
             G.tdm = G.tcnt + nt;
+            G.skey = (unsigned long long *)h->w_key.p;
+            G.scnt = (int32_t *)h->w_sc.p;
+
             hipLaunchKernelGGL(k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, G);
             MoveArgs M;
             M.ntiles = nt;
@@ -1984,13 +2003,11 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             M.acc = (DevAcc *)h->d_acc.p;
             M.host_acc = A.host_acc;
             M.seq = A.seq;
-            // the next population's slots are reset here (k_slot_init skipped next time)
-            M.SI.K = h->K; M.SI.live = (const int32_t *)h->d_live.p; M.SI.max_ray_len = h->max_ray_len;
-            M.SI.skey = (unsigned long long *)h->w_key.p; M.SI.scnt = (int32_t *)h->w_sc.p;
-            M.SI.misc = (uint32_t *)h->d_misc.p; M.SI.acc = nullptr; M.SI.m_total = 0;
-            M.slot_cap = h->ws_rays;
+            M.misc = (uint32_t *)h->d_misc.p;
             hipLaunchKernelGGL(k_stage_move, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
-            fused_slot_cap = h->ws_rays;        // k_stage_move resets the next population's slots if it fits
+            h->slots_clean = true;              // k_shade_stage restored what it read
+            h->slots_mrl = h->max_ray_len;
+            h->misc_clean = true;               // k_stage_move reset the next launch's words
             HIPCHK(h, hipGetLastError());
             if (h->prof && !h->prof_light) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
             continue;
@@ -2077,7 +2094,6 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     h->pop_traced = traced;
     h->pop_emitted = false;
     h->n_cur = nR + nT;
-    h->slots_reset_n = (fused_slot_cap >= nR + nT) ? nR + nT : -1;
     h->order_ready = h->order_pending;
     h->order_pending = false;
     h->order_n = nR + nT;

@@ -167,13 +167,17 @@ class Engine:
         power_threshold or no ray is kept (at most `iterations`).  Returns the
         per-iteration stats and the measured (count, per-mesh power)."""
         cap = max(int(iterations), 0)
-        arr = (_lib.IterStats * max(cap, 1))()
-        k = ctypes.c_int32(0)
-        c = ctypes.c_int64(0)
-        mp = np.zeros(max(self.mesh_count, 1), np.float64)
+        key = (cap, self.mesh_count)
+        bufs = self._run_bufs.get(key) if hasattr(self, "_run_bufs") else None
+        if bufs is None:            # output buffers kept per cap (one ctypes call per trace)
+            bufs = ((_lib.IterStats * max(cap, 1))(), ctypes.c_int32(0), ctypes.c_int64(0),
+                    np.zeros(max(self.mesh_count, 1), np.float64))
+            self.__dict__.setdefault("_run_bufs", {})[key] = bufs
+        arr, k, c, mp = bufs
         self._c(self.L.lpc_trace_run(self.h, cap, float(power_threshold), arr, ctypes.byref(k), ctypes.byref(c),
-                                     ptr(mp)))
-        return [arr[i] for i in range(k.value)], (c.value, mp[: self.mesh_count])
+                                     mp.ctypes.data_as(ctypes.c_void_p)))
+        return [_lib.IterStats.from_buffer_copy(arr[i]) for i in range(k.value)], (c.value,
+                                                                                   mp[: self.mesh_count].copy())
 
     def measured(self):
         """(count, per-mesh measured power float64[K])."""

@@ -385,3 +385,43 @@ def test_fused_compaction_equals_four_kernels(monkeypatch, name, n):
     for x, y in zip(a[3:6], b[3:6]):
         np.testing.assert_array_equal(x, y)
     np.testing.assert_allclose(a[6], b[6], rtol=1e-12)
+
+
+
+def test_clean_slots_across_paths(oracle_mod):
+    """Traced iterations leave the slot arrays clean instead of resetting them;
+    traces after a per-ray export (which dirties them), a bounce on the same
+    handle and a new max_ray_len must still match a fresh handle's trace."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.lens(n=20000, seed=31)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+
+    def trace(e, mrl):
+        e.set_rays(o4, d4, pw, mrl, sc.ior_env)
+        stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+        return [(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp
+
+    fresh = []
+    for mrl in (sc.max_ray_len, np.float32(sc.max_ray_len * 0.75)):
+        e = Engine(0)
+        e.upload_meshes(sc.meshes)
+        fresh.append(trace(e, mrl))
+        e.close()
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        a = trace(e, sc.max_ray_len)
+        e.reset()
+        e.iterate(export=True)                      # reference-order iteration (slots dirty)
+        e.iterate()
+        b = trace(e, sc.max_ray_len)
+        z = np.zeros(len(pw), np.int32)
+        e.bounce(o4, d4, pw, z, np.full(len(pw), -2, np.int32), sc.max_ray_len, sc.ior_env)
+        c = trace(e, np.float32(sc.max_ray_len * 0.75))
+        d = trace(e, sc.max_ray_len)
+    finally:
+        e.close()
+    for got, want in ((a, fresh[0]), (b, fresh[0]), (c, fresh[1]), (d, fresh[0])):
+        assert got[0] == want[0] and got[1] == want[1]
+        np.testing.assert_array_equal(got[2], want[2])
