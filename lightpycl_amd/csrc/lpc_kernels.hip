@@ -207,7 +207,10 @@ struct WaveLds {
 // rays (filter form d <= 0, see filter_record; node data wave-uniform through
 // the scalar cache); a child node is pushed when any ray passes it, a child
 // triangle's (index, lane mask) is queued for the exact test.
-template <int W>
+// QH: the persistent queue's hand-over to waiting waves (k_trav only); PROF:
+// the profiling counters / records and the LPC_DBG timing switches (compiled
+// out of the default launches: fewer live registers in the hot loop).
+template <int W, bool QH = false, bool PROF = true>
 static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, const float *__restrict__ rs,
                                                    int64_t n, const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
@@ -244,7 +247,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     L.lkey[lane] = key0;
     L.lcnt[lane] = 0;
 
-    const uint64_t clk0 = (stats || wrec) ? wall_clock64() : 0;
+    const uint64_t clk0 = (PROF && (stats || wrec)) ? wall_clock64() : 0;
     int32_t top = 0, nq = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
     uint32_t n_pairs = 0;                           // exact pairs drained (wave-uniform; hand-over cost)
@@ -256,7 +259,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
     auto drain = [&]() {
         if (nq == 0) return;
-        if (lpc_dbg & 4) { nq = 0; return; }     // TIMING EXPERIMENT ONLY (results wrong): no exact tests
+        if (PROF && (lpc_dbg & 4)) { nq = 0; return; }   // TIMING EXPERIMENT ONLY (results wrong): no exact tests
         const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
         int incl = pc;
         for (int o = 1; o < 64; o <<= 1) {
@@ -285,7 +288,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
                     atomicAdd(&L.lcnt[r], 1);
                     if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
                 }
-                ++n_exact;
+                if (PROF) ++n_exact;
             }
         }
         nq = 0;
@@ -320,7 +323,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
         // taken beyond the slots reserved) as read 4 nodes ago are acted on, and
         // a new read is issued (its latency, ~1-2 us, overlaps the next nodes)
         int waiting = 0;
-        if (Q.hunger && Q.dshard >= 0 && (n_nodes & 3u) == 0u) {
+        if (QH && Q.hunger && Q.dshard >= 0 && (n_nodes & 3u) == 0u) {
             waiting = (int)__builtin_amdgcn_readfirstlane((int)(q_head - q_tail));
             q_tail = __hip_atomic_load(Q.ctl + LPC_Q_TP(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             q_head = __hip_atomic_load(Q.ctl + LPC_Q_DHEAD(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -338,7 +341,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
             d[k] = r.x;
             d[k + 1] = r.y;
         }
-        if (lpc_dbg & 2) {      // TIMING EXPERIMENT ONLY (results wrong): cull children behind the origin
+        if (PROF && (lpc_dbg & 2)) {   // TIMING EXPERIMENT ONLY (results wrong): cull children behind the origin
 #pragma unroll
             for (int k = 0; k < W; ++k) {
                 const float wx = N.cx[k] - O.x, wy = N.cy[k] - O.y, wz = N.cz[k] - O.z;
@@ -373,7 +376,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
         }
         // hand the bottom of the stack (the largest subtrees) to waiting waves,
         // at most one entry per waiting wave; keep the top entry
-        if (waiting > 0 && top >= 2) {
+        if (QH && waiting > 0 && top >= 2) {
             const int k = min(min(top - 1, waiting), 63);
             const int32_t ent = lane < k ? L.stack[lane] : 0;
             const int fit = q_publish(Q, k, q_item((uint32_t)w, (uint32_t)ent, (uint32_t)P.slot));
@@ -387,7 +390,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
         }
     }
     drain();
-    if (stats) {
+    if (PROF && stats) {
         for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
         // packet spread: max angle between a lane's direction and lane 0's
         const float cs = nx * bcast(nx, 0) + ny * bcast(ny, 0) + nz * bcast(nz, 0);
@@ -409,14 +412,14 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
         }
     }
     if (gcount && lane == 0) gcount[gslot] = ngr;
-    if (wrec) {                                // per-wave record (diagnostic, no contention)
+    if (PROF && wrec) {                        // per-wave record (diagnostic, no contention)
         for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
         if (lane == 0) {
             uint32_t *r = wrec + 4 * ridx;
             r[0] = (uint32_t)(wall_clock64() - clk0); r[1] = n_nodes; r[2] = n_exact; r[3] = (uint32_t)piece_id;
         }
     }
-    if (s < n && !(lpc_dbg & 1)) {
+    if (s < n && !(PROF && (lpc_dbg & 1))) {
         const unsigned long long k = L.lkey[lane];
         const int32_t c = L.lcnt[lane];
         const int64_t o = (int64_t)P.slot * n, q = perm ? perm[s] : s;
@@ -514,8 +517,8 @@ __global__ __launch_bounds__(256) void k_lane(RaysIn R, const float *__restrict_
 // level's queue (`out`; budget 0 on the last level).  Only used without fan
 // groups (the host checks).
 // WPB waves per block (1: a wave's slot frees when its items end, see k_rootwalk).
-template <int W, int WPB>
-__global__ __launch_bounds__(64 * WPB, 6) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
+template <int W, int WPB, bool PROF = false, int MINW = 6>
+__global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_spill(RaysIn R, const float *__
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
-        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
+        trav_packet<W, false, PROF>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
                     max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
     }
 }
@@ -640,8 +643,8 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
 // WPB waves per block: 1 by default -- a block's slots free as soon as its one
 // item ends, where a 4-wave block holds its LDS until its slowest item ends
 // (per-item records: ~2 800 of 6 144 wave slots walking on average with 4).
-template <int W, int WPB>
-__global__ __launch_bounds__(64 * WPB, 6) void k_rootwalk(RaysIn R, const float *__restrict__ rs, int64_t n,
+template <int W, int WPB, bool PROF = false, int MINW = 6>
+__global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -666,14 +669,14 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_rootwalk(RaysIn R, const float 
         P.slot = (int32_t)q_slot(it);
         // profiling (lpc_prof_enable(h, 5)): an 8-word record per item, by item
         // index (no atomics): walk ticks, nodes, exact tests, slot, start time, 0, HW_ID, XCC_ID
-        uint32_t *rec = (Q.irec && i < Q.irec_cap) ? Q.irec + 8 * (size_t)i : nullptr;
+        uint32_t *rec = (PROF && Q.irec && i < Q.irec_cap) ? Q.irec + 8 * (size_t)i : nullptr;
         if (rec && (threadIdx.x & 63) == 0) {
             rec[4] = (uint32_t)wall_clock64(); rec[5] = rec[4];
             rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
             rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (1u << 8);
         }
-        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
-                       eps, max_ray_len, skey, scnt, stats, rec, 0, out, P.root);
+        trav_packet<W, false, PROF>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P,
+                                    (int64_t)q_w(it), P.slot, eps, max_ray_len, skey, scnt, stats, rec, 0, out, P.root);
     }
 }
 
@@ -721,7 +724,7 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_trav(RaysIn R, const float *__r
                 }
             }
         }
-        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
+        trav_packet<W, true, true>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
                        eps, max_ray_len, skey, scnt, stats, rec, 0, SpillArgs{nullptr, nullptr, 0u, 0, 31},
                        P.root, Q);
     };

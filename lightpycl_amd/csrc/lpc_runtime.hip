@@ -123,6 +123,7 @@ struct lpc_handle {
     float slots_mrl = 0.0f;
     bool misc_clean = false;                        // the launch words were reset for the next launch
     bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
+    int walk_waves = 6;                             // LPC_WALK_WAVES: k_rootwalk / k_spill launch bounds (6-8 waves/SIMD)
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -829,16 +830,28 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
         const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
         const int wpb = h->spill_wpb;
         const unsigned g = sb * 4u / (unsigned)wpb;
-#define LPC_LAUNCH_SPILL(WW, PB, NT)                                                                             \
-    hipLaunchKernelGGL((k_spill<WW, PB>), dim3(g), dim3(64 * PB), 0, h->stream, in, rs, n, perm,                 \
+#define LPC_LAUNCH_SPILL(WW, PB, NT, PF)                                                                         \
+    hipLaunchKernelGGL((k_spill<WW, PB, PF>), dim3(g), dim3(64 * PB), 0, h->stream, in, rs, n, perm,             \
                        (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
                        I, O)
-        if (h->built_w == 8) {
-            if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8);
-            else LPC_LAUNCH_SPILL(8, 1, Node8);
+        // profiling counters only in the PROF instantiation (fewer live registers without)
+        if (stats) {
+            if (h->built_w == 8) { if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8, true); else LPC_LAUNCH_SPILL(8, 1, Node8, true); }
+            else { if (wpb == 4) LPC_LAUNCH_SPILL(4, 4, Node4, true); else LPC_LAUNCH_SPILL(4, 1, Node4, true); }
         } else {
-            if (wpb == 4) LPC_LAUNCH_SPILL(4, 4, Node4);
-            else LPC_LAUNCH_SPILL(4, 1, Node4);
+            if (h->built_w == 8) {
+                if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8, false);
+                else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
+                    hipLaunchKernelGGL((k_spill<8, 1, false, 7>), dim3(g), dim3(64), 0, h->stream, in, rs, n, perm,
+                                       (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
+                                       skey, scnt, stats, I, O);
+                else if (h->walk_waves == 8)
+                    hipLaunchKernelGGL((k_spill<8, 1, false, 8>), dim3(g), dim3(64), 0, h->stream, in, rs, n, perm,
+                                       (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
+                                       skey, scnt, stats, I, O);
+                else LPC_LAUNCH_SPILL(8, 1, Node8, false);
+            }
+            else { if (wpb == 4) LPC_LAUNCH_SPILL(4, 4, Node4, false); else LPC_LAUNCH_SPILL(4, 1, Node4, false); }
         }
 #undef LPC_LAUNCH_SPILL
     }
@@ -950,16 +963,27 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
         // event packets between the kernels
         if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
-#define LPC_LAUNCH_WALK(WW, PB, NT)                                                                              \
-    hipExtLaunchKernelGGL((k_rootwalk<WW, PB>), dim3(grid), dim3(64 * PB), 0, h->stream, k0, k1, 0, in, rs, n,    \
+#define LPC_LAUNCH_WALK(WW, PB, NT, PF)                                                                          \
+    hipExtLaunchKernelGGL((k_rootwalk<WW, PB, PF>), dim3(grid), dim3(64 * PB), 0, h->stream, k0, k1, 0, in, rs, n, \
                           perm, (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,   \
                           scnt, stats, Q, SP)
-        if (h->built_w == 8) {
-            if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8);
-            else LPC_LAUNCH_WALK(8, 1, Node8);
+        if (stats || Q.irec) {
+            if (h->built_w == 8) { if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8, true); else LPC_LAUNCH_WALK(8, 1, Node8, true); }
+            else { if (wpb == 4) LPC_LAUNCH_WALK(4, 4, Node4, true); else LPC_LAUNCH_WALK(4, 1, Node4, true); }
         } else {
-            if (wpb == 4) LPC_LAUNCH_WALK(4, 4, Node4);
-            else LPC_LAUNCH_WALK(4, 1, Node4);
+            if (h->built_w == 8) {
+                if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8, false);
+                else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
+                    hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 7>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
+                                          in, rs, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
+                                          eps, max_ray_len, skey, scnt, stats, Q, SP);
+                else if (h->walk_waves == 8)
+                    hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 8>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
+                                          in, rs, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
+                                          eps, max_ray_len, skey, scnt, stats, Q, SP);
+                else LPC_LAUNCH_WALK(8, 1, Node8, false);
+            }
+            else { if (wpb == 4) LPC_LAUNCH_WALK(4, 4, Node4, false); else LPC_LAUNCH_WALK(4, 1, Node4, false); }
         }
 #undef LPC_LAUNCH_WALK
         if (h->prof) h->ev_kern.push_back({k0, k1});
@@ -1349,6 +1373,11 @@ int lpc_open(int device, lpc_handle **out)
     }
     int rc = dalloc(h, h->d_acc, sizeof(DevAcc));
     if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
+    if (hipMemset(h->d_acc.p, 0, sizeof(DevAcc)) != hipSuccess) {    // counters start empty (qerr 0)
+        g_open_err = "counter init";
+        lpc_close(h);
+        return LPC_E_HIP;
+    }
     // launch-policy overrides (A/B measurements; results do not depend on them)
     auto env_int = [](const char *k, int64_t dflt) -> int64_t {
         const char *v = getenv(k);
@@ -1362,6 +1391,7 @@ int lpc_open(int device, lpc_handle **out)
     h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
     h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
     h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
+    h->walk_waves = (int)std::min<int64_t>(8, std::max<int64_t>(6, env_int("LPC_WALK_WAVES", h->walk_waves)));
     h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
     h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
