@@ -156,6 +156,25 @@ static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__
     }
 }
 
+// Ray loaders of the traversal: a population as RaysIn or the coherence copy
+// (RayPair, the general form), or as one base of 8 equally spaced arrays
+// (RayBase: fewer kernel arguments and live registers in k_rootwalk / k_spill).
+struct RayPair {
+    RaysIn R;
+    const float *rs;
+    int64_t n;
+    __device__ __forceinline__ void load(int64_t q, f3 &O, f3 &D) const { load_ray(R, rs, n, q, O, D); }
+};
+struct RayBase {
+    const float *b;                   // ox at b, oy at b + s, ... dz at b + 5 s
+    int64_t s;
+    __device__ __forceinline__ void load(int64_t q, f3 &O, f3 &D) const
+    {
+        O = mk3(b[q], b[s + q], b[2 * s + q]);
+        D = mk3(b[3 * s + q], b[4 * s + q], b[5 * s + q]);
+    }
+};
+
 // Stack depth per wave (node refs); the host checks every hierarchy fits.
 #define LPC_STACK 64
 
@@ -210,8 +229,8 @@ struct WaveLds {
 // QH: the persistent queue's hand-over to waiting waves (k_trav only); PROF:
 // the profiling counters / records and the LPC_DBG timing switches (compiled
 // out of the default launches: fewer live registers in the hot loop).
-template <int W, bool QH = false, bool PROF = true>
-static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, const float *__restrict__ rs,
+template <int W, bool QH = false, bool PROF = true, class RL = RayPair>
+static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                                                    int64_t n, const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
                                                    const ExactRec *__restrict__ xrec, GItem *__restrict__ gitems,
@@ -231,7 +250,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RaysIn &R, 
     const int lane = threadIdx.x & 63;
     const int64_t s = w * 64 + lane;
     f3 O, D;
-    load_ray(R, rs, n, s < n ? s : n - 1, O, D);
+    ray.load(s < n ? s : n - 1, O, D);
     // unit direction for the filter only (its rounding is inside the margin)
     const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
     const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
@@ -466,7 +485,8 @@ __global__ __launch_bounds__(256, MINB) void k_intersect(RaysIn R, const float *
     for (int p = p0; p < p1; ++p) {
         const Piece P = pieces[p];
         const int64_t slot = (int64_t)p * ((n + 63) / 64) + w;
-        trav_packet<W>(lds[wv], R, rs, n, perm, nodes, xrec, gitems, gcount, gmax, slot, P, w, p, eps, max_ray_len,
+        trav_packet<W>(lds[wv], RayPair{R, rs, n}, n, perm, nodes, xrec, gitems, gcount, gmax, slot, P, w, p, eps,
+                       max_ray_len,
                     skey, scnt, stats, wrec, slot, SP);
     }
 }
@@ -518,7 +538,7 @@ __global__ __launch_bounds__(256) void k_lane(RaysIn R, const float *__restrict_
 // groups (the host checks).
 // WPB waves per block (1: a wave's slot frees when its items end, see k_rootwalk).
 template <int W, int WPB, bool PROF = false, int MINW = 6>
-__global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RaysIn R, const float *__restrict__ rs, int64_t n,
+__global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RayBase ray, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
@@ -535,7 +555,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RaysIn R, const float 
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
-        trav_packet<W, false, PROF>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
+        trav_packet<W, false, PROF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
                     max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
     }
 }
@@ -644,7 +664,7 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
 // item ends, where a 4-wave block holds its LDS until its slowest item ends
 // (per-item records: ~2 800 of 6 144 wave slots walking on average with 4).
 template <int W, int WPB, bool PROF = false, int MINW = 6>
-__global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RaysIn R, const float *__restrict__ rs, int64_t n,
+__global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -675,7 +695,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RaysIn R, const flo
             rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
             rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (1u << 8);
         }
-        trav_packet<W, false, PROF>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P,
+        trav_packet<W, false, PROF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P,
                                     (int64_t)q_w(it), P.slot, eps, max_ray_len, skey, scnt, stats, rec, 0, out, P.root);
     }
 }
@@ -724,7 +744,7 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_trav(RaysIn R, const float *__r
                 }
             }
         }
-        trav_packet<W, true, true>(lds[wv], R, rs, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
+        trav_packet<W, true, true>(lds[wv], RayPair{R, rs, n}, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
                        eps, max_ray_len, skey, scnt, stats, rec, 0, SpillArgs{nullptr, nullptr, 0u, 0, 31},
                        P.root, Q);
     };

@@ -809,6 +809,19 @@ static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
     return 0;
 }
 
+// The rays of a launch as one base of 8 equally spaced arrays (RayBase): the
+// coherence copy (stride n) or a population / staging buffer (stride = its
+// capacity).  Every RaysIn the runtime builds has this shape.
+static int ray_base(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, RayBase *out)
+{
+    if (rs) { *out = RayBase{rs, n}; return 0; }
+    const int64_t st = in.oy - in.ox;
+    if (in.oz - in.oy != st || in.dx - in.oz != st || in.dy - in.dx != st || in.dz - in.dy != st)
+        return set_err(h, LPC_E_ARG, "internal: ray arrays not equally spaced");
+    *out = RayBase{in.ox, st};
+    return 0;
+}
+
 // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
 // what exceeds the budget for level l + 1; the last level finishes
 static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
@@ -816,6 +829,8 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
                             unsigned long long *stats, const SpillArgs &SP)
 {
     uint32_t *misc = (uint32_t *)h->d_misc.p;
+    RayBase ray;
+    RETIF(ray_base(h, in, rs, n, &ray));
     const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
     const int levels = SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
     for (int l = 0; l < levels; ++l) {
@@ -831,7 +846,7 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
         const int wpb = h->spill_wpb;
         const unsigned g = sb * 4u / (unsigned)wpb;
 #define LPC_LAUNCH_SPILL(WW, PB, NT, PF)                                                                         \
-    hipLaunchKernelGGL((k_spill<WW, PB, PF>), dim3(g), dim3(64 * PB), 0, h->stream, in, rs, n, perm,             \
+    hipLaunchKernelGGL((k_spill<WW, PB, PF>), dim3(g), dim3(64 * PB), 0, h->stream, ray, n, perm,                \
                        (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
                        I, O)
         // profiling counters only in the PROF instantiation (fewer live registers without)
@@ -842,11 +857,11 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
             if (h->built_w == 8) {
                 if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8, false);
                 else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
-                    hipLaunchKernelGGL((k_spill<8, 1, false, 7>), dim3(g), dim3(64), 0, h->stream, in, rs, n, perm,
+                    hipLaunchKernelGGL((k_spill<8, 1, false, 7>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
                                        (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
                                        skey, scnt, stats, I, O);
                 else if (h->walk_waves == 8)
-                    hipLaunchKernelGGL((k_spill<8, 1, false, 8>), dim3(g), dim3(64), 0, h->stream, in, rs, n, perm,
+                    hipLaunchKernelGGL((k_spill<8, 1, false, 8>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
                                        (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
                                        skey, scnt, stats, I, O);
                 else LPC_LAUNCH_SPILL(8, 1, Node8, false);
@@ -955,6 +970,8 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
+        RayBase ray;
+        RETIF(ray_base(h, in, rs, n, &ray));
         SpillArgs SP;
         RETIF(spill_setup(h, n, &SP));
         // the grid in waves (LPC_Q_WALK_BLOCKS x 4), in blocks of q_walk_wpb waves
@@ -964,7 +981,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         // event packets between the kernels
         if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
 #define LPC_LAUNCH_WALK(WW, PB, NT, PF)                                                                          \
-    hipExtLaunchKernelGGL((k_rootwalk<WW, PB, PF>), dim3(grid), dim3(64 * PB), 0, h->stream, k0, k1, 0, in, rs, n, \
+    hipExtLaunchKernelGGL((k_rootwalk<WW, PB, PF>), dim3(grid), dim3(64 * PB), 0, h->stream, k0, k1, 0, ray, n,    \
                           perm, (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,   \
                           scnt, stats, Q, SP)
         if (stats || Q.irec) {
@@ -975,11 +992,11 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
                 if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8, false);
                 else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
                     hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 7>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
-                                          in, rs, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
+                                          ray, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
                                           eps, max_ray_len, skey, scnt, stats, Q, SP);
                 else if (h->walk_waves == 8)
                     hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 8>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
-                                          in, rs, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
+                                          ray, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
                                           eps, max_ray_len, skey, scnt, stats, Q, SP);
                 else LPC_LAUNCH_WALK(8, 1, Node8, false);
             }
