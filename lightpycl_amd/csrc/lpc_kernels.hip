@@ -229,7 +229,7 @@ struct WaveLds {
 // QH: the persistent queue's hand-over to waiting waves (k_trav only); PROF:
 // the profiling counters / records and the LPC_DBG timing switches (compiled
 // out of the default launches: fewer live registers in the hot loop).
-template <int W, bool QH = false, bool PROF = true, class RL = RayPair>
+template <int W, bool QH = false, bool PROF = true, class RL = RayPair, bool HALF = false>
 static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                                                    int64_t n, const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
@@ -354,9 +354,12 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
         float d[W];
 #pragma unroll
         for (int k = 0; k < W; k += 2) {
-            const lpc_f2 r = filter_test2(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
-                                          lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
-                                          lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz);
+            const lpc_f2 r = HALF ? filter_test2h(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
+                                                  lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
+                                                  lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz)
+                                  : filter_test2(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
+                                                 lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
+                                                 lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz);
             d[k] = r.x;
             d[k + 1] = r.y;
         }
@@ -537,7 +540,7 @@ __global__ __launch_bounds__(256) void k_lane(RaysIn R, const float *__restrict_
 // level's queue (`out`; budget 0 on the last level).  Only used without fan
 // groups (the host checks).
 // WPB waves per block (1: a wave's slot frees when its items end, see k_rootwalk).
-template <int W, int WPB, bool PROF = false, int MINW = 6>
+template <int W, int WPB, bool PROF = false, int MINW = 6, bool HALF = false>
 __global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RayBase ray, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -555,7 +558,8 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RayBase ray, int64_t n
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
-        trav_packet<W, false, PROF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w, I.piece, eps,
+        trav_packet<W, false, PROF, RayBase, HALF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w,
+                                                   I.piece, eps,
                     max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
     }
 }
@@ -663,7 +667,7 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
 // WPB waves per block: 1 by default -- a block's slots free as soon as its one
 // item ends, where a 4-wave block holds its LDS until its slowest item ends
 // (per-item records: ~2 800 of 6 144 wave slots walking on average with 4).
-template <int W, int WPB, bool PROF = false, int MINW = 6>
+template <int W, int WPB, bool PROF = false, int MINW = 6, bool HALF = false>
 __global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
@@ -695,7 +699,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_
             rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
             rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (1u << 8);
         }
-        trav_packet<W, false, PROF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P,
+        trav_packet<W, false, PROF, RayBase, HALF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P,
                                     (int64_t)q_w(it), P.slot, eps, max_ray_len, skey, scnt, stats, rec, 0, out, P.root);
     }
 }

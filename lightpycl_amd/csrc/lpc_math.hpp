@@ -314,6 +314,28 @@ LPC_HD lpc_f2 filter_test2(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2 
     return pp + (negA + negB * ww);
 }
 
+// filter_test2 with the half-line cull (LPC_HALF): a record whose test sphere
+// (radius^2 = A + B |w|^2) lies wholly behind the ray origin by a margin is
+// failed (+1): wn = w.n < 0 and wn^2 > 2 (A + B ww) + LPC_HALF_MU2 ww.  Moller-
+// Trumbore accepts such a triangle with t > eps only through rounding on rays
+// nearly parallel to its plane (scope of the filter proof).
+#define LPC_HALF_MU2 8e-4f
+LPC_HD lpc_f2 filter_test2h(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2 negA, float ox, float oy,
+                            float oz, float nx, float ny, float nz)
+{
+    const lpc_f2 wx = cx - ox, wy = cy - oy, wz = cz - oz;
+    const lpc_f2 px = wy * nz - wz * ny, py = wz * nx - wx * nz, pz = wx * ny - wy * nx;
+    const lpc_f2 pp = px * px + py * py + pz * pz;
+    const lpc_f2 ww = wx * wx + wy * wy + wz * wz;
+    const lpc_f2 q = negA + negB * ww;                       // -(A + B ww)
+    const lpc_f2 wn = wx * nx + wy * ny + wz * nz;
+    const lpc_f2 b = wn * wn + (q + q) - LPC_HALF_MU2 * ww;  // > 0: sphere behind, clear of the origin
+    lpc_f2 d = pp + q;
+    if (wn.x < 0.0f && b.x > 0.0f) d.x = 1.0f;
+    if (wn.y < 0.0f && b.y > 0.0f) d.y = 1.0f;
+    return d;
+}
+
 // Float-evaluation slack of filter_test, both ways (factor on A and B, and an
 // absolute term on B = (1 + 1/h') 49 eps^2 with h' = 1e-3, rounded up).
 #define LPC_FILT_REL 2e-3

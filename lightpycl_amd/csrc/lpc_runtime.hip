@@ -124,6 +124,8 @@ struct lpc_handle {
     bool misc_clean = false;                        // the launch words were reset for the next launch
     bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
     int walk_waves = 6;                             // LPC_WALK_WAVES: k_rootwalk / k_spill launch bounds (6-8 waves/SIMD)
+    int half = 0;                                   // LPC_HALF: half-line node cull (1: not for emitted rays, 2: all)
+    bool half_now = false;                          // ... for the launch in progress
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -856,6 +858,10 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
         } else {
             if (h->built_w == 8) {
                 if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8, false);
+                else if (h->half_now)             // the half-line cull (LPC_HALF)
+                    hipLaunchKernelGGL((k_spill<8, 1, false, 6, true>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
+                                       (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
+                                       skey, scnt, stats, I, O);
                 else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
                     hipLaunchKernelGGL((k_spill<8, 1, false, 7>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
                                        (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
@@ -990,6 +996,10 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         } else {
             if (h->built_w == 8) {
                 if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8, false);
+                else if (h->half_now)             // the half-line cull (LPC_HALF)
+                    hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 6, true>), dim3(grid), dim3(64), 0, h->stream, k0,
+                                          k1, 0, ray, n, perm, (const Node8 *)h->d_nodes.p,
+                                          (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, Q, SP);
                 else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
                     hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 7>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
                                           ray, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
@@ -1059,6 +1069,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // the clean state (max_ray_len, idx -1, count 0), so once the whole slot array
     // is clean no slot needs a reset; only the launch words do (k_stage_move
     // reset them for the next launch; the emitted rays' k_raykey does).
+    h->half_now = h->half == 2 || (h->half == 1 && !(traced && h->pop_emitted));
     const bool restore = traced && h->fuse_compact;
     const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
     const bool misc_clean = restore && h->misc_clean;
@@ -1409,6 +1420,7 @@ int lpc_open(int device, lpc_handle **out)
     h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
     h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
     h->walk_waves = (int)std::min<int64_t>(8, std::max<int64_t>(6, env_int("LPC_WALK_WAVES", h->walk_waves)));
+    h->half = (int)env_int("LPC_HALF", h->half);
     h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
     h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
