@@ -149,6 +149,7 @@ struct ShadeArgs {
     ShadeOutPtrs o;
 };
 
+#define LPC_MP_MAX 4                      // measure meshes whose power the traced path sums per tile
 struct DevAcc {                       // device-side counters of one iteration
     unsigned long long nR, nT;        // kept reflected / refracted (running within iteration)
     unsigned long long m_total;       // measured record length (persistent)
@@ -158,6 +159,7 @@ struct DevAcc {                       // device-side counters of one iteration
     unsigned int qerr;                // k_trav gave up waiting on its work queue (QueueArgs::err)
     unsigned int seq;                 // host copy only: iteration number, written last (k_scan)
     unsigned int pad;
+    double mpow[LPC_MP_MAX];          // traced path: measured power of the trace so far per measure mesh
 };
 
 struct SlotInit {                     // per-mesh slot initial state of a launch (k_slot_init)
@@ -203,6 +205,9 @@ struct StageArgs {
     uint32_t *tdm;                    // [ntiles] max |dir|^2 (float bits) of kept children
     unsigned long long *skey;         // the slots read by the shading, restored to the clean state
     int32_t *scnt;                    //   (key slot_key(max_ray_len, -1), count 0) after the read
+    int nmp;                          // measure meshes summed per tile (<= LPC_MP_MAX; 0: none)
+    int32_t mpm[LPC_MP_MAX];          // their mesh ids
+    double *tmp;                      // [ntiles][LPC_MP_MAX] measured power per tile and measure mesh
 };
 struct MoveArgs {
     int64_t ntiles;
@@ -220,6 +225,9 @@ struct MoveArgs {
     DevAcc *host_acc;                 // mapped pinned host copy (or NULL)
     unsigned int seq;
     uint32_t *misc;                   // the next launch's words (LPC_MISC_WORDS), reset here
+    int nmp;                          // measure meshes summed per tile (StageArgs)
+    const double *tmp;
+    double *mrun;                     // [LPC_MP_MAX] the trace's running sums (own buffer: counter resets keep it)
 };
 
 // Order chaining (k_ocount / k_oscan / k_oscatter): the next population's

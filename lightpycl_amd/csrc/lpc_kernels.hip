@@ -1652,6 +1652,7 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
 // kernels ([reflected ; refracted], each in parent order).
 __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
 {
+    __shared__ double s_mp[LPC_MP_MAX][LPC_ST_TILE / 64];
     __shared__ int32_t s_w[3][LPC_ST_TILE / 64];
     __shared__ double s_pow[LPC_ST_TILE / 64];
     __shared__ float s_dm[LPC_ST_TILE / 64];
@@ -1700,6 +1701,11 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     }
     pk = wave_sum(pk);
     dm = wave_max(dm);
+    // measured power per measure mesh (fixed order: waves, then tiles in k_stage_move)
+    for (int m = 0; m < A.nmp; ++m) {
+        const double v = wave_sum((fM && po.hit_mesh == A.mpm[m]) ? (double)s.pow : 0.0);
+        if (lane == 0) s_mp[m][wv] = v;
+    }
     if (lane == 0) {
         s_w[0][wv] = __popcll(bR); s_w[1][wv] = __popcll(bT); s_w[2][wv] = __popcll(bM);
         s_pow[wv] = pk; s_dm[wv] = dm;
@@ -1708,6 +1714,11 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     int32_t wo[3] = {0, 0, 0};
     for (int w = 0; w < wv; ++w)
         for (int f = 0; f < 3; ++f) wo[f] += s_w[f][w];
+    if (threadIdx.x < A.nmp) {
+        double v = 0.0;
+        for (int k = 0; k < LPC_ST_TILE / 64; ++k) v += s_mp[threadIdx.x][k];
+        A.tmp[tile * LPC_MP_MAX + threadIdx.x] = v;
+    }
     const int64_t c = A.cst, t0 = tile * LPC_ST_TILE;
     auto put = [&](float *b, int64_t q, f3 d, float pw) {
         b[q] = dest.x; b[c + q] = dest.y; b[2 * c + q] = dest.z;
@@ -1741,6 +1752,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     __shared__ long long s_pre[3], s_tot[3];
     __shared__ double s_p[LPC_ST_TILE];
     __shared__ float s_d[LPC_ST_TILE];
+    __shared__ double s_m[LPC_MP_MAX][LPC_ST_TILE];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t tile = blockIdx.x;
     // this tile's prefix and the totals, from all tile counts (4 B each)
@@ -1769,19 +1781,32 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     __syncthreads();
     if (tile == 0) {
         // iteration counters: fixed-order power sum, max |dir|^2
-        double lp = 0.0;
+        double lp = 0.0, lm[LPC_MP_MAX] = {0.0, 0.0, 0.0, 0.0};
         float ld = 0.0f;
-        for (int64_t j = t; j < A.ntiles; j += LPC_ST_TILE) { lp += A.tpow[j]; ld = fmaxf(ld, __uint_as_float(A.tdm[j])); }
+        for (int64_t j = t; j < A.ntiles; j += LPC_ST_TILE) {
+            lp += A.tpow[j];
+            ld = fmaxf(ld, __uint_as_float(A.tdm[j]));
+            for (int m = 0; m < A.nmp; ++m) lm[m] += A.tmp[j * LPC_MP_MAX + m];
+        }
         s_p[t] = lp;
         s_d[t] = ld;
+        for (int m = 0; m < LPC_MP_MAX; ++m) s_m[m][t] = lm[m];
         for (int off = LPC_ST_TILE / 2; off >= 1; off >>= 1) {
             __syncthreads();
-            if (t < off) { s_p[t] += s_p[t + off]; s_d[t] = fmaxf(s_d[t], s_d[t + off]); }
+            if (t < off) {
+                s_p[t] += s_p[t + off];
+                s_d[t] = fmaxf(s_d[t], s_d[t + off]);
+                for (int m = 0; m < LPC_MP_MAX; ++m) s_m[m][t] += s_m[m][t + off];
+            }
         }
         __syncthreads();
         if (t == 0) {
             DevAcc a;
             memset(&a, 0, sizeof(a));
+            for (int m = 0; m < A.nmp; ++m) {         // the trace's running sums, in iteration order
+                A.mrun[m] = (A.m_base == 0 ? 0.0 : A.mrun[m]) + s_m[m][0];
+                a.mpow[m] = A.mrun[m];
+            }
             a.nR = (unsigned long long)s_tot[0]; a.nT = (unsigned long long)s_tot[1];
             a.m_total = A.m_base + (unsigned long long)s_tot[2];
             a.nM_iter = (unsigned long long)s_tot[2];
@@ -1801,6 +1826,9 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&o->dmax2_bits, a.dmax2_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&o->qerr, a.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                for (int m = 0; m < A.nmp; ++m)
+                    __hip_atomic_store((unsigned long long *)&o->mpow[m], __double_as_longlong(a.mpow[m]),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(&o->seq, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }

@@ -191,6 +191,9 @@ struct lpc_handle {
     double host_last = 0.0, t_first = 0.0;
     int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     bool pop_init = false;                          // the population is I (the emitted rays, set_rays)
+    bool mp_valid = false;                          // mp_last = the trace's measured power per measure mesh
+    DBuf d_mrun;                                    // its running sums on the device (k_stage_move)
+    double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;
     int64_t n_cur = 0, n_init = 0;
@@ -734,7 +737,8 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_sort_tmp, tb));
         RETIF(dalloc(h, h->w_keypart, (size_t)((C + 255) / 256) * 16 + 64 * 4));
         const int64_t nt = (C + LPC_ST_TILE - 1) / LPC_ST_TILE;
-        RETIF(dalloc(h, h->w_fc, (size_t)nt * (8 + 4 + 4) + 64));       // staging tiles' power, counts, max |dir|^2
+        RETIF(dalloc(h, h->w_fc, (size_t)nt * (8 + 4 + 4 + 8 * LPC_MP_MAX) + 64));   // staging tiles' power, counts,
+                                                                                      // max |dir|^2, measured power
 
         h->slots_clean = h->misc_clean = false;         // fresh slot arrays
         h->sort_tmp_bytes = tb;
@@ -1401,6 +1405,8 @@ int lpc_open(int device, lpc_handle **out)
     }
     int rc = dalloc(h, h->d_acc, sizeof(DevAcc));
     if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
+    rc = dalloc(h, h->d_mrun, LPC_MP_MAX * sizeof(double));
+    if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
     if (hipMemset(h->d_acc.p, 0, sizeof(DevAcc)) != hipSuccess) {    // counters start empty (qerr 0)
         g_open_err = "counter init";
         lpc_close(h);
@@ -1503,7 +1509,7 @@ int lpc_close(lpc_handle *h)
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_qroots, &h->d_qdq, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
-                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1], &h->w_fc};
+                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1], &h->w_fc, &h->d_mrun};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1886,6 +1892,7 @@ int lpc_trace_reset(lpc_handle *h)
     // the first iteration reads the emitted rays where set_rays put them (I is
     // never written by an iteration: no copy)
     h->pop_init = true;
+    h->mp_valid = true;                             // until an iteration does not sum it
     h->n_cur = h->n_init;
     h->pop_traced = false;
     h->pop_emitted = true;
@@ -1966,6 +1973,7 @@ static int wait_mapped_acc(lpc_handle *h, DevAcc *out)
     out->nR = m->nR; out->nT = m->nT; out->m_total = m->m_total; out->nM_iter = m->nM_iter;
     out->pow_next = m->pow_next; out->dmax2_bits = m->dmax2_bits; out->qerr = m->qerr;
     out->seq = m->seq; out->pad = 0;
+    for (int k = 0; k < LPC_MP_MAX; ++k) out->mpow[k] = m->mpow[k];
     return 0;
 }
 
@@ -2007,6 +2015,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (early) ++h->acc_seq;
     // traced single chunk: k_shade_stage + k_stage_move
     const bool fused = traced && h->fuse_compact && C >= N;
+    bool mp_fused = false;                  // this iteration summed the measured power per mesh
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         RaysIn in = (h->pop_init ? h->I : h->A).in(base);
@@ -2050,6 +2059,10 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             G.tdm = G.tcnt + nt;
             G.skey = (unsigned long long *)h->w_key.p;
             G.scnt = (int32_t *)h->w_sc.p;
+            // measured power per measure mesh summed on the way (no k_mesh_sum at the trace end)
+            G.nmp = h->meas_meshes.size() <= (size_t)LPC_MP_MAX ? (int)h->meas_meshes.size() : 0;
+            for (int m = 0; m < LPC_MP_MAX; ++m) G.mpm[m] = m < G.nmp ? h->meas_meshes[(size_t)m] : -1;
+            G.tmp = (double *)(G.tdm + nt);             // 16 nt bytes in: 8-aligned
 
             hipLaunchKernelGGL(k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, G);
             MoveArgs M;
@@ -2063,6 +2076,10 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             M.host_acc = A.host_acc;
             M.seq = A.seq;
             M.misc = (uint32_t *)h->d_misc.p;
+            M.nmp = G.nmp;
+            M.tmp = G.tmp;
+            M.mrun = (double *)h->d_mrun.p;
+            mp_fused = G.nmp > 0 || h->meas_meshes.empty();
             hipLaunchKernelGGL(k_stage_move, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
             h->slots_clean = true;              // k_shade_stage restored what it read
             h->slots_mrl = h->max_ray_len;
@@ -2158,6 +2175,9 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     h->order_n = nR + nT;
     h->split = nR;
     h->m_total = (int64_t)acc.m_total;
+    // the running per-mesh measured power stays valid while every iteration sums it
+    h->mp_valid = h->mp_valid && mp_fused;
+    if (h->mp_valid) memcpy(h->mp_last, acc.mpow, sizeof(h->mp_last));
     S.n_reflect = nR; S.n_refract = nT; S.n_measured = (int64_t)acc.nM_iter;
     S.power_next = acc.pow_next;
     float dm2;
@@ -2172,6 +2192,10 @@ static int mesh_power(lpc_handle *h, double *out)
 {
     for (int32_t j = 0; j < h->K; ++j) out[j] = 0.0;
     if (h->m_total == 0) return 0;
+    if (h->mp_valid && h->meas_meshes.size() <= (size_t)LPC_MP_MAX) {   // summed per tile by the traced iterations
+        for (size_t m = 0; m < h->meas_meshes.size(); ++m) out[h->meas_meshes[m]] = h->mp_last[m];
+        return 0;
+    }
     const int64_t nb = (h->m_total + LPC_MSUM_TILE - 1) / LPC_MSUM_TILE;
     RETIF(dalloc(h, h->d_tmp, (size_t)nb * 8));
     std::vector<double> part((size_t)nb);

@@ -381,7 +381,7 @@ def test_fused_compaction_equals_four_kernels(monkeypatch, name, n):
             e.close()
     a, b = out
     assert a[0] == b[0] and a[1] == b[1]
-    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)     # per-tile vs record-order float64 sums
     for x, y in zip(a[3:6], b[3:6]):
         np.testing.assert_array_equal(x, y)
     np.testing.assert_allclose(a[6], b[6], rtol=1e-12)
