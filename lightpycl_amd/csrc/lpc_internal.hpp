@@ -208,7 +208,13 @@ struct StageArgs {
     int nmp;                          // measure meshes summed per tile (<= LPC_MP_MAX; 0: none)
     int32_t mpm[LPC_MP_MAX];          // their mesh ids
     double *tmp;                      // [ntiles][LPC_MP_MAX] measured power per tile and measure mesh
+    unsigned long long *gsum;         // per group of LPC_ST_GROUP tiles: counts (21 bits each), zero before
 };
+#define LPC_ST_GROUP 256                  // tiles per count group (k_stage_move prefixes: groups, then tiles)
+__host__ __device__ inline unsigned long long gsum_pack(uint32_t r, uint32_t t, uint32_t m)
+{
+    return (unsigned long long)r | ((unsigned long long)t << 21) | ((unsigned long long)m << 42);
+}
 struct MoveArgs {
     int64_t ntiles;
     const float *stR, *stT, *stM;
@@ -228,6 +234,10 @@ struct MoveArgs {
     int nmp;                          // measure meshes summed per tile (StageArgs)
     const double *tmp;
     double *mrun;                     // [LPC_MP_MAX] the trace's running sums (own buffer: counter resets keep it)
+    const unsigned long long *gsum;   // group counts of this launch (StageArgs::gsum)
+    int64_t ngroups;
+    unsigned long long *gsum_next;    // the next launch's group counts: its first gdirty_next (left by the
+    int64_t gdirty_next;              //   launch before this one) zeroed here
 };
 
 // Order chaining (k_ocount / k_oscan / k_oscatter): the next population's

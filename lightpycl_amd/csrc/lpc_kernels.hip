@@ -572,7 +572,8 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RayBase ray, int64_t n
 // packet's rays (read from LDS: broadcast), so the tests pipeline without a
 // ballot per test; one claim atomic per block and 64-piece chunk.
 __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                               const Piece *__restrict__ pieces, int npieces, QueueArgs Q)
+                                               const Piece *__restrict__ pieces, int npieces, QueueArgs Q,
+                                               int half)
 {
     __shared__ float s_ray[4][6][64];
     __shared__ uint32_t s_cnt[4];
@@ -596,8 +597,10 @@ __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict
         bool pass = false;
         if (live && p < npieces && P.root >= 0) {
             for (int r = 0; r < 64; ++r) {
-                const float d = filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, s_ray[wv][0][r], s_ray[wv][1][r],
-                                            s_ray[wv][2][r], s_ray[wv][3][r], s_ray[wv][4][r], s_ray[wv][5][r]);
+                const float d = half ? filter_testh(P.cx, P.cy, P.cz, P.negB, P.negA, s_ray[wv][0][r], s_ray[wv][1][r],
+                                                    s_ray[wv][2][r], s_ray[wv][3][r], s_ray[wv][4][r], s_ray[wv][5][r])
+                                     : filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, s_ray[wv][0][r], s_ray[wv][1][r],
+                                                   s_ray[wv][2][r], s_ray[wv][3][r], s_ray[wv][4][r], s_ray[wv][5][r]);
                 pass = pass || d <= 0.0f;
             }
         }
@@ -623,7 +626,8 @@ __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict
 // loops over the pieces (one test and a ballot each); lane-per-piece would
 // leave most lanes idle through 64 ray iterations.  Same tests, same items.
 __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                 const Piece *__restrict__ pieces, int npieces, QueueArgs Q)
+                                                 const Piece *__restrict__ pieces, int npieces, QueueArgs Q,
+                                                 int half)
 {
     __shared__ uint32_t s_cnt[4];
     __shared__ uint32_t s_base;
@@ -641,8 +645,10 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     if (live)
         for (int p = 0; p < npieces; ++p) {
             if (bcasti(Pl.root, p) < 0) continue;
-            const float d = filter_test(bcast(Pl.cx, p), bcast(Pl.cy, p), bcast(Pl.cz, p), bcast(Pl.negB, p),
-                                        bcast(Pl.negA, p), O.x, O.y, O.z, nx, ny, nz);
+            const float d = half ? filter_testh(bcast(Pl.cx, p), bcast(Pl.cy, p), bcast(Pl.cz, p), bcast(Pl.negB, p),
+                                                bcast(Pl.negA, p), O.x, O.y, O.z, nx, ny, nz)
+                                 : filter_test(bcast(Pl.cx, p), bcast(Pl.cy, p), bcast(Pl.cz, p), bcast(Pl.negB, p),
+                                               bcast(Pl.negA, p), O.x, O.y, O.z, nx, ny, nz);
             if (any_lane(d <= 0.0f)) m |= 1ull << p;
         }
     if (lane == 0) s_cnt[wv] = (uint32_t)__builtin_popcountll(m);
@@ -1743,6 +1749,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
         A.tcnt[tile] = cR | (cT << 9) | (cM << 18);
         A.tpow[tile] = tp;
         A.tdm[tile] = __float_as_uint(td);
+        if (cR | cT | cM) atomicAdd(&A.gsum[tile / LPC_ST_GROUP], gsum_pack(cR, cT, cM));
     }
 }
 
@@ -1755,15 +1762,22 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     __shared__ double s_m[LPC_MP_MAX][LPC_ST_TILE];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t tile = blockIdx.x;
-    // this tile's prefix and the totals, from all tile counts (4 B each)
+    // this tile's prefix and the totals: the group counts (the groups before this
+    // tile's, all groups), then this group's tiles before it
     long long pre[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
-    for (int64_t j = t; j < A.ntiles; j += LPC_ST_TILE) {
-        const uint32_t v = A.tcnt[j];
-        const long long c[3] = {(long long)(v & 511u), (long long)((v >> 9) & 511u), (long long)((v >> 18) & 511u)};
+    const int64_t g = tile / LPC_ST_GROUP;
+    const unsigned long long m21 = (1ull << 21) - 1ull;
+    for (int64_t k = t; k < A.ngroups; k += LPC_ST_TILE) {
+        const unsigned long long v = A.gsum[k];
+        const long long c[3] = {(long long)(v & m21), (long long)((v >> 21) & m21), (long long)((v >> 42) & m21)};
         for (int f = 0; f < 3; ++f) {
             tot[f] += c[f];
-            if (j < tile) pre[f] += c[f];
+            if (k < g) pre[f] += c[f];
         }
+    }
+    for (int64_t j = g * LPC_ST_GROUP + t; j < tile; j += LPC_ST_TILE) {
+        const uint32_t v = A.tcnt[j];
+        pre[0] += v & 511u; pre[1] += (v >> 9) & 511u; pre[2] += (v >> 18) & 511u;
     }
     for (int f = 0; f < 3; ++f) {
         long long a = pre[f], b = tot[f];
@@ -1833,9 +1847,10 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
                 __hip_atomic_store(&o->seq, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
-        // the next launch's words (k_slot_init's misc reset)
+        // the next launch's words (k_slot_init's misc reset) and group counts
         if (A.misc)
             for (int i = t; i < LPC_MISC_WORDS; i += LPC_ST_TILE) A.misc[i] = i < 3 ? 0xffffffffu : 0u;
+        for (int64_t k = t; k < A.gdirty_next; k += LPC_ST_TILE) A.gsum_next[k] = 0ull;
     }
     // this tile's staged rows into place: kept children (two per thread at most,
     // loads of both issued before the stores), then measured rays

@@ -336,6 +336,20 @@ LPC_HD lpc_f2 filter_test2h(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2
     return d;
 }
 
+// filter_test with the half-line cull (filter_test2h, one record)
+LPC_HD float filter_testh(float cx, float cy, float cz, float negB, float negA, float ox, float oy, float oz,
+                          float nx, float ny, float nz)
+{
+    const float wx = cx - ox, wy = cy - oy, wz = cz - oz;
+    const float px = wy * nz - wz * ny, py = wz * nx - wx * nz, pz = wx * ny - wy * nx;
+    const float pp = px * px + py * py + pz * pz;
+    const float ww = wx * wx + wy * wy + wz * wz;
+    const float q = negA + negB * ww;
+    const float wn = wx * nx + wy * ny + wz * nz;
+    if (wn < 0.0f && wn * wn + (q + q) - LPC_HALF_MU2 * ww > 0.0f) return 1.0f;
+    return pp + q;
+}
+
 // Float-evaluation slack of filter_test, both ways (factor on A and B, and an
 // absolute term on B = (1 + 1/h') 49 eps^2 with h' = 1e-3, rounded up).
 #define LPC_FILT_REL 2e-3

@@ -119,13 +119,18 @@ struct lpc_handle {
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
+    DBuf w_gsum;                                    // per 256-tile group counts, two buffers (zero when unused)
+    int64_t gcap = 0;
+    int gpar = 0;                                   // the buffer the next traced launch uses
+    int64_t gdirty[2] = {0, 0};                     // groups a launch left non-zero in each buffer
     bool slots_clean = false;                       // every slot (max_ray_len slots_mrl, idx -1, count 0)
     float slots_mrl = 0.0f;
     bool misc_clean = false;                        // the launch words were reset for the next launch
     bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
     int walk_waves = 6;                             // LPC_WALK_WAVES: k_rootwalk / k_spill launch bounds (6-8 waves/SIMD)
-    int half = 0;                                   // LPC_HALF: half-line node cull (1: not for emitted rays, 2: all)
+    int half = 3;                                   // LPC_HALF: half-line cull (see run_intersect; 3: piece roots, not for emitted rays)
     bool half_now = false;                          // ... for the launch in progress
+    bool half_roots = false;                        // ... at the piece roots (k_roots)
     bool gather_aos = true;
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
@@ -739,6 +744,11 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         const int64_t nt = (C + LPC_ST_TILE - 1) / LPC_ST_TILE;
         RETIF(dalloc(h, h->w_fc, (size_t)nt * (8 + 4 + 4 + 8 * LPC_MP_MAX) + 64));   // staging tiles' power, counts,
                                                                                       // max |dir|^2, measured power
+        h->gcap = (nt + LPC_ST_GROUP - 1) / LPC_ST_GROUP + 1;                        // group counts, two launches'
+        RETIF(dalloc(h, h->w_gsum, (size_t)2 * h->gcap * 8));
+        HIPCHK(h, hipMemsetAsync(h->w_gsum.p, 0, h->w_gsum.bytes, h->stream));
+        h->gpar = 0;
+        h->gdirty[0] = h->gdirty[1] = 0;
 
         h->slots_clean = h->misc_clean = false;         // fresh slot arrays
         h->sort_tmp_bytes = tb;
@@ -974,10 +984,10 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     }
     if (pt->npieces <= 64)
         hipLaunchKernelGGL(k_roots_r, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
-                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
+                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
     else
         hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
-                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q);
+                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
         RayBase ray;
@@ -1073,7 +1083,11 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // the clean state (max_ray_len, idx -1, count 0), so once the whole slot array
     // is clean no slot needs a reset; only the launch words do (k_stage_move
     // reset them for the next launch; the emitted rays' k_raykey does).
-    h->half_now = h->half == 2 || (h->half == 1 && !(traced && h->pop_emitted));
+    // LPC_HALF 1 / 2: every node test (not for the emitted rays / for all); 3 / 4:
+    // the piece roots only (k_roots items), not for the emitted rays / for all
+    const bool emitted = traced && h->pop_emitted;
+    h->half_now = h->half == 2 || (h->half == 1 && !emitted);
+    h->half_roots = h->half_now || h->half == 4 || (h->half == 3 && !emitted);
     const bool restore = traced && h->fuse_compact;
     const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
     const bool misc_clean = restore && h->misc_clean;
@@ -1509,7 +1523,7 @@ int lpc_close(lpc_handle *h)
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_qroots, &h->d_qdq, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
-                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1], &h->w_fc, &h->d_mrun};
+                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1], &h->w_fc, &h->d_mrun, &h->w_gsum};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -2063,6 +2077,9 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             G.nmp = h->meas_meshes.size() <= (size_t)LPC_MP_MAX ? (int)h->meas_meshes.size() : 0;
             for (int m = 0; m < LPC_MP_MAX; ++m) G.mpm[m] = m < G.nmp ? h->meas_meshes[(size_t)m] : -1;
             G.tmp = (double *)(G.tdm + nt);             // 16 nt bytes in: 8-aligned
+            const int64_t ng = (nt + LPC_ST_GROUP - 1) / LPC_ST_GROUP;
+            unsigned long long *gs = (unsigned long long *)h->w_gsum.p;
+            G.gsum = gs + (size_t)h->gpar * (size_t)h->gcap;
 
             hipLaunchKernelGGL(k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, G);
             MoveArgs M;
@@ -2079,6 +2096,13 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             M.nmp = G.nmp;
             M.tmp = G.tmp;
             M.mrun = (double *)h->d_mrun.p;
+            M.gsum = G.gsum;
+            M.ngroups = ng;
+            M.gsum_next = gs + (size_t)(1 - h->gpar) * (size_t)h->gcap;
+            M.gdirty_next = h->gdirty[1 - h->gpar];
+            h->gdirty[1 - h->gpar] = 0;
+            h->gdirty[h->gpar] = ng;            // this launch's k_shade_stage adds into its first ng groups
+            h->gpar = 1 - h->gpar;
             mp_fused = G.nmp > 0 || h->meas_meshes.empty();
             hipLaunchKernelGGL(k_stage_move, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
             h->slots_clean = true;              // k_shade_stage restored what it read
