@@ -666,6 +666,66 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     }
 }
 
+// k_roots_s: k_roots_r's tests (lanes = a packet's rays, one ballot per piece)
+// as tasks: a block takes pb packets, task t = (packet t / S, piece class t % S)
+// tests the pieces p = class + S k (npieces <= 64 S), the block's 4 waves take
+// the tasks in turn, and the block reserves all its items with one atomic.
+// Small populations (few packets) get S = 2..4 waves per packet instead of one
+// wave looping over every piece; large ones several packets per atomic.
+// Same tests, same items as k_roots / k_roots_r (their order in the queue may
+// differ; the walk's results do not depend on it).
+#define LPC_ROOTS_TASKS 16
+__global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                 const Piece *__restrict__ pieces, int npieces, QueueArgs Q,
+                                                 int half, int S, int pb)
+{
+    __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
+    __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    const int ntask = S * pb;
+    for (int t = wv; t < ntask; t += 4) {
+        const int64_t w = (int64_t)blockIdx.x * pb + t / S;
+        const int cls = t % S;
+        uint64_t m = 0;
+        if (w * 64 < n) {
+            const int64_t s = w * 64 + lane;
+            f3 O, D;
+            load_ray(R, rs, n, s < n ? s : n - 1, O, D);
+            const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);   // as trav_packet
+            const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+            const int np = (npieces - cls + S - 1) / S;                       // this class's pieces
+            const Piece Pl = pieces[min(cls + S * lane, npieces - 1)];
+            for (int k = 0; k < np; ++k) {
+                if (bcasti(Pl.root, k) < 0) continue;
+                const float cx = bcast(Pl.cx, k), cy = bcast(Pl.cy, k), cz = bcast(Pl.cz, k);
+                const float nb = bcast(Pl.negB, k), na = bcast(Pl.negA, k);
+                const float d = half ? filter_testh(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz)
+                                     : filter_test(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz);
+                if (any_lane(d <= 0.0f)) m |= 1ull << k;
+            }
+        }
+        if (lane == 0) s_m[t] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int t = 0; t < ntask; ++t) { s_off[t] = tot; tot += (uint32_t)__builtin_popcountll(s_m[t]); }
+        s_off[ntask] = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(c), tot) : 0u;
+    }
+    __syncthreads();
+    const uint32_t base = s_off[ntask];
+    for (int t = wv; t < ntask; t += 4) {
+        const uint64_t m = s_m[t];
+        if (!((m >> lane) & 1ull)) continue;
+        const int64_t w = (int64_t)blockIdx.x * pb + t / S;
+        const int p = t % S + S * lane;
+        const uint32_t pos = base + s_off[t] + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (pos < Q.rcap)
+            Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)pieces[p].root, (uint32_t)pieces[p].slot);
+    }
+}
+
 // k_rootwalk: the root items (k_roots), grid-stride, one item per wave at a
 // time -- k_intersect's (packet, piece) waves without the waves whose root test
 // fails.  A wave that exceeds the hand-over budget queues its remaining
@@ -1349,6 +1409,9 @@ __global__ __launch_bounds__(256) void k_keypack(RaysIn R, int64_t n, float bx0,
 // k_shade: postproc + Fresnel for one ray per lane (exact arithmetic).
 // touched (optional): bit j set for slots j < 64 that hold anything but the clean
 // state (max_ray_len, idx -1, count 0), noted as postproc reads them
+// KU > 0 (A.K <= KU): the ray's K slots are loaded up front into registers (one
+// memory round trip instead of one per mesh and loop).
+template <int KU = 0>
 static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_t r, PostOut &po, f3 &dest,
                                                       uint64_t *touched = nullptr)
 {
@@ -1357,13 +1420,33 @@ static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_
     const int32_t prev = A.in.pmid[r];
     const int64_t n = A.n;
     const unsigned long long k0 = slot_key(A.max_ray_len, -1);
-    auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
-        const int64_t a = (int64_t)j * n + r;
-        const unsigned long long k = A.skey[a];
-        t = slot_key_t(k); i = slot_key_idx(k); c = A.sc[a];
-        if (touched && j < 64 && (k != k0 || c != 0)) *touched |= 1ull << j;
-    };
-    po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
+    if constexpr (KU > 0) {
+        unsigned long long kr[KU];
+        int32_t cr[KU];
+#pragma unroll
+        for (int j = 0; j < KU; ++j) {
+            kr[j] = k0; cr[j] = 0;
+            if (j < A.K) { kr[j] = A.skey[(int64_t)j * n + r]; cr[j] = A.sc[(int64_t)j * n + r]; }
+        }
+        if (touched) {
+            uint64_t m = 0;
+#pragma unroll
+            for (int j = 0; j < KU; ++j) m |= (kr[j] != k0 || cr[j] != 0) ? 1ull << j : 0ull;
+            *touched = m;
+        }
+        auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
+            t = slot_key_t(kr[j]); i = slot_key_idx(kr[j]); c = cr[j];
+        };
+        po = postproc<KU>(A.K, prev, A.mat_type, A.max_ray_len, slot);
+    } else {
+        auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
+            const int64_t a = (int64_t)j * n + r;
+            const unsigned long long k = A.skey[a];
+            t = slot_key_t(k); i = slot_key_idx(k); c = A.sc[a];
+            if (touched && j < 64 && (k != k0 || c != 0)) *touched |= 1ull << j;
+        };
+        po = postproc(A.K, prev, A.mat_type, A.max_ray_len, slot);
+    }
     dest = ray_dest(O, D, po.t_min);
     const int32_t meas_in = A.meas_in ? A.meas_in[r] : 0;
     auto tri = [&](int32_t idx, f3 &v0, f3 &v1, f3 &v2) {
@@ -1374,11 +1457,12 @@ static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_
                  A.refl, A.diss, A.ior_env, tri);
 }
 
+template <int KU = 0>
 static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t r)
 {
     PostOut po;
     f3 dest;
-    const ShadeOut s = shade_eval(A, r, po, dest);
+    const ShadeOut s = shade_eval<KU>(A, r, po, dest);
     A.o.destx[r] = dest.x; A.o.desty[r] = dest.y; A.o.destz[r] = dest.z;
     A.o.imid[r] = po.hit_mesh;
     A.o.pw[r] = s.pow;
@@ -1393,11 +1477,12 @@ static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t
     return s;
 }
 
+template <int KU>
 __global__ __launch_bounds__(256) void k_shade(ShadeArgs A)
 {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= A.n) return;
-    (void)shade_ray(A, r);
+    (void)shade_ray<KU>(A, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -1656,6 +1741,7 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
 //                  sum) and publishes them to the host.
 // Children and measured rays land at the same positions as with the four
 // kernels ([reflected ; refracted], each in parent order).
+template <int KU>
 __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
 {
     __shared__ double s_mp[LPC_MP_MAX][LPC_ST_TILE / 64];
@@ -1674,7 +1760,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     s.r_meas = -1; s.t_meas = -1;
     if (in) {
         uint64_t touched = 0;
-        s = shade_eval(A.S, r, po, dest, &touched);
+        s = shade_eval<KU>(A.S, r, po, dest, &touched);
         // the slots just read back to the clean state: those a flush wrote (noted
         // while postproc read them; slots 64 and up are read again)
         const unsigned long long k0 = slot_key(A.S.max_ray_len, -1);

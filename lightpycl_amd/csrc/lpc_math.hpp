@@ -82,10 +82,12 @@ LPC_HD void mt_accumulate(f3 O, f3 D, f3 V0, f3 E1, f3 E2, int32_t idx, float ep
 
 // ---------------------------------------------------------------------------
 // intersect_postproc (.cl:105-240) given the per-mesh (slot) results of one ray.
-// `slot(j, t, c)` must return slot j's min t and hit count.
+// `slot(j, t, c)` must return slot j's min t and hit count.  KU > 0 (K <= KU)
+// unrolls both mesh loops KU times, so a slot function over a register array
+// indexes it with constants.
 struct PostOut { int32_t hit_mesh, hit_idx, n1, n2, entering; float t_min; };
 
-template <class SlotFn>
+template <int KU = 0, class SlotFn>
 LPC_HD PostOut postproc(int32_t K, int32_t prev, const int32_t *mat_type, float max_ray_len,
                         SlotFn slot)
 {
@@ -95,10 +97,13 @@ LPC_HD PostOut postproc(int32_t K, int32_t prev, const int32_t *mat_type, float 
     o.hit_mesh = -1; o.hit_idx = -1; o.n1 = -1; o.n2 = -1; o.entering = -1;
     float t_min = max_ray_len;
     int32_t hit_cnt = 0;
-    for (int32_t j = 0; j < K; ++j) {                                   // .cl:127-135
+    constexpr int32_t KL = KU > 0 ? KU : 0x7fffffff;
+#pragma unroll
+    for (int32_t j = 0; j < KL; ++j) {                                  // .cl:127-135
+        if (KU == 0 && j >= K) break;
         float tj; int32_t cj, ij;
         slot(j, tj, cj, ij);
-        if (tj < t_min) { t_min = tj; o.hit_mesh = j; o.hit_idx = ij; hit_cnt = cj; }
+        if (j < K && tj < t_min) { t_min = tj; o.hit_mesh = j; o.hit_idx = ij; hit_cnt = cj; }
     }
     if (o.hit_mesh >= 0) {
         int32_t entering = 1 - (hit_cnt % 2);                            // .cl:142
@@ -112,8 +117,10 @@ LPC_HD PostOut postproc(int32_t K, int32_t prev, const int32_t *mat_type, float 
         }
         float t_minmin = t_min, t_maxmin = t_min, t_minmax = max_ray_len;
         int32_t maxmin_entering = 0, maxmin_idx = -1, minmax_idx = -1;
-        for (int32_t j = 0; j < K; ++j) {                               // .cl:193-214
-            int32_t mt = mat_type[j];
+#pragma unroll
+        for (int32_t j = 0; j < KL; ++j) {                              // .cl:193-214
+            if (KU == 0 && j >= K) break;
+            int32_t mt = j < K ? mat_type[j] : -1;
             if (mt == 0 || mt == 4) {
                 float tj; int32_t cj, ij;
                 slot(j, tj, cj, ij);
@@ -320,6 +327,7 @@ LPC_HD lpc_f2 filter_test2(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2 
 // Trumbore accepts such a triangle with t > eps only through rounding on rays
 // nearly parallel to its plane (scope of the filter proof).
 #define LPC_HALF_MU2 8e-4f
+#if defined(__HIP__)          // lane access of the 2-vector (gcc builds of this header, tests/csrc, see one float)
 LPC_HD lpc_f2 filter_test2h(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2 negA, float ox, float oy,
                             float oz, float nx, float ny, float nz)
 {
@@ -335,6 +343,7 @@ LPC_HD lpc_f2 filter_test2h(lpc_f2 cx, lpc_f2 cy, lpc_f2 cz, lpc_f2 negB, lpc_f2
     if (wn.y < 0.0f && b.y > 0.0f) d.y = 1.0f;
     return d;
 }
+#endif
 
 // filter_test with the half-line cull (filter_test2h, one record)
 LPC_HD float filter_testh(float cx, float cy, float cz, float negB, float negA, float ox, float oy, float oz,

@@ -116,6 +116,8 @@ struct lpc_handle {
     const int32_t *last_perm = nullptr;             // order of the last intersect launch (NULL: unsorted)
     DBuf w_chR, w_chT, w_oblk, w_perm2[2], w_rs2[2];
     int64_t acc_pending_total = 0;
+    int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
+    int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
@@ -238,6 +240,19 @@ static int set_err(lpc_handle *h, int code, const std::string &msg)
     do {                          \
         int rc_ = (x);            \
         if (rc_) return rc_;      \
+    } while (0)
+
+// Shading kernels templated on the register-resident slot count KU (shade_eval):
+// the smallest of 4, 8, 12, 16 that holds the scene's K meshes, 0 = slots read
+// from memory as postproc needs them (K > 16 or LPC_SHADE_KU=0).
+#define LPC_KU_LAUNCH(h, KERN, grid, block, stream, ...)                                          \
+    do {                                                                                         \
+        const int K_ = (h)->shade_ku ? (h)->K : 1 << 30;                                         \
+        if (K_ <= 4) hipLaunchKernelGGL(KERN<4>, grid, block, 0, stream, __VA_ARGS__);           \
+        else if (K_ <= 8) hipLaunchKernelGGL(KERN<8>, grid, block, 0, stream, __VA_ARGS__);      \
+        else if (K_ <= 12) hipLaunchKernelGGL(KERN<12>, grid, block, 0, stream, __VA_ARGS__);    \
+        else if (K_ <= 16) hipLaunchKernelGGL(KERN<16>, grid, block, 0, stream, __VA_ARGS__);    \
+        else hipLaunchKernelGGL(KERN<0>, grid, block, 0, stream, __VA_ARGS__);                   \
     } while (0)
 
 static int dalloc(lpc_handle *h, DBuf &b, size_t bytes, bool keep = false)
@@ -953,7 +968,13 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
 {
     const int64_t npk = (n + 63) / 64;
     const int64_t rblocks = (npk + 3) / 4;
-    const int64_t rcap = ((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces;
+    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 4), pb packets per block
+    const int rs_S = (int)((pt->npieces + 63) / 64);
+    const bool roots_s = h->roots_s > 0 && rs_S <= 4;
+    const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? 1 : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
+    const int64_t rs_blocks = roots_s ? (npk + rs_pb - 1) / rs_pb : 0;
+    const int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
+                                  ((rs_blocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
     if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "work queue: too many root items per shard");
     RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
     const size_t dq_bytes = (size_t)LPC_Q_DSHARDS * (size_t)h->q_dcap * 8;
@@ -982,7 +1003,10 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         Q.irec = (uint32_t *)h->d_wrec.p;
         Q.irec_cap = (uint32_t)cap;
     }
-    if (pt->npieces <= 64)
+    if (roots_s)
+        hipLaunchKernelGGL(k_roots_s, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
+                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0, rs_S, rs_pb);
+    else if (pt->npieces <= 64)
         hipLaunchKernelGGL(k_roots_r, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
     else
@@ -1367,7 +1391,7 @@ static int run_shade(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, in
     A.verts = (const float *)h->d_verts.p;
     A.max_ray_len = max_ray_len; A.ior_env = ior_env;
     A.o = shade_ptrs(h, extra);
-    hipLaunchKernelGGL(k_shade, dim3(grid1(n)), dim3(256), 0, h->stream, A);
+    LPC_KU_LAUNCH(h, k_shade, dim3(grid1(n)), dim3(256), h->stream, A);
     HIPCHK(h, hipGetLastError());
     return 0;
 }
@@ -1447,6 +1471,8 @@ int lpc_open(int device, lpc_handle **out)
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
+    h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
+    h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
     h->lane_max = env_int("LPC_LANE_MAX", h->lane_max);
     h->lane_g = std::max<int64_t>(1, env_int("LPC_LANE_G", h->lane_g));
     h->isect_minb = env_int("LPC_ISECT_MINB", h->isect_minb) == 1 ? 1 : 6;
@@ -2081,7 +2107,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             unsigned long long *gs = (unsigned long long *)h->w_gsum.p;
             G.gsum = gs + (size_t)h->gpar * (size_t)h->gcap;
 
-            hipLaunchKernelGGL(k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, G);
+            LPC_KU_LAUNCH(h, k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
             MoveArgs M;
             M.ntiles = nt;
             M.stR = G.stR; M.stT = G.stT; M.stM = G.stM; M.cst = G.cst;

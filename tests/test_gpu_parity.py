@@ -81,7 +81,7 @@ _POLICIES = [
     # root items walked by k_rootwalk (default): piece level, grid, block shape
     dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"), dict(LPC_Q_WALK_BLOCKS="1"),
     dict(LPC_Q_WALK_WPB="4", LPC_SPILL_WPB="4"), dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"),
-    dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_WALK_WAVES="7"),
+    dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_WALK_WAVES="7"), dict(LPC_SHADE_KU="0"), dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
     # persistent work queue (k_roots + k_trav): claim batch, piece level, hand-over
     # queue that overflows, grids of one block, of a few blocks and far beyond residency
     dict(_TRAV, LPC_Q_BATCH="1"), dict(_TRAV, LPC_Q_BATCH="7"), dict(_TRAV, LPC_Q_TARGET="1"),

@@ -11,6 +11,11 @@ for d in sorted(glob.glob(os.path.join(root, "*")), key=lambda p: int(os.path.ba
     st = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
     b = [l for l in open(os.path.join(d, "bench.log")) if l.startswith("{")]
     v = json.loads(b[-1]) if b else {}
+    if not v:
+        v = {"value": 0, "ms_per_step": 0}
+        for l in open(os.path.join(d, "bench.log")):
+            if "ms/step" in l:
+                print("   " + l.strip()[:100])
     print(f"== {cfg}: {v.get('value', 0) / 1e6:.1f} M/s, {v.get('ms_per_step', 0):.3f} ms/step")
     if not st:
         continue
