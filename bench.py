@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-rays", type=int, default=1 << 20, help="CPU baseline sample (rays, one bounce)")
+    ap.add_argument("--no-prof", action="store_true", help="no HIP events in the timed region (A/B of their cost)")
     return ap.parse_args()
 
 
@@ -118,10 +119,13 @@ def main():
     runner = ShardedTrace(eng, comm)
 
     def step():
+        # one process: the trace returns once its outputs are final, so the next
+        # step's launches queue behind its last row moves (sync() waits for all)
         eng.reset()
-        return runner.run(sc.iterations, sc.tau, in_pow)
+        return runner.run(sc.iterations, sc.tau, in_pow, wait=False)
 
     def sync():
+        eng.sync()
         if dist:
             import torch
             torch.cuda.synchronize(local)
@@ -129,7 +133,8 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    eng.prof_enable(True, light=True)        # HIP events around the hierarchy kernel launches only
+    if not a.no_prof:
+        eng.prof_enable(True, light=True)    # HIP events around the hierarchy kernel launches only
     eng.prof_read(reset=True)
     sync()
     t0 = time.perf_counter()
@@ -162,13 +167,13 @@ def main():
     kernel = HIER_KERNEL.get(os.environ.get("LPC_QUEUE", "2"), "k_rootwalk")
     rays_per_launch = bounces / launches                 # rank-0 launches
     alg_bytes = rays_per_launch * RAY_BYTES + M * TRI_BYTES
-    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     pairs_per_s = bounces_all * M / dt                   # reference-equivalent RI/s (sum N_iter * M / T)
     mt_tflops = pairs_per_s * MT_FLOPS / 1e12
     pmc = load_pmc()
     traffic = pmc.get("hbm_bytes_per_launch")
     valu_per_launch = pmc.get("sq_insts_valu_mean")
-    valu_rate = valu_per_launch / (avg_ms * 1e-3) if valu_per_launch else None
+    valu_rate = valu_per_launch / (avg_ms * 1e-3) if valu_per_launch and avg_ms > 0 else None
     out = {
         "metric": "ray-bounces/sec @ 1M rays x 100k tris",
         "value": bounces_all / dt,

@@ -151,6 +151,15 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
  * receive lpc_trace_measured's outputs at the end. */
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                   int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+/* lpc_trace_run without waiting for the last iteration's kernels (the moves of
+ * the next population's rows and of the measured record; the outputs above are
+ * final when it returns): a caller that traces batch after batch lets the next
+ * batch's launches queue behind them.  Every entry point that copies device data
+ * to the host waits for them first; lpc_sync waits explicitly. */
+int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                        int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+/* Wait until the handle's stream has finished every queued kernel. */
+int lpc_sync(lpc_handle *h);
 /* Current population size. */
 int lpc_trace_population(lpc_handle *h, int64_t *n);
 /* Measured record so far: count and per-mesh measured power (double[mesh_count]). */

@@ -64,6 +64,8 @@ _PROTOS = {
     "lpc_trace_reset": [_P],
     "lpc_trace_iterate": [_P, _P, _P, _P, _P, _P, _P],
     "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P],
+    "lpc_trace_run_async": [_P, _I32, _F64, _P, _P, _P, _P],
+    "lpc_sync": [_P],
     "lpc_trace_population": [_P, _P],
     "lpc_trace_measured": [_P, _P, _P],
     "lpc_trace_fetch_measured": [_P, _P, _P, _P],

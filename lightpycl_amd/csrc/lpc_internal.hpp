@@ -45,7 +45,7 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 // a 128-byte line of its own: a device-scope atomic evicts its line from the
 // L2, and one word serialises its atomics (~11 ns each), so counters are sharded.
 #define LPC_MISC_SPILL 6                  // [6 + l]: items queued for hand-over level l (l < 8)
-#define LPC_Q_CSHARDS 8                   // root-item shards (k_roots block b -> b % 8)
+#define LPC_Q_CSHARDS 8                   // root-item shards (k_roots block b -> b % 8, or packet-range eighths)
 #define LPC_Q_DSHARDS 32                  // hand-over queue shards (k_trav block b -> b % 32)
 #define LPC_Q_NINIT(c) (32 * (1 + (c)))   // root items k_roots wrote into shard c
 #define LPC_Q_CHEAD(c) (32 * (9 + (c)))   // claim head of root shard c
@@ -92,7 +92,20 @@ struct QueueArgs {
     int32_t dshard;                   // set per wave by k_trav (-1: no hand-over)
     uint32_t *irec;                   // per-item records (profiling, lpc_prof_enable(h, 5)) or NULL
     uint32_t irec_cap;
+    // XCD-local walk (LPC_XCD_WALK): the root shards are contiguous eighths of the
+    // packet range (k_roots*), and k_rootwalk's waves on XCD x (blocks b % 8 == x,
+    // the hardware's round-robin dispatch) walk the x-th eighth of the item list,
+    // so each XCD's L2 holds the scene records of one eighth of the directions.
+    int32_t xcd;
+    int64_t npk;                      // packets of the launch (range shards)
 };
+// root shard of a k_roots* block whose first packet is w0
+__host__ __device__ inline int q_shard(const QueueArgs &Q, int64_t w0, uint32_t block)
+{
+    if (!Q.xcd) return (int)(block % LPC_Q_CSHARDS);
+    const int64_t c = (w0 * LPC_Q_CSHARDS) / (Q.npk > 0 ? Q.npk : 1);
+    return (int)(c < LPC_Q_CSHARDS - 1 ? c : LPC_Q_CSHARDS - 1);
+}
 #define LPC_Q_IREC_N 16                   // misc word: item records written this launch
 
 // Work hand-over: a k_intersect wave that has visited `budget` nodes with two or

@@ -579,7 +579,7 @@ __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict
     __shared__ uint32_t s_cnt[4];
     __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    const int c = q_shard(Q, (int64_t)blockIdx.x * 4, blockIdx.x);
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     const bool live = w * 64 < n;
     {
@@ -632,7 +632,7 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     __shared__ uint32_t s_cnt[4];
     __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    const int c = q_shard(Q, (int64_t)blockIdx.x * 4, blockIdx.x);
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     const bool live = w * 64 < n;
     const int64_t s = w * 64 + lane;
@@ -682,7 +682,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
+    const int c = q_shard(Q, (int64_t)blockIdx.x * pb, blockIdx.x);
     const int ntask = S * pb;
     for (int t = wv; t < ntask; t += 4) {
         const int64_t w = (int64_t)blockIdx.x * pb + t / S;
@@ -748,8 +748,18 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_
     pre[0] = 0;
 #pragma unroll
     for (int c = 0; c < LPC_Q_CSHARDS; ++c) pre[c + 1] = pre[c] + min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-    const uint32_t stride = gridDim.x * (uint32_t)WPB;
-    for (uint32_t i = blockIdx.x * (uint32_t)WPB + (uint32_t)wv; i < pre[LPC_Q_CSHARDS]; i += stride) {
+    uint32_t stride = gridDim.x * (uint32_t)WPB, i0 = blockIdx.x * (uint32_t)WPB + (uint32_t)wv,
+             iend = pre[LPC_Q_CSHARDS];
+    if (Q.xcd && (gridDim.x & 7u) == 0u) {
+        // XCD-local: block b runs on XCD b % 8 (round-robin dispatch) and walks the
+        // (b % 8)-th eighth of the items (range shards: an eighth of the packets);
+        // any placement still visits every item exactly once
+        const uint32_t x = blockIdx.x & 7u, T = iend;
+        i0 = (uint32_t)(((uint64_t)T * x) / 8u) + (blockIdx.x >> 3) * (uint32_t)WPB + (uint32_t)wv;
+        iend = (uint32_t)(((uint64_t)T * (x + 1u)) / 8u);
+        stride = (gridDim.x >> 3) * (uint32_t)WPB;
+    }
+    for (uint32_t i = i0; i < iend; i += stride) {
         int c = 0;
         while (i >= pre[c + 1]) ++c;
         const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - pre[c])];

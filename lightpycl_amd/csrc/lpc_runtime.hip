@@ -117,6 +117,9 @@ struct lpc_handle {
     DBuf w_chR, w_chT, w_oblk, w_perm2[2], w_rs2[2];
     int64_t acc_pending_total = 0;
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
+    int64_t roots_tasks = 16384;                    // LPC_ROOTS_TASKS: k_roots_s splits each packet's pieces into up to 16
+                                                    //   classes so that a launch has about this many tasks (0: fewest classes)
+    int xcd_walk = 0;                               // LPC_XCD_WALK: packet-range root shards, XCD-local k_rootwalk (QueueArgs::xcd)
     int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
@@ -206,6 +209,7 @@ struct lpc_handle {
     int64_t n_cur = 0, n_init = 0;
     float max_ray_len = 1e3f, ior_env = 1.0f;
     bool traced_ready = false;
+    bool inflight = false;                          // the stream may still run a trace's last kernels (settle)
     DBuf m_buf;                                     // measured: x y z pw | mesh
     int64_t m_cap = 0, m_total = 0;
     DBuf d_acc;
@@ -254,6 +258,19 @@ static int set_err(lpc_handle *h, int code, const std::string &msg)
         else if (K_ <= 16) hipLaunchKernelGGL(KERN<16>, grid, block, 0, stream, __VA_ARGS__);    \
         else hipLaunchKernelGGL(KERN<0>, grid, block, 0, stream, __VA_ARGS__);                   \
     } while (0)
+
+// Wait for a trace's kernels still queued on the stream: lpc_trace_iterate and
+// lpc_trace_run_async return once the iteration counters are published, while
+// the rows of the next population still move.  Every entry point that copies
+// device data to the host or reuses the caller's buffers calls this first.
+static int settle(lpc_handle *h)
+{
+    if (h && h->inflight) {
+        h->inflight = false;
+        if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    return 0;
+}
 
 static int dalloc(lpc_handle *h, DBuf &b, size_t bytes, bool keep = false)
 {
@@ -853,6 +870,25 @@ static int ray_base(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n,
     return 0;
 }
 
+// hand-over levels of a launch of n rays (0: none)
+static int spill_level_count(const lpc_handle *h, int64_t n, const SpillArgs &SP)
+{
+    const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
+    return SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
+}
+
+// level l's input (queue l % 2, length misc[6 + l]) and output (level l + 1)
+static void spill_level_args(lpc_handle *h, const SpillArgs &SP, int l, int levels, SpillArgs *I, SpillArgs *O)
+{
+    uint32_t *misc = (uint32_t *)h->d_misc.p;
+    *I = SP; *O = SP;
+    I->items = (SpillItem *)h->w_spill.p + (size_t)(l % 2) * (size_t)h->spill_cap;
+    I->ctr = misc + LPC_MISC_SPILL + l;
+    O->items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
+    O->ctr = misc + LPC_MISC_SPILL + l + 1;
+    O->budget = l + 1 < levels ? SP.budget : 0;
+}
+
 // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
 // what exceeds the budget for level l + 1; the last level finishes
 static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
@@ -862,15 +898,10 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
     uint32_t *misc = (uint32_t *)h->d_misc.p;
     RayBase ray;
     RETIF(ray_base(h, in, rs, n, &ray));
-    const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
-    const int levels = SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
+    const int levels = spill_level_count(h, n, SP);
     for (int l = 0; l < levels; ++l) {
-        SpillArgs I = SP, O = SP;
-        I.items = (SpillItem *)h->w_spill.p + (size_t)(l % 2) * (size_t)h->spill_cap;
-        I.ctr = misc + LPC_MISC_SPILL + l;
-        O.items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
-        O.ctr = misc + LPC_MISC_SPILL + l + 1;
-        O.budget = l + 1 < levels ? SP.budget : 0;
+        SpillArgs I, O;
+        spill_level_args(h, SP, l, levels, &I, &O);
         // later levels hold fewer items (and often none): smaller grids
         // grid in 4-wave units, launched as single-wave blocks unless LPC_SPILL_WPB=4
         const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
@@ -968,13 +999,23 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
 {
     const int64_t npk = (n + 63) / 64;
     const int64_t rblocks = (npk + 3) / 4;
-    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 4), pb packets per block
-    const int rs_S = (int)((pt->npieces + 63) / 64);
+    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 16), pb packets per block
+    // small populations (few packets): more piece classes per packet, so that the
+    // launch has ~roots_tasks waves' worth of tasks instead of a few long loops
+    int rs_S = (int)((pt->npieces + 63) / 64);
     const bool roots_s = h->roots_s > 0 && rs_S <= 4;
+    if (roots_s && h->roots_tasks > 0)
+        rs_S = (int)std::max<int64_t>(rs_S, std::min<int64_t>({(h->roots_tasks + npk - 1) / npk,
+                                                                (int64_t)LPC_ROOTS_TASKS, (int64_t)pt->npieces}));
     const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? 1 : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
     const int64_t rs_blocks = roots_s ? (npk + rs_pb - 1) / rs_pb : 0;
-    const int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
-                                  ((rs_blocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+    // packet-range shards (xcd): a shard takes the blocks whose first packet lies in
+    // its eighth of [0, npk), at most npk / 8 + 1 blocks' packets
+    const bool xcd = h->xcd_walk != 0 && h->queue == 2;
+    const int64_t pbmax = std::max<int64_t>(4, rs_pb);
+    const int64_t rcap = std::max({((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
+                                   ((rs_blocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces,
+                                   xcd ? (npk / LPC_Q_CSHARDS + 2 * pbmax) * (int64_t)pt->npieces : (int64_t)0});
     if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "work queue: too many root items per shard");
     RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
     const size_t dq_bytes = (size_t)LPC_Q_DSHARDS * (size_t)h->q_dcap * 8;
@@ -995,6 +1036,8 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     Q.dshard = -1;
     Q.irec = nullptr;
     Q.irec_cap = 0;
+    Q.xcd = xcd ? 1 : 0;
+    Q.npk = npk;
     if (h->prof_items) {              // per-item records of this launch (the last one is kept)
         const int64_t cap = (int64_t)1 << 21;
         RETIF(dalloc(h, h->d_wrec, (size_t)cap * 32));
@@ -1473,6 +1516,8 @@ int lpc_open(int device, lpc_handle **out)
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
+    h->xcd_walk = (int)env_int("LPC_XCD_WALK", h->xcd_walk);
+    h->roots_tasks = env_int("LPC_ROOTS_TASKS", h->roots_tasks);
     h->lane_max = env_int("LPC_LANE_MAX", h->lane_max);
     h->lane_g = std::max<int64_t>(1, env_int("LPC_LANE_G", h->lane_g));
     h->isect_minb = env_int("LPC_ISECT_MINB", h->isect_minb) == 1 ? 1 : 6;
@@ -1542,6 +1587,7 @@ int lpc_open(int device, lpc_handle **out)
 int lpc_close(lpc_handle *h)
 {
     if (!h) return 0;
+    (void)settle(h);                     // a trace still running (lpc_trace_iterate / _run_async)
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     DBuf *bufs[] = {&h->d_nodes, &h->w_pk, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
@@ -1581,6 +1627,7 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
                      const float *diss)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if (tri_count <= 0 || mesh_count <= 0 || !v0 || !v1 || !v2 || !mesh_id || !mat_type || !ior ||
         !refl || !diss)
         return set_err(h, LPC_E_ARG, "scene needs >= 1 triangle, >= 1 mesh and all tables");
@@ -1716,6 +1763,7 @@ int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float 
                     int32_t *n1_mid, int32_t *n2_mid, int32_t *entering, int32_t *isect_idx)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
     if (n < 0 || !origin4 || !dir4 || !pow || !meas || !prev_mid || !dest4 || !isect_mid ||
         !r_dir4 || !r_pow || !r_meas || !t_dir4 || !t_pow || !t_meas)
@@ -1780,6 +1828,7 @@ int lpc_intersect(lpc_handle *h, int64_t n, const float *dev_origin4, const floa
                   float max_ray_len, float *dev_tmin, int32_t *dev_cnt, int32_t *dev_itmp)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
     if (n < 0 || !dev_origin4 || !dev_dir4 || !dev_tmin || !dev_cnt || !dev_itmp)
         return set_err(h, LPC_E_ARG, "intersect: missing buffer");
@@ -1815,6 +1864,7 @@ int lpc_intersect_postproc(lpc_handle *h, int64_t n, const float *dev_origin4,
                            const int32_t *dev_itmp, float max_ray_len)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
     if (n < 0 || !dev_origin4 || !dev_dir4 || !dev_dest4 || !dev_prev_mid || !dev_n1_mid ||
         !dev_n2_mid || !dev_entering || !dev_isect_mid || !dev_isect_idx || !dev_tmin ||
@@ -1846,6 +1896,7 @@ int lpc_reflect_refract_rays(lpc_handle *h, int64_t n, const float *dev_origin4,
                              float ior_env)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
     if (n < 0 || !dev_origin4 || !dev_dest4 || !dev_dir4 || !dev_pow || !dev_meas ||
         !dev_n1_mid || !dev_n2_mid || !dev_r_origin4 || !dev_r_dir4 || !dev_r_pow ||
@@ -1893,6 +1944,7 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
                        const float *pow, float max_ray_len, float ior_env)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
     if (n < 0 || (n > 0 && (!origin4 || !dir4 || !pow))) return set_err(h, LPC_E_ARG, "set_rays: missing buffer");
     HIPCHK(h, hipSetDevice(h->device));
@@ -1943,8 +1995,8 @@ int lpc_trace_reset(lpc_handle *h)
     return 0;
 }
 
-int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                  int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
@@ -1962,8 +2014,26 @@ int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_i
         RETIF(lpc_trace_measured(h, &c, mesh_power));
         if (measured_count) *measured_count = c;
     }
-    HIPCHK(h, hipStreamSynchronize(h->stream));             // the trace's last kernels too
+    if (wait) RETIF(settle(h));                             // the trace's last kernels too
     return 0;
+}
+
+int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                  int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+{
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, true);
+}
+
+int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                        int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+{
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, false);
+}
+
+int lpc_sync(lpc_handle *h)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    return settle(h);
 }
 
 int lpc_trace_population(lpc_handle *h, int64_t *n)
@@ -2234,6 +2304,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     memcpy(&dm2, &acc.dmax2_bits, 4);
     RETIF(check_dcap(h, (double)dm2));
     h->pop_dmax2 = (double)dm2;                 // the next population's max |D|^2 (float, see run_intersect)
+    h->inflight = true;                         // k_stage_move / k_scatter may still run
     if (st) *st = S;
     return 0;
 }
@@ -2276,6 +2347,7 @@ int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_pow)
 int lpc_trace_fetch_measured(lpc_handle *h, float *pos4, float *pow, int32_t *mesh)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     HIPCHK(h, hipSetDevice(h->device));
     const int64_t n = h->m_total;
     if (n == 0) return 0;
@@ -2300,6 +2372,7 @@ int lpc_project_hist(lpc_handle *h, int mode, int64_t n, const float *pos4, cons
                      float *y, float *pwr_cor)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     if ((mode != 0 && mode != 1) || nx <= 0 || ny <= 0 || !rot4 || !pivot4 || !xedges || !yedges || !H)
         return set_err(h, LPC_E_ARG, "project_hist: bad argument");
     if (pos4 && !pwr) return set_err(h, LPC_E_ARG, "project_hist: pwr is NULL");
@@ -2357,6 +2430,7 @@ int lpc_project_hist(lpc_handle *h, int mode, int64_t n, const float *pos4, cons
 int lpc_prof_enable(lpc_handle *h, int on)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     h->prof = on != 0;
     h->prof_stats = on == 2;
     h->prof_waves = on == 3;
@@ -2372,6 +2446,7 @@ int lpc_prof_enable(lpc_handle *h, int on)
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
 {
     if (!h || !out) return set_err(h, LPC_E_ARG, "null argument");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     (void)hipStreamSynchronize(h->stream);
     prof_resolve(h);
     out->intersect_ms = h->prof_isect_ms;
@@ -2404,6 +2479,7 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
 int lpc_prof_waves(lpc_handle *h, uint32_t *rec4, int64_t cap, int64_t *count)
 {
     if (!h || !count) return set_err(h, LPC_E_ARG, "null argument");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     HIPCHK(h, hipStreamSynchronize(h->stream));
     *count = h->d_wrec.p ? h->wrec_count : 0;
     if (rec4 && *count > 0) {

@@ -81,10 +81,12 @@ class ShardedTrace:
             return np.asarray(vals, dtype=np.float64)
         return self.comm.allreduce_sum(vals)
 
-    def run(self, iterations, tau, input_power_local, hist=None):
+    def run(self, iterations, tau, input_power_local, hist=None, wait=True):
         """Trace to the reference's termination.  hist=(limits, points): also bin
         the measured rays (get_binned_data_angular) on every rank and all-reduce
-        the histogram (float64, bin counts are additive)."""
+        the histogram (float64, bin counts are additive).  wait=False (one
+        process): return once the outputs are final, without waiting for the last
+        rows to move on the device (engine.sync() waits)."""
         in_pow = float(self._sum([input_power_local])[0])
         thr = (1.0 - tau) * in_pow
         bounces = 0
@@ -93,7 +95,7 @@ class ShardedTrace:
         measured = None
         if self.comm is None and hasattr(self.engine, "run_local"):
             # one process: the same loop inside the library (lpc_trace_run)
-            stats, measured = self.engine.run_local(int(iterations), thr)
+            stats, measured = self.engine.run_local(int(iterations), thr, wait=wait or hist is not None)
             for st in stats:
                 bounces += int(st.n_in)
                 iters += 1

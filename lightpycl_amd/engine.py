@@ -162,7 +162,11 @@ class Engine:
         return st, dict(origin=org, dest=dst, pow=pw, meas=ms,
                         next_pow=nxt[: st.n_reflect + st.n_refract])
 
-    def run_local(self, iterations, power_threshold):
+    def sync(self):
+        """lpc_sync: wait for every kernel queued on the engine's stream."""
+        self._c(self.L.lpc_sync(self.h))
+
+    def run_local(self, iterations, power_threshold, wait=True):
         """lpc_trace_run: iterate until the next population's power is below
         power_threshold or no ray is kept (at most `iterations`).  Returns the
         per-iteration stats and the measured (count, per-mesh power)."""
@@ -174,8 +178,11 @@ class Engine:
                     np.zeros(max(self.mesh_count, 1), np.float64))
             self.__dict__.setdefault("_run_bufs", {})[key] = bufs
         arr, k, c, mp = bufs
-        self._c(self.L.lpc_trace_run(self.h, cap, float(power_threshold), arr, ctypes.byref(k), ctypes.byref(c),
-                                     mp.ctypes.data_as(ctypes.c_void_p)))
+        # wait=False: lpc_trace_run_async (the outputs are final; the last rows may
+        # still move on the device and the next batch's launches queue behind them)
+        fn = self.L.lpc_trace_run if wait else self.L.lpc_trace_run_async
+        self._c(fn(self.h, cap, float(power_threshold), arr, ctypes.byref(k), ctypes.byref(c),
+                   mp.ctypes.data_as(ctypes.c_void_p)))
         return [_lib.IterStats.from_buffer_copy(arr[i]) for i in range(k.value)], (c.value,
                                                                                    mp[: self.mesh_count].copy())
 

@@ -8,6 +8,7 @@ rays that crossed a dissipative medium) and the angular projection
 (acos/atan2/sin/cos: bins may move for points within 1e-6 of an edge; histogram
 L1 rel <= 1e-5).
 """
+import ctypes
 import numpy as np
 import pytest
 
@@ -82,6 +83,10 @@ _POLICIES = [
     dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"), dict(LPC_Q_WALK_BLOCKS="1"),
     dict(LPC_Q_WALK_WPB="4", LPC_SPILL_WPB="4"), dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"),
     dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_WALK_WAVES="7"), dict(LPC_SHADE_KU="0"), dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
+    dict(LPC_XCD_WALK="1"), dict(LPC_XCD_WALK="1", LPC_Q_WALK_BLOCKS="2"), dict(LPC_XCD_WALK="1", LPC_Q_WALK_BLOCKS="3"),
+    dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"),
+    dict(LPC_ROOTS_TASKS="0"), dict(LPC_ROOTS_TASKS="100000000"), dict(LPC_ROOTS_TASKS="1000000", LPC_Q_TARGET="1"),
+    dict(LPC_XCD_WALK="1", LPC_ROOTS_S="0", LPC_Q_TARGET="10000000"), dict(LPC_XCD_WALK="1", LPC_ROOTS_S="0"),
     # persistent work queue (k_roots + k_trav): claim batch, piece level, hand-over
     # queue that overflows, grids of one block, of a few blocks and far beyond residency
     dict(_TRAV, LPC_Q_BATCH="1"), dict(_TRAV, LPC_Q_BATCH="7"), dict(_TRAV, LPC_Q_TARGET="1"),
@@ -426,3 +431,38 @@ def test_clean_slots_across_paths(oracle_mod):
     for got, want in ((a, fresh[0]), (b, fresh[0]), (c, fresh[1]), (d, fresh[0])):
         assert got[0] == want[0] and got[1] == want[1]
         np.testing.assert_array_equal(got[2], want[2])
+
+
+@pytest.mark.parametrize("name,n", [("synthetic", 100000), ("lens", 30000)])
+def test_async_trace_run_equals_sync(name, n):
+    """lpc_trace_run_async returns once the trace's outputs are final and lets
+    the next trace queue behind its last row moves: back-to-back async traces
+    give the synchronous trace's stats and per-mesh power, and the measured
+    record read afterwards (the entry point waits for the stream) is the same
+    element for element, also through the power-only copy."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.BUILDERS[name](n=n, seed=41)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+        stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+        want = ([(s.n_in, s.n_reflect, s.n_refract, s.n_measured, s.power_next) for s in stats], cnt, mp.tolist())
+        rec = e.fetch_measured()
+        for rep in range(3):
+            e.reset()
+            stats, (cnt, mp) = e.run_local(sc.iterations, thr, wait=False)
+            got = ([(s.n_in, s.n_reflect, s.n_refract, s.n_measured, s.power_next) for s in stats], cnt, mp.tolist())
+            assert got == want
+        p = np.zeros(cnt, np.float32)
+        e._c(e.L.lpc_trace_fetch_measured(e.h, None, p.ctypes.data_as(ctypes.c_void_p), None))
+        np.testing.assert_array_equal(p, rec[1])
+        e.reset()
+        e.run_local(sc.iterations, thr, wait=False)
+        for x, y in zip(e.fetch_measured(), rec):
+            np.testing.assert_array_equal(x, y)
+        e.sync()
+    finally:
+        e.close()

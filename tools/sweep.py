@@ -19,7 +19,7 @@ from lightpycl_amd.engine import Engine  # noqa: E402
 
 KNOBS = ("KEY", "LARGE_PER_TRI", "BUDGET_LARGE", "LARGE_N", "FLAT", "TARGET_BLOCKS", "SORT", "BUDGET", "SPILL_CAP", "SPILL_BLOCKS", "LOOP", "SLIVER_WAVES",
          "SLIVER_PPW", "NODE_W", "SPILL_LEVELS", "PAIR_SHIFT", "SORT_MIN", "LOOP_MIN", "GATHER_AOS", "SLIVER_RAYS", "WAVE_TARGET", "SLIVER_CULL", "SPILL_SHRINK", "SPILL_MIN_BLOCKS", "LANE_MAX", "LANE_G", "ISECT_MINB", "ONESWEEP_MIN", "SPILL_LEVELS_SMALL", "FUSE_SHADE", "XCD_ROWS", "CHAIN", "CHUNK", "QUEUE", "TRACED", "TRACED_SORT", "Q_TARGET", "Q_WALK_BLOCKS", "Q_WALK_WPB",
-         "SPILL_WPB", "SIDE_STREAM", "EARLY_ACC", "DBG", "FUSE_COMPACT", "SLIVER_LATE", "WALK_WAVES", "HALF", "SHADE_KU", "ROOTS_S")
+         "SPILL_WPB", "SIDE_STREAM", "EARLY_ACC", "DBG", "FUSE_COMPACT", "SLIVER_LATE", "WALK_WAVES", "HALF", "SHADE_KU", "ROOTS_S", "XCD_WALK", "ROOTS_TASKS")
 name = sys.argv[1] if len(sys.argv) > 1 else "synthetic"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
@@ -54,11 +54,20 @@ ms = {cfg: [] for cfg, *_ in engs}
 isect = {cfg: [] for cfg, *_ in engs}
 for _ in range(rounds):
     for cfg, e, run, _, nit in engs:
-        for _ in range(steps):
-            e.reset()
+        if os.environ.get("SWEEP_ASYNC"):     # back-to-back async traces (bench.py's steps), one sync
+            e.sync()
             t = time.perf_counter()
-            run.run(sc.iterations, sc.tau, in_pow)
-            ms[cfg].append(1e3 * (time.perf_counter() - t))
+            for _ in range(steps):
+                e.reset()
+                run.run(sc.iterations, sc.tau, in_pow, wait=False)
+            e.sync()
+            ms[cfg].append(1e3 * (time.perf_counter() - t) / steps)
+        else:
+            for _ in range(steps):
+                e.reset()
+                t = time.perf_counter()
+                run.run(sc.iterations, sc.tau, in_pow)
+                ms[cfg].append(1e3 * (time.perf_counter() - t))
         # per-iteration intersect stage time (HIP events)
         e.prof_enable(True)
         e.reset()
