@@ -119,6 +119,9 @@ struct lpc_handle {
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     int64_t roots_tasks = 16384;                    // LPC_ROOTS_TASKS: k_roots_s splits each packet's pieces into up to 16
                                                     //   classes so that a launch has about this many tasks (0: fewest classes)
+    bool fork_late = false;                         // LPC_FORK_LATE: side-stream fork event after k_roots (measured: no gain)
+    bool fork_pending = false;                      // run_intersect -> run_queue: the fork event is still to record
+    bool ev_sysfence = true;                        // LPC_EV_SYSFENCE=0: events without the system-scope fence (measured slower)
     int xcd_walk = 0;                               // LPC_XCD_WALK: packet-range root shards, XCD-local k_rootwalk (QueueArgs::xcd)
     int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
@@ -812,7 +815,10 @@ static hipEvent_t ev_get(lpc_handle *h)
         return e;
     }
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    // LPC_EV_SYSFENCE=0: profiling events without the system-scope fence (measured:
+    // the timed stage shortens, the step does not)
+    if (hipEventCreateWithFlags(&e, h->ev_sysfence ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess)
+        return nullptr;
     return e;
 }
 
@@ -1055,6 +1061,10 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     else
         hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
+    if (h->fork_pending) {                  // the side stream's fork (run_intersect, LPC_FORK_LATE)
+        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        h->fork_pending = false;
+    }
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
         RayBase ray;
@@ -1271,14 +1281,24 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // add to the slots with order-independent atomics); joined at the end
     hipStream_t ss = h->stream;
     const bool side = nsp > 0 && h->stream2 && h->ev_side[0];
+    // the fork event: recorded here, or (LPC_FORK_LATE, work-queue path with late
+    // slivers) right after k_roots, so the marker's fence does not sit between the
+    // previous iteration's compaction and the root tests
+    bool fork_pending = false;
     if (side) {
-        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
         ss = h->stream2;
+        fork_pending = h->fork_late && h->sliver_late && h->queue == 2;
+        if (!fork_pending) HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
     }
+    h->fork_pending = fork_pending;
     // on the side stream the sliver kernels are launched after the hierarchy
     // stage's (the host reaches k_roots / k_rootwalk sooner; the slivers still
     // run beside k_rootwalk)
     auto launch_slivers = [&]() -> int {
+    if (side && h->fork_pending) {          // no k_roots launched (no pieces): record it now
+        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        h->fork_pending = false;
+    }
     if (side) HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
     if (nsp > 0) {
         // packets per wave: enough (packet, piece) waves to fill the GPU, no more
@@ -1559,10 +1579,15 @@ int lpc_open(int device, lpc_handle **out)
     h->q_spin = std::min<int64_t>(0xffffffffLL, std::max<int64_t>(1024, env_int("LPC_Q_SPIN", h->q_spin)));
     h->early_acc = env_int("LPC_EARLY_ACC", h->early_acc) != 0;
     h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
+    h->ev_sysfence = env_int("LPC_EV_SYSFENCE", 1) != 0;
+    h->fork_late = env_int("LPC_FORK_LATE", 0) != 0;
     if (env_int("LPC_SIDE_STREAM", 1) != 0) {
+        // the side stream's join events (LPC_EV_SYSFENCE=0: device-scope release only,
+        // measured 4-8 % slower per step)
+        const unsigned evf = hipEventDisableTiming | (h->ev_sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&h->ev_side[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&h->ev_side[1], hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
             h->stream2 = nullptr;       // all on the main stream
             h->ev_side[0] = h->ev_side[1] = nullptr;
         }
