@@ -1,6 +1,7 @@
-mkdir -p gpurun_out/sweep
-SWEEP_ASYNC=1 SWEEP_STEPS=10 timeout -k 10 300 python -u tools/sweep.py synthetic 1000000 5 FORK_LATE=1 FORK_LATE=0 FORK_LATE=1,KEY=0 EV_SYSFENCE=0 > gpurun_out/sweep/aba.log 2>&1 || { tail -5 gpurun_out/sweep/aba.log; exit 1; }
-grep -v amdgpu gpurun_out/sweep/aba.log
-SWEEP_ASYNC=1 SWEEP_STEPS=10 timeout -k 10 300 python -u tools/sweep.py lens 1000000 5 FORK_LATE=1 FORK_LATE=0 FORK_LATE=1,KEY=0 > gpurun_out/sweep/aba2.log 2>&1 || { tail -5 gpurun_out/sweep/aba2.log; exit 1; }
-grep -v amdgpu gpurun_out/sweep/aba2.log
-bash tools/kt_cfg.sh 'LPC_ROOTS_TASKS=0' 'LPC_ROOTS_TASKS=4096' 'LPC_ROOTS_S=0' > gpurun_out/sweep/kt.log 2>&1 || { tail -5 gpurun_out/sweep/kt.log; exit 1; }
+mkdir -p gpurun_out/v
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/v/smoke.log 2>&1 || { tail -5 gpurun_out/v/smoke.log; exit 1; }
+tail -1 gpurun_out/v/smoke.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/v/pytest.log 2>&1 || { tail -30 gpurun_out/v/pytest.log; exit 1; }
+tail -1 gpurun_out/v/pytest.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/v/bench.log 2>&1 || { tail -5 gpurun_out/v/bench.log; exit 1; }
+grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/v/bench.log
