@@ -2242,6 +2242,8 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         }
         if (out_origin4 || out_dest4 || out_pow || out_meas) {
+            // the copies below run on the null stream: the shading on h->stream first
+            HIPCHK(h, hipStreamSynchronize(h->stream));
             auto pack = [&](float *dst4, const float *x, const float *y, const float *z) -> int {
                 hipLaunchKernelGGL(k_pack4, dim3(grid1(nc)), dim3(256), 0, h->stream, nc, x, y, z,
                                    (float4 *)h->w_stage.p);
