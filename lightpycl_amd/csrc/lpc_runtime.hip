@@ -117,7 +117,7 @@ struct lpc_handle {
     DBuf w_chR, w_chT, w_oblk, w_perm2[2], w_rs2[2];
     int64_t acc_pending_total = 0;
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
-    int64_t roots_tasks = 16384;                    // LPC_ROOTS_TASKS: k_roots_s splits each packet's pieces into up to 16
+    int64_t roots_tasks = 0;                        // LPC_ROOTS_TASKS: k_roots_s splits each packet's pieces into up to 16
                                                     //   classes so that a launch has about this many tasks (0: fewest classes)
     bool fork_late = false;                         // LPC_FORK_LATE: side-stream fork event after k_roots (measured: no gain)
     bool fork_pending = false;                      // run_intersect -> run_queue: the fork event is still to record
@@ -1052,6 +1052,9 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         Q.irec = (uint32_t *)h->d_wrec.p;
         Q.irec_cap = (uint32_t)cap;
     }
+    if (h->host_prof)
+        fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d S %d pb %d blocks %lld rcap %lld\n",
+                (long long)n, (long long)npk, (int)pt->npieces, rs_S, rs_pb, (long long)rs_blocks, (long long)rcap);
     if (roots_s)
         hipLaunchKernelGGL(k_roots_s, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0, rs_S, rs_pb);
