@@ -160,6 +160,10 @@ struct ShadeArgs {
     const float *ior, *refl, *diss, *verts;
     float max_ray_len, ior_env;
     ShadeOutPtrs o;
+    // counts first (LPC_SHADE_CFIRST, traced iterations only, whose slots start in
+    // the uniform clean state): a slot's key is read only when its count is not 0
+    // (a count of 0 means the key is still slot_key(max_ray_len, -1))
+    int32_t cfirst;
 };
 
 #define LPC_MP_MAX 4                      // measure meshes whose power the traced path sums per tile

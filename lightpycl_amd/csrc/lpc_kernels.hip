@@ -1433,10 +1433,17 @@ static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_
     if constexpr (KU > 0) {
         unsigned long long kr[KU];
         int32_t cr[KU];
+        if (A.cfirst) {
 #pragma unroll
-        for (int j = 0; j < KU; ++j) {
-            kr[j] = k0; cr[j] = 0;
-            if (j < A.K) { kr[j] = A.skey[(int64_t)j * n + r]; cr[j] = A.sc[(int64_t)j * n + r]; }
+            for (int j = 0; j < KU; ++j) cr[j] = j < A.K ? A.sc[(int64_t)j * n + r] : 0;
+#pragma unroll
+            for (int j = 0; j < KU; ++j) kr[j] = (j < A.K && cr[j] != 0) ? A.skey[(int64_t)j * n + r] : k0;
+        } else {
+#pragma unroll
+            for (int j = 0; j < KU; ++j) {
+                kr[j] = k0; cr[j] = 0;
+                if (j < A.K) { kr[j] = A.skey[(int64_t)j * n + r]; cr[j] = A.sc[(int64_t)j * n + r]; }
+            }
         }
         if (touched) {
             uint64_t m = 0;

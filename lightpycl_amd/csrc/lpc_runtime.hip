@@ -123,6 +123,7 @@ struct lpc_handle {
     bool fork_pending = false;                      // run_intersect -> run_queue: the fork event is still to record
     bool ev_sysfence = true;                        // LPC_EV_SYSFENCE=0: events without the system-scope fence (measured slower)
     int xcd_walk = 0;                               // LPC_XCD_WALK: packet-range root shards, XCD-local k_rootwalk (QueueArgs::xcd)
+    int shade_cfirst = 0;                           // LPC_SHADE_CFIRST: traced shading reads a slot's key only if its count > 0 (measured neutral)
     int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
     bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
@@ -1443,6 +1444,7 @@ static ShadeArgs shade_args(lpc_handle *h, const RaysIn &in, const int32_t *meas
     A.verts = (const float *)h->d_verts.p;
     A.max_ray_len = max_ray_len; A.ior_env = ior_env;
     A.o = shade_ptrs(h, extra);
+    A.cfirst = 0;
     return A;
 }
 
@@ -1457,6 +1459,7 @@ static int run_shade(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, in
     A.verts = (const float *)h->d_verts.p;
     A.max_ray_len = max_ray_len; A.ior_env = ior_env;
     A.o = shade_ptrs(h, extra);
+    A.cfirst = 0;                           // slots may hold the reference's non-uniform initial state
     LPC_KU_LAUNCH(h, k_shade, dim3(grid1(n)), dim3(256), h->stream, A);
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -1538,6 +1541,7 @@ int lpc_open(int device, lpc_handle **out)
     h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
+    h->shade_cfirst = (int)env_int("LPC_SHADE_CFIRST", h->shade_cfirst);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
     h->xcd_walk = (int)env_int("LPC_XCD_WALK", h->xcd_walk);
     h->roots_tasks = env_int("LPC_ROOTS_TASKS", h->roots_tasks);
@@ -2188,6 +2192,7 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             const size_t Cs = (size_t)h->ws_rays;
             StageArgs G;
             G.S = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
+            G.S.cfirst = h->shade_cfirst ? 1 : 0;        // the slots start uniform-clean here
             G.stR = (float *)h->w_shf.p;                // the 20 shade-output arrays hold the staging rows
             G.stT = (float *)h->w_shi.p;
             G.stM = (float *)h->w_soa.p;

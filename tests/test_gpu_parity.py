@@ -84,7 +84,7 @@ _POLICIES = [
     dict(LPC_Q_WALK_WPB="4", LPC_SPILL_WPB="4"), dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"),
     dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_WALK_WAVES="7"), dict(LPC_SHADE_KU="0"), dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
     dict(LPC_XCD_WALK="1"), dict(LPC_XCD_WALK="1", LPC_Q_WALK_BLOCKS="2"), dict(LPC_XCD_WALK="1", LPC_Q_WALK_BLOCKS="3"),
-    dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_EV_SYSFENCE="0"), dict(LPC_FORK_LATE="1"),
+    dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_EV_SYSFENCE="0"), dict(LPC_FORK_LATE="1"), dict(LPC_SHADE_CFIRST="1"),
     dict(LPC_ROOTS_TASKS="0"), dict(LPC_ROOTS_TASKS="100000000"), dict(LPC_ROOTS_TASKS="1000000", LPC_Q_TARGET="1"),
     dict(LPC_XCD_WALK="1", LPC_ROOTS_S="0", LPC_Q_TARGET="10000000"), dict(LPC_XCD_WALK="1", LPC_ROOTS_S="0"),
     # persistent work queue (k_roots + k_trav): claim batch, piece level, hand-over

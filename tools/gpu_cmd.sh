@@ -1,1 +1,4 @@
-BENCH_ARGS="--steps 30 --warmup 3 --no-cpu" bash tools/gpu_ab.sh 'LPC_Q_TARGET=45000' 'LPC_Q_TARGET=95000' 'LPC_BUDGET=20' 'LPC_BUDGET=28' 'LPC_Q_TARGET=65536' 'LPC_Q_TARGET=45000' 'LPC_Q_TARGET=95000' 'LPC_BUDGET=20' 'LPC_BUDGET=28'
+mkdir -p gpurun_out/v
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/v/pytest.log 2>&1 || { tail -30 gpurun_out/v/pytest.log; exit 1; }
+tail -1 gpurun_out/v/pytest.log
+BENCH_ARGS="--steps 30 --warmup 3 --no-cpu" bash tools/gpu_ab.sh 'LPC_SHADE_CFIRST=0' 'LPC_SHADE_CFIRST=1' 'LPC_SHADE_CFIRST=0' 'LPC_SHADE_CFIRST=1' 'LPC_SHADE_CFIRST=0' 'LPC_SHADE_CFIRST=1'

@@ -19,7 +19,7 @@ from lightpycl_amd.engine import Engine  # noqa: E402
 
 KNOBS = ("KEY", "LARGE_PER_TRI", "BUDGET_LARGE", "LARGE_N", "FLAT", "TARGET_BLOCKS", "SORT", "BUDGET", "SPILL_CAP", "SPILL_BLOCKS", "LOOP", "SLIVER_WAVES",
          "SLIVER_PPW", "NODE_W", "SPILL_LEVELS", "PAIR_SHIFT", "SORT_MIN", "LOOP_MIN", "GATHER_AOS", "SLIVER_RAYS", "WAVE_TARGET", "SLIVER_CULL", "SPILL_SHRINK", "SPILL_MIN_BLOCKS", "LANE_MAX", "LANE_G", "ISECT_MINB", "ONESWEEP_MIN", "SPILL_LEVELS_SMALL", "FUSE_SHADE", "XCD_ROWS", "CHAIN", "CHUNK", "QUEUE", "TRACED", "TRACED_SORT", "Q_TARGET", "Q_WALK_BLOCKS", "Q_WALK_WPB",
-         "SPILL_WPB", "SIDE_STREAM", "EARLY_ACC", "DBG", "FUSE_COMPACT", "SLIVER_LATE", "WALK_WAVES", "HALF", "SHADE_KU", "ROOTS_S", "XCD_WALK", "ROOTS_TASKS", "EV_SYSFENCE", "FORK_LATE")
+         "SPILL_WPB", "SIDE_STREAM", "EARLY_ACC", "DBG", "FUSE_COMPACT", "SLIVER_LATE", "WALK_WAVES", "HALF", "SHADE_KU", "ROOTS_S", "XCD_WALK", "ROOTS_TASKS", "EV_SYSFENCE", "FORK_LATE", "SHADE_CFIRST")
 name = sys.argv[1] if len(sys.argv) > 1 else "synthetic"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
