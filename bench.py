@@ -7,16 +7,30 @@ scene (every iteration until the reference's termination rule), with the rays
 resident in HBM when the timed region starts (lpc_trace_reset restores them
 device-to-device).  value = ray-bounces of all ranks / max-over-ranks time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--no-cpu] [--no-configs]
 
 Multi-GPU: launched by torch.distributed.run; rays shard by rank (independent
-seeds, weak scaling), the scene is replicated, and each iteration all-reduces
-(power left, live rays) over RCCL so every rank takes the reference's global
-termination decision; per-mesh measured power is all-reduced at trace end.
+seeds, weak scaling), the scene is replicated.  Each iteration's termination
+decision (iterative_tracer.py:383-391) is taken inside the library's trace loop
+on the stats all-reduced over the ranks of the node through the library's
+shared-memory hook (lpc_set_allreduce + lpc_shm_allreduce); the trace-end
+histogram and the timing go over RCCL (torch.distributed "nccl").
+
+The line also carries:
+  parity        the timed workload checked against the oracle: the first bounce
+                of the rank's first --cpu-rays rays bit for bit (the same oracle
+                outputs the cpu_baseline leg times), the trace's first-iteration
+                counts against them, and every timed step's per-iteration counts
+                and measured power identical;
+  roofline      HBM roofline of k_rootwalk (algorithmic bytes / its own average
+                launch time from HIP events; traffic from the committed rocprofv3
+                --pmc summary);
+  configs       BASELINE.json configs 2-4 at full size (N=1 only).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -29,60 +43,143 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector peak
-# MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, 2.4 GHz, a wave64 VALU instruction issues over
-# 2 cycles -> chip-wide VALU issue peak in wave-instructions per second
+# MI355X_MICROARCH.md ("v_fma_f32 (wave64): 2 cyc (SIMD-32)"; "4 SIMD-32 vector units"
+# per CU): 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction =
+# chip-wide VALU issue peak in wave-instructions per second (= 157.3 TF / 64 lanes / 2 flops)
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 RAY_BYTES = 156                # algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # per triangle per bounce-iteration
 MT_FLOPS = 46                  # Moller-Trumbore flops per ray-triangle test
-# the hierarchy-traversal kernel timed for the roofline, by LPC_QUEUE launch policy
-HIER_KERNEL = {"0": "k_intersect", "1": "k_trav", "2": "k_rootwalk"}
+WALK_KERNEL = "k_rootwalk"     # the hierarchy-walk kernel the HIP events time
+# BASELINE.json configs 2-4: scene, rays, depth (full size, one GPU)
+CONFIGS = [("parabolic", 1_000_000, 4), ("lens", 10_000_000, 8), ("eye", 10_000_000, 16)]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     ap.add_argument("--cpu-rays", type=int, default=1 << 20, help="CPU baseline sample (rays, one bounce)")
+    ap.add_argument("--no-configs", action="store_true", help="skip BASELINE configs 2-4")
     ap.add_argument("--no-prof", action="store_true", help="no HIP events in the timed region (A/B of their cost)")
     return ap.parse_args()
 
 
+def src_sha16():
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "lightpycl_amd", "csrc", "lpc_kernels.hip"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def load_pmc():
-    """Per-launch PMC figures of the hierarchy kernel from the committed rocprofv3 --pmc
-    summary (profiles/pmc_intersect.json, written by tools/pmc_summary.py), or {}."""
+    """Per-launch PMC figures of the walk kernel from the committed rocprofv3 --pmc
+    summary (profiles/pmc_intersect.json, tools/pmc_summary.py); marked stale when
+    it was collected on another version of the kernels."""
     p = os.path.join(ROOT, "profiles", "pmc_intersect.json")
-    if os.path.exists(p):
-        try:
-            with open(p) as f:
-                return json.load(f)
-        except Exception:
-            return {}
-    return {}
+    try:
+        with open(p) as f:
+            pmc = json.load(f)
+    except Exception:
+        return {}
+    pmc["stale"] = pmc.get("kernels_sha16") != src_sha16() or pmc.get("kernel") not in (None, WALK_KERNEL)
+    return pmc
 
 
-def cpu_baseline(sc, nrays):
-    """Oracle (C/OpenMP restatement of the reference kernels) on a bounded sample:
-    the first `nrays` rays of the same workload, one bounce."""
+def rays_of(sc):
+    o = np.concatenate([np.asarray(s.rays_origin, np.float32) for s in sc.sources])
+    d = np.concatenate([np.asarray(s.rays_dir, np.float32) for s in sc.sources])
+    p = np.concatenate([np.asarray(s.rays_power, np.float32).reshape(-1) for s in sc.sources])
+    return o, d, p
+
+
+def cpu_leg(sc, eng, o, d, p, nrays, first_stats, timed):
+    """Oracle (C/OpenMP restatement of the reference kernels) on the first `nrays`
+    rays of the workload, one bounce: timed as the CPU baseline (timed=True), and
+    its outputs compared bit for bit with liblpc's bounce of the same rays, and
+    (when the sample is the whole population) with the timed trace's first
+    iteration counts."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
-    o = np.concatenate([np.asarray(s.rays_origin, np.float32) for s in sc.sources])[:nrays]
-    d = np.concatenate([np.asarray(s.rays_dir, np.float32) for s in sc.sources])[:nrays]
-    p = np.concatenate([np.asarray(s.rays_power, np.float32).reshape(-1) for s in sc.sources])[:nrays]
+    n = min(nrays, len(p))
+    o, d, p = o[:n], d[:n], p[:n]
     S = oracle.Scene(sc.meshes)
-    n = o.shape[0]
+    z = np.zeros(n, np.int32)
+    pm = np.full(n, -2, np.int32)
     t = time.perf_counter()
-    oracle.bounce(S, o, d, p, np.zeros(n, np.int32), np.full(n, -2, np.int32), sc.max_ray_len, sc.ior_env)
+    ref = oracle.bounce(S, o, d, p, z, pm, sc.max_ray_len, sc.ior_env)
     dt = time.perf_counter() - t
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return dict(value=n / dt, unit="ray-bounces/s", cores=cores, kind="port",
-                sample=f"first {n} rays of the workload, 1 bounce (intersect+postproc+Fresnel) over "
-                       f"{S.tri_count} triangles, {dt:.2f} s",
-                ri_per_s=n * S.tri_count / dt)
+    g = eng.bounce(o, d, p, z, pm, sc.max_ray_len, sc.ior_env)
+    bad = np.zeros(n, bool)
+    for k in ("isect_mid", "isect_idx", "meas", "r_meas", "t_meas", "n1", "n2", "pow", "r_pow", "t_pow"):
+        bad |= np.asarray(g[k]).reshape(-1) != np.asarray(ref[k]).reshape(-1)
+    for k in ("dest", "r_dir", "t_dir"):
+        bad |= np.any(g[k][:, :3] != ref[k][:, :3], axis=1)
+    parity = {"rays": int(n), "mismatches": int(bad.sum()),
+              "fields": "dest, isect mesh/triangle, n1, n2, meas, r/t dir, r/t pow, dissipated pow (bitwise)",
+              "checked_against": "oracle/lpc_oracle.c (C restatement of kernel_reflect_refract_intersect.cl)"}
+    if n == len(first_stats["population"]):
+        kr = int(np.sum(ref["r_meas"] == 0))
+        kt = int(np.sum(ref["t_meas"] == 0))
+        km = int(np.sum(ref["meas"] == 1))
+        pw = float(np.sum(np.concatenate([ref["r_pow"][ref["r_meas"] == 0], ref["t_pow"][ref["t_meas"] == 0]]),
+                          dtype=np.float64))
+        st = first_stats["stats"]
+        parity["trace_first_iteration"] = {
+            "n_reflect": [int(st.n_reflect), kr], "n_refract": [int(st.n_refract), kt],
+            "n_measured": [int(st.n_measured), km], "power_next": [float(st.power_next), pw],
+            "match": bool(st.n_reflect == kr and st.n_refract == kt and st.n_measured == km
+                          and abs(st.power_next - pw) <= 1e-12 * max(abs(pw), 1e-300))}
+    base = None
+    if timed:
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        base = dict(value=n / dt, unit="ray-bounces/s", cores=cores, kind="port",
+                    sample=f"first {n} rays of the workload, 1 bounce (intersect+postproc+Fresnel) over "
+                           f"{S.tri_count} triangles, {dt:.2f} s",
+                    ri_per_s=n * S.tri_count / dt)
+    return parity, base
+
+
+def run_configs(Engine, ShardedTrace, scenes):
+    """BASELINE.json configs 2-4 at full size on this GPU: whole traces with the
+    rays resident, the hierarchy walk's share of the step from HIP events."""
+    out = {}
+    for name, n, depth in CONFIGS:
+        sc = scenes.BUILDERS[name](n=n, seed=7, iterations=depth)
+        o, d, p = rays_of(sc)
+        e = Engine(0)
+        e.upload_meshes(sc.meshes)
+        e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+        in_pow = float(np.sum(p, dtype=np.float64))
+        run = ShardedTrace(e)
+        steps = 1 if name == "eye" else 5
+        e.reset()
+        run.run(depth, sc.tau, in_pow, wait=False)            # warm-up (allocations)
+        e.sync()
+        e.prof_enable(True, light=True)
+        e.prof_read(reset=True)
+        t = time.perf_counter()
+        res = []
+        for _ in range(steps):
+            e.reset()
+            res.append(run.run(depth, sc.tau, in_pow, wait=False))
+        e.sync()
+        dt = (time.perf_counter() - t) / steps
+        pr = e.prof_read(reset=True)
+        e.prof_enable(False)
+        r = res[-1]
+        b = int(r["bounces"])
+        out[name] = {"rays": n, "depth": depth, "triangles": int(e.tri_count), "iterations": int(r["iterations"]),
+                     "ray_bounces": b, "ms_per_trace": dt * 1e3, "ray_bounces_per_s": b / dt,
+                     "walk_kernel_share": pr["kernel_ms"] / steps / (dt * 1e3) if dt > 0 else None,
+                     "steps_identical": all(x["global_counts"] == r["global_counts"] for x in res),
+                     "measured_power": float(np.sum(r["mesh_power"])), "input_power": in_pow}
+        e.close()
+    return out
 
 
 def main():
@@ -105,24 +202,24 @@ def main():
         dist.barrier()
     from lightpycl_amd import scenes
     from lightpycl_amd.engine import Engine
-    from lightpycl_amd.distributed import ShardedTrace, TorchComm
+    from lightpycl_amd.distributed import ShardedTrace, ShmComm, TorchComm
 
     sc = scenes.synthetic(n=a.rays, seed=7 + rank)
     eng = Engine(local)
     eng.upload_meshes(sc.meshes)
-    o = np.concatenate([np.asarray(s.rays_origin, np.float32) for s in sc.sources])
-    d = np.concatenate([np.asarray(s.rays_dir, np.float32) for s in sc.sources])
-    p = np.concatenate([np.asarray(s.rays_power, np.float32).reshape(-1) for s in sc.sources])
+    o, d, p = rays_of(sc)
     eng.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
     in_pow = float(np.sum(p, dtype=np.float64))
     comm = TorchComm(dist, local) if dist else None
-    runner = ShardedTrace(eng, comm)
+    shm = ShmComm.from_dist(dist) if dist else None
+    runner = ShardedTrace(eng, comm, iter_comm=shm)
+    in_pow_all = float(comm.allreduce_sum([in_pow])[0]) if comm else in_pow
 
     def step():
-        # one process: the trace returns once its outputs are final, so the next
-        # step's launches queue behind its last row moves (sync() waits for all)
+        # the trace returns once its outputs are final, so the next step's launches
+        # queue behind its last row moves (sync() waits for all)
         eng.reset()
-        return runner.run(sc.iterations, sc.tau, in_pow, wait=False)
+        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_pow_all)
 
     def sync():
         eng.sync()
@@ -131,48 +228,65 @@ def main():
             torch.cuda.synchronize(local)
             dist.barrier()
 
+    # the first iteration alone, for the parity leg (same stats the timed trace starts with)
+    eng.reset()
+    st0, _ = eng.iterate()
+    first = {"stats": st0, "population": p}
+    eng.sync()
     for _ in range(a.warmup):
         step()
     if not a.no_prof:
-        eng.prof_enable(True, light=True)    # HIP events around the hierarchy kernel launches only
+        eng.prof_enable(True, light=True)    # HIP events around the walk kernel's launches only
     eng.prof_read(reset=True)
     sync()
     t0 = time.perf_counter()
     bounces = 0
     iters = 0
+    results = []
     for _ in range(a.steps):
         r = step()
         bounces += r["bounces"]
         iters += r["iterations"]
+        results.append((r["global_counts"], [float(x) for x in r["mesh_power"]]))
     sync()
     dt = time.perf_counter() - t0
     prof = eng.prof_read(reset=True)
+    eng.prof_enable(False)
+    steps_identical = all(x == results[0] for x in results)
+    # trace-end histogram over RCCL (the north star's all-reduce), outside the timed region
+    eng.reset()
+    hr = runner.run(sc.iterations, sc.tau, in_pow, hist=(sc.hist_limits, sc.hist_points),
+                    input_power_global=in_pow_all)
+    hist_total = float(np.sum(hr["hist"][0]) * ((sc.hist_limits[0][1] - sc.hist_limits[0][0]) / sc.hist_points) ** 2)
     if dist:
         import torch
-        t = torch.tensor([dt, float(bounces)], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt, float(bounces), 0.0 if steps_identical else 1.0], dtype=torch.float64,
+                         device=f"cuda:{local}")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         dt, bounces_all = float(mx[0]), float(t[1])
+        steps_identical = float(mx[2]) == 0.0
     else:
         bounces_all = float(bounces)
     if rank != 0:
+        shm.close()
         if dist:
             dist.destroy_process_group()
         return
 
     M = eng.tri_count
     launches = max(prof["intersect_launches"], 1)
-    avg_ms = prof["kernel_ms"] / launches               # the hierarchy kernel's launches alone
-    kernel = HIER_KERNEL.get(os.environ.get("LPC_QUEUE", "2"), "k_rootwalk")
+    avg_ms = prof["kernel_ms"] / launches               # the walk kernel's launches alone
     rays_per_launch = bounces / launches                 # rank-0 launches
     alg_bytes = rays_per_launch * RAY_BYTES + M * TRI_BYTES
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     pairs_per_s = bounces_all * M / dt                   # reference-equivalent RI/s (sum N_iter * M / T)
     mt_tflops = pairs_per_s * MT_FLOPS / 1e12
     pmc = load_pmc()
-    traffic = pmc.get("hbm_bytes_per_launch")
-    valu_per_launch = pmc.get("sq_insts_valu_mean")
+    stale = pmc.get("stale", True)
+    traffic = None if stale else pmc.get("hbm_bytes_per_launch")
+    valu_per_launch = None if stale else pmc.get("sq_insts_valu_mean")
     valu_rate = valu_per_launch / (avg_ms * 1e-3) if valu_per_launch and avg_ms > 0 else None
     out = {
         "metric": "ray-bounces/sec @ 1M rays x 100k tris",
@@ -193,19 +307,20 @@ def main():
                    "parallelism": f"ray-sharded x{world}", "iterations_per_step": iters / a.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": kernel, "avg_launch_ms": avg_ms,
+                     "kernel": WALK_KERNEL, "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "note": f"achieved = algorithmic bytes per launch / {kernel}'s own average "
-                             "launch time (HIP events on its stream); traffic = 2*FETCH_SIZE+WRITE_SIZE per "
-                             f"{kernel} launch (profiles/pmc_intersect.json)"},
-        # the bound that actually limits the hierarchy kernel: executed VALU issue
-        "roofline_valu": {"bound": "valu", "kernel": kernel,
+                     "note": f"achieved = algorithmic bytes per launch (156 B x rays + 40 B x triangles) / "
+                             f"{WALK_KERNEL}'s own average launch time (HIP events on its stream); traffic = "
+                             f"2*FETCH_SIZE+WRITE_SIZE per {WALK_KERNEL} launch from profiles/pmc_intersect.json "
+                             f"(null when that summary was collected on other kernel sources)"},
+        # the bound that actually limits the walk kernel: executed VALU issue
+        "roofline_valu": {"bound": "valu", "kernel": WALK_KERNEL,
                           "achieved": valu_rate, "peak": VALU_ISSUE_PEAK, "unit": "wave-instr/s",
                           "frac": valu_rate / VALU_ISSUE_PEAK if valu_rate else None,
-                          "valu_insts_per_launch": valu_per_launch,
-                          "note": f"executed VALU wave-instructions per {kernel} launch (PMC SQ_INSTS_VALU, "
+                          "valu_insts_per_launch": valu_per_launch, "pmc_stale": stale,
+                          "note": f"executed VALU wave-instructions per {WALK_KERNEL} launch (PMC SQ_INSTS_VALU, "
                                   "profiles/pmc_intersect.json) / its live average launch time / chip issue "
-                                  "peak (256 CU x 4 SIMD x 2.4 GHz / 2 cycles)"},
+                                  "peak (256 CU x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction)"},
         # brute-force equivalent: what the reference's O(N*M) loop would have to sustain
         "ri_equivalent": {"ri_per_s": pairs_per_s, "mt_tflops_equiv": mt_tflops,
                           "fp32_peak_tflops": FP32_PEAK_TFLOPS,
@@ -213,12 +328,27 @@ def main():
                                   "triangle) / whole-job time; above the FP32 peak because the hierarchy "
                                   "filter skips almost all tests: not a utilisation figure"},
         "ri_per_s": pairs_per_s,
+        "exchange": {"per_iteration_us": prof["xchg_us"] / max(prof["xchg_calls"], 1),
+                     "calls": prof["xchg_calls"], "transport": "lpc_shm_allreduce" if world > 1 else None,
+                     "trace_end": "RCCL all-reduce (histogram)" if world > 1 else None},
+        "hist_total_power": hist_total,
         "cpu_baseline": None,
     }
-    if world == 1 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(sc, a.cpu_rays)
+    par = {"steps_identical": bool(steps_identical)}
+    if not a.no_cpu:
+        # N=1: the timed CPU baseline and the bitwise check on the same oracle outputs;
+        # N>1: rank 0 checks a 20k-ray sample of its shard (untimed)
+        nr = a.cpu_rays if world == 1 else 20000
+        pp, base = cpu_leg(sc, eng, o, d, p, nr, first, timed=(world == 1))
+        par.update(pp)
+        out["cpu_baseline"] = base
+    out["parity"] = par
+    if world == 1 and not a.no_configs:
+        eng.close()
+        out["configs"] = run_configs(Engine, ShardedTrace, scenes)
     print(json.dumps(out))
     if dist:
+        shm.close()
         dist.destroy_process_group()
 
 

@@ -158,6 +158,31 @@ int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_i
  * to the host waits for them first; lpc_sync waits explicitly. */
 int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                         int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+/* ---- ray-sharded trace: one process per GPU ---------- */
+/* All-reduce (sum, in place) of n doubles over the ranks of a sharded trace;
+ * every rank must receive the identical bits.  Returns 0 on success. */
+typedef int (*lpc_allreduce_fn)(void *ctx, double *vals, int32_t n);
+/* Install (fn != NULL) or remove the all-reduce hook of h.  With a hook, the
+ * loop of lpc_trace_run(_async) all-reduces each iteration's stats and takes
+ * the reference's termination decisions (iterative_tracer.py:383-391) on the
+ * sums over all ranks, so every rank stops at the iteration a single device
+ * tracing all rays would; *measured_count and mesh_power are then the sums over
+ * all ranks too.  per_iter keeps this rank's own stats. */
+int lpc_set_allreduce(lpc_handle *h, lpc_allreduce_fn fn, void *ctx);
+/* The all-reduced per-iteration stats of the last lpc_trace_run(_async) (this
+ * rank's own without a hook).  *n_iter = iterations; at most cap are copied. */
+int lpc_trace_global_stats(lpc_handle *h, lpc_iter_stats *per_iter, int32_t cap, int32_t *n_iter);
+/* The library's all-reduce for the ranks of one node: POSIX shared memory
+ * segment `name`, created by the rank passing create != 0 (the others wait for
+ * it); rank-order sums, so identical bits on every rank.  lpc_shm_allreduce is
+ * an lpc_allreduce_fn (ctx = the comm).  lpc_shm_comm_unlink removes the name
+ * once every rank has opened it (the mapping stays); close unmaps. */
+typedef struct lpc_shm_comm lpc_shm_comm;
+int lpc_shm_comm_open(const char *name, int32_t rank, int32_t world, int32_t create, lpc_shm_comm **out);
+int lpc_shm_comm_unlink(lpc_shm_comm *comm);
+int lpc_shm_allreduce(void *comm, double *vals, int32_t n);
+int lpc_shm_comm_close(lpc_shm_comm *comm);
+
 /* Wait until the handle's stream has finished every queued kernel. */
 int lpc_sync(lpc_handle *h);
 /* Current population size. */
@@ -204,6 +229,8 @@ typedef struct {
     int64_t tail_exact;      /* their exact tests                               */
     double kernel_ms;        /* k_intersect launches alone (HIP events around each
                                 launch; intersect_ms adds k_spill, k_packet, k_slivers) */
+    double xchg_us;          /* host time spent in the all-reduce hook (lpc_set_allreduce) */
+    int64_t xchg_calls;      /* its calls (per-iteration stats + trace-end aggregates)  */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * traversal counters (2, diagnostic: adds atomics), timing plus per-wave

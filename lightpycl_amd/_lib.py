@@ -36,7 +36,7 @@ class Prof(ctypes.Structure):
                 ("heavy_piece_ticks", ctypes.c_int64), ("piece_ticks", ctypes.c_int64),
                 ("tail_waves", ctypes.c_int64), ("tail_nodes", ctypes.c_int64),
                 ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64),
-                ("kernel_ms", ctypes.c_double)]
+                ("kernel_ms", ctypes.c_double), ("xchg_us", ctypes.c_double), ("xchg_calls", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p
@@ -75,7 +75,16 @@ _PROTOS = {
     "lpc_prof_enable": [_P, _INT],
     "lpc_prof_read": [_P, _P, _INT],
     "lpc_prof_waves": [_P, _P, _I64, _P],
+    "lpc_set_allreduce": [_P, _P, _P],
+    "lpc_trace_global_stats": [_P, _P, _I32, _P],
+    "lpc_shm_comm_open": [ctypes.c_char_p, _I32, _I32, _I32, _P],
+    "lpc_shm_comm_unlink": [_P],
+    "lpc_shm_allreduce": [_P, _P, _I32],
+    "lpc_shm_comm_close": [_P],
 }
+
+# lpc_allreduce_fn (include/lpc.h): int (*)(void *ctx, double *vals, int32_t n)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32)
 
 EXPORTED = tuple(_PROTOS) + ("lpc_last_error",)
 

@@ -5,6 +5,7 @@
 // population of a trace.  All launches go to the handle's stream.
 #include "lpc_kernels.hip"
 #include "lpc.h"
+#include "lpc_comm.hpp"
 #include <hip/hip_ext.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -227,6 +228,13 @@ struct lpc_handle {
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
     int64_t prof_launches = 0, prof_pairs = 0;
+    // ray-sharded trace (lpc_set_allreduce): the termination decisions and the
+    // trace-end aggregates over all ranks
+    lpc_allreduce_fn xchg = nullptr;
+    void *xchg_ctx = nullptr;
+    std::vector<lpc_iter_stats> gstats;             // all-reduced per-iteration stats of the last lpc_trace_run
+    double xchg_us = 0.0;                           // host time inside the hook (lpc_prof)
+    int64_t xchg_calls = 0;
 };
 
 static std::string g_open_err;
@@ -2027,24 +2035,53 @@ int lpc_trace_reset(lpc_handle *h)
     return 0;
 }
 
+// All-reduce (sum) of the iteration's stats over the ranks of a sharded trace.
+static int xchg_stats(lpc_handle *h, const lpc_iter_stats &S, lpc_iter_stats *G)
+{
+    double v[5] = {(double)S.n_in, (double)S.n_reflect, (double)S.n_refract, (double)S.n_measured, S.power_next};
+    const double t0 = host_us();
+    const int rc = h->xchg(h->xchg_ctx, v, 5);
+    h->xchg_us += host_us() - t0;
+    h->xchg_calls += 1;
+    if (rc != 0) return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
+    G->n_in = (int64_t)v[0]; G->n_reflect = (int64_t)v[1]; G->n_refract = (int64_t)v[2];
+    G->n_measured = (int64_t)v[3]; G->power_next = v[4];
+    return 0;
+}
+
 static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                      int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
     *n_iter = 0;
+    h->gstats.clear();
     for (int32_t i = 0; i < max_iter; ++i) {
         lpc_iter_stats S;
         RETIF(lpc_trace_iterate(h, nullptr, nullptr, nullptr, nullptr, nullptr, &S));
         per_iter[i] = S;
         *n_iter = i + 1;
-        if (S.power_next < power_threshold) break;          // :383
-        if (S.n_reflect + S.n_refract == 0) break;          // :389
+        // sharded trace: every rank decides on the sums over all ranks (the
+        // identical bits everywhere), so all stop at the iteration a single
+        // device would (iterative_tracer.py:383-391)
+        lpc_iter_stats G = S;
+        if (h->xchg) RETIF(xchg_stats(h, S, &G));
+        h->gstats.push_back(G);
+        if (G.power_next < power_threshold) break;          // :383
+        if (G.n_reflect + G.n_refract == 0) break;          // :389
     }
     if (measured_count || mesh_power) {                     // the trace's aggregates, same call
         int64_t c = 0;
-        RETIF(lpc_trace_measured(h, &c, mesh_power));
+        std::vector<double> mp((size_t)h->K + 1, 0.0);
+        RETIF(lpc_trace_measured(h, &c, mp.data()));
+        if (h->xchg) {                                      // trace-end sums over the ranks
+            mp[(size_t)h->K] = (double)c;
+            if (h->xchg(h->xchg_ctx, mp.data(), h->K + 1) != 0)
+                return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
+            c = (int64_t)mp[(size_t)h->K];
+        }
         if (measured_count) *measured_count = c;
+        if (mesh_power) memcpy(mesh_power, mp.data(), (size_t)h->K * 8);
     }
     if (wait) RETIF(settle(h));                             // the trace's last kernels too
     return 0;
@@ -2060,6 +2097,55 @@ int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold,
                         int32_t *n_iter, int64_t *measured_count, double *mesh_power)
 {
     return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, false);
+}
+
+int lpc_set_allreduce(lpc_handle *h, lpc_allreduce_fn fn, void *ctx)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    h->xchg = fn;
+    h->xchg_ctx = ctx;
+    return 0;
+}
+
+int lpc_trace_global_stats(lpc_handle *h, lpc_iter_stats *per_iter, int32_t cap, int32_t *n_iter)
+{
+    if (!h || !n_iter) return set_err(h, LPC_E_ARG, "null argument");
+    *n_iter = (int32_t)h->gstats.size();
+    if (per_iter)
+        for (int32_t i = 0; i < std::min(cap, *n_iter); ++i) per_iter[i] = h->gstats[(size_t)i];
+    return 0;
+}
+
+int lpc_shm_comm_open(const char *name, int32_t rank, int32_t world, int32_t create, lpc_shm_comm **out)
+{
+    if (!out) return set_err(nullptr, LPC_E_ARG, "shm comm: null output");
+    std::string err;
+    lpcc::ShmComm *c = nullptr;
+    if (lpcc::shm_open_comm(name, rank, world, create, &c, &err) != 0) return set_err(nullptr, LPC_E_ARG, err);
+    *out = (lpc_shm_comm *)c;
+    return 0;
+}
+
+int lpc_shm_comm_unlink(lpc_shm_comm *c)
+{
+    if (!c) return set_err(nullptr, LPC_E_ARG, "shm comm: null");
+    lpcc::shm_unlink_comm((lpcc::ShmComm *)c);
+    return 0;
+}
+
+int lpc_shm_allreduce(void *comm, double *vals, int32_t n)
+{
+    lpcc::ShmComm *c = (lpcc::ShmComm *)comm;
+    if (!c) return set_err(nullptr, LPC_E_ARG, "shm comm: null");
+    if (lpcc::shm_allreduce(c, vals, n) != 0)
+        return set_err(nullptr, LPC_E_STATE, c->err.empty() ? "shm comm: bad argument" : c->err);
+    return 0;
+}
+
+int lpc_shm_comm_close(lpc_shm_comm *c)
+{
+    lpcc::shm_close_comm((lpcc::ShmComm *)c);
+    return 0;
 }
 
 int lpc_sync(lpc_handle *h)
@@ -2488,6 +2574,8 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     out->kernel_ms = h->prof_kern_ms;
     out->shade_ms = h->prof_rest_ms;
     out->intersect_launches = h->prof_launches;
+    out->xchg_us = h->xchg_us;
+    out->xchg_calls = h->xchg_calls;
     out->pairs = h->prof_pairs;
     std::vector<unsigned long long> st(LPC_STATS_WORDS, 0ull);
     if (h->d_stats.p) HIPCHK(h, hipMemcpy(st.data(), h->d_stats.p, LPC_STATS_WORDS * 8, hipMemcpyDeviceToHost));
@@ -2506,6 +2594,7 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     }
     if (reset) {
         h->prof_isect_ms = h->prof_rest_ms = h->prof_kern_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
+        h->xchg_us = 0.0; h->xchg_calls = 0;
         if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
     }
     return 0;

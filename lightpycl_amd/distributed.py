@@ -18,6 +18,9 @@ All messages are a few doubles: latency-bound, one RCCL all-reduce each.  On CPU
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 
 
@@ -61,6 +64,61 @@ class TorchComm:
         return self.dist.get_world_size()
 
 
+class ShmComm:
+    """The library's intra-node all-reduce (lpc_shm_comm_*, POSIX shared memory):
+    rank-order sums, identical bits on every rank, ~1 us per exchange.  Installed
+    in an engine it runs inside lpc_trace_run's loop with no Python in between
+    (``native_hook``); ``allreduce_sum`` calls it from Python."""
+
+    def __init__(self, name, rank, world, create):
+        from . import _lib
+        self._lib = _lib
+        self.L = _lib.load()
+        self.rank = int(rank)
+        self.world = int(world)
+        c = ctypes.c_void_p()
+        _lib.check(self.L.lpc_shm_comm_open(name.encode(), self.rank, self.world, 1 if create else 0,
+                                            ctypes.byref(c)))
+        self.c = c
+
+    @classmethod
+    def from_dist(cls, dist):
+        """One segment per torch.distributed job: rank 0 names and creates it, the
+        others open it, then the name is unlinked (nothing is left in /dev/shm)."""
+        import secrets
+        rank, world = dist.get_rank(), dist.get_world_size()
+        box = [f"lpc_{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = cls(box[0], rank, world, create=(rank == 0))
+        dist.barrier()
+        comm.unlink()
+        return comm
+
+    def native_hook(self):
+        fn = ctypes.cast(self.L.lpc_shm_allreduce, ctypes.c_void_p)
+        return fn, self.c
+
+    def allreduce_sum(self, values):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float64).reshape(-1)).copy()
+        self._lib.check(self.L.lpc_shm_allreduce(self.c, v.ctypes.data_as(ctypes.c_void_p), v.shape[0]))
+        return v
+
+    def unlink(self):
+        if self.c:
+            self.L.lpc_shm_comm_unlink(self.c)
+
+    def close(self):
+        if getattr(self, "c", None):
+            self.L.lpc_shm_comm_close(self.c)
+            self.c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def shard_bounds(n, rank, world):
     """Contiguous shard [lo, hi) of n rays for `rank` (sizes differ by at most 1)."""
     q, r = divmod(n, world)
@@ -70,49 +128,63 @@ def shard_bounds(n, rank, world):
 
 class ShardedTrace:
     """Drive one rank's engine through the reference's iteration loop with global
-    termination decisions."""
+    termination decisions.
 
-    def __init__(self, engine, comm=None):
+    A liblpc engine runs the loop inside the library (lpc_trace_run(_async));
+    with a comm the per-iteration all-reduce is the library's hook
+    (``iter_comm``: the native shared-memory comm when given, else ``comm``
+    through a ctypes callback), so N > 1 adds one tiny exchange per iteration
+    and keeps the single-GPU pipelining.  The trace-end histogram is all-reduced
+    over ``comm`` (RCCL on GPU ranks).  Engines without ``run_local`` (the CPU
+    tests' OracleEngine) run the same loop here in Python."""
+
+    def __init__(self, engine, comm=None, iter_comm=None):
         self.engine = engine
         self.comm = comm
+        self.iter_comm = iter_comm if iter_comm is not None else comm
+        self._installed = None
 
     def _sum(self, vals):
         if self.comm is None:
             return np.asarray(vals, dtype=np.float64)
         return self.comm.allreduce_sum(vals)
 
-    def run(self, iterations, tau, input_power_local, hist=None, wait=True):
+    def run(self, iterations, tau, input_power_local, hist=None, wait=True, input_power_global=None):
         """Trace to the reference's termination.  hist=(limits, points): also bin
         the measured rays (get_binned_data_angular) on every rank and all-reduce
-        the histogram (float64, bin counts are additive).  wait=False (one
-        process): return once the outputs are final, without waiting for the last
-        rows to move on the device (engine.sync() waits)."""
-        in_pow = float(self._sum([input_power_local])[0])
+        the histogram (float64, bin counts are additive).  wait=False: return once
+        the outputs are final, without waiting for the last rows to move on the
+        device (engine.sync() waits).  input_power_global: the all-ranks input power
+        if already known (no all-reduce for it)."""
+        in_pow = (float(input_power_global) if input_power_global is not None
+                  else float(self._sum([input_power_local])[0]))
         thr = (1.0 - tau) * in_pow
         bounces = 0
         iters = 0
         counts = []
-        measured = None
-        if self.comm is None and hasattr(self.engine, "run_local"):
-            # one process: the same loop inside the library (lpc_trace_run)
-            stats, measured = self.engine.run_local(int(iterations), thr, wait=wait or hist is not None)
-            for st in stats:
+        if hasattr(self.engine, "run_local"):
+            if self.iter_comm is not None and self._installed is not self.iter_comm:
+                self.engine.set_allreduce(self.iter_comm)
+                self._installed = self.iter_comm
+            stats, (_, mesh_pow) = self.engine.run_local(int(iterations), thr, wait=wait or hist is not None)
+            glob = self.engine.global_stats() if self.iter_comm is not None else stats
+            bounces = sum(int(st.n_in) for st in stats)
+            iters = len(stats)
+            counts = [int(st.n_in) for st in glob]
+            mesh_pow = np.asarray(mesh_pow, dtype=np.float64)
+        else:
+            for _ in range(int(iterations)):
+                st, _ = self.engine.iterate()
                 bounces += int(st.n_in)
                 iters += 1
-                counts.append(int(st.n_in))
-            iterations = 0
-        for _ in range(int(iterations)):
-            st, _ = self.engine.iterate()
-            bounces += int(st.n_in)
-            iters += 1
-            tot = self._sum([st.n_in, st.power_next, st.n_reflect + st.n_refract])
-            counts.append(int(tot[0]))
-            if tot[1] < thr:
-                break
-            if tot[2] == 0:
-                break
-        _, mesh_pow = measured if measured is not None else self.engine.measured()
-        mesh_pow = self._sum(np.asarray(mesh_pow, dtype=np.float64))
+                tot = self._sum([st.n_in, st.power_next, st.n_reflect + st.n_refract])
+                counts.append(int(tot[0]))
+                if tot[1] < thr:
+                    break
+                if tot[2] == 0:
+                    break
+            _, mesh_pow = self.engine.measured()
+            mesh_pow = self._sum(np.asarray(mesh_pow, dtype=np.float64))
         out = dict(bounces=bounces, iterations=iters, global_counts=counts, mesh_power=mesh_pow)
         if hist is not None:
             limits, points = hist

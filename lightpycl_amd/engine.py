@@ -186,6 +186,42 @@ class Engine:
         return [_lib.IterStats.from_buffer_copy(arr[i]) for i in range(k.value)], (c.value,
                                                                                    mp[: self.mesh_count].copy())
 
+    # -- ray-sharded trace --------------------------------------------------------
+    def set_allreduce(self, comm):
+        """Install the all-reduce hook of lpc_trace_run's loop (lpc_set_allreduce):
+        the library's shared-memory comm (:class:`distributed.ShmComm`, native, no
+        Python in the loop) or any object with ``allreduce_sum(values) -> array``
+        (called back through ctypes).  None removes it."""
+        if comm is None:
+            self._xchg = None
+            self._c(self.L.lpc_set_allreduce(self.h, None, None))
+            return
+        native = getattr(comm, "native_hook", None)
+        if native is not None:
+            fn, ctx = native()
+            self._xchg = (comm, fn)
+            self._c(self.L.lpc_set_allreduce(self.h, fn, ctx))
+            return
+
+        def cb(_ctx, vals, n):
+            try:
+                v = np.ctypeslib.as_array(vals, shape=(n,))
+                v[:] = np.asarray(comm.allreduce_sum(v.copy()), dtype=np.float64).reshape(-1)
+                return 0
+            except Exception:           # an exception must not cross the C frame
+                return -1
+        fn = _lib.ALLREDUCE_FN(cb)
+        self._xchg = (comm, fn)         # keep the callback alive while installed
+        self._c(self.L.lpc_set_allreduce(self.h, ctypes.cast(fn, ctypes.c_void_p), None))
+
+    def global_stats(self):
+        """All-reduced per-iteration stats of the last run_local (lpc_trace_global_stats)."""
+        n = ctypes.c_int32(0)
+        self._c(self.L.lpc_trace_global_stats(self.h, None, 0, ctypes.byref(n)))
+        arr = (_lib.IterStats * max(n.value, 1))()
+        self._c(self.L.lpc_trace_global_stats(self.h, arr, n.value, ctypes.byref(n)))
+        return [_lib.IterStats.from_buffer_copy(arr[i]) for i in range(n.value)]
+
     def measured(self):
         """(count, per-mesh measured power float64[K])."""
         c = ctypes.c_int64(0)
@@ -268,4 +304,5 @@ class Engine:
                     group_tests=p.group_tests, wave_traversals=p.wave_traversals, exact_tests=p.exact_tests,
                     wave_hist=list(p.wave_hist), heavy_piece=p.heavy_piece, heavy_piece_ticks=p.heavy_piece_ticks,
                     piece_ticks=p.piece_ticks, tail_waves=p.tail_waves, tail_nodes=p.tail_nodes,
-                    tail_spread_urad=p.tail_spread_urad, tail_exact=p.tail_exact, kernel_ms=p.kernel_ms)
+                    tail_spread_urad=p.tail_spread_urad, tail_exact=p.tail_exact, kernel_ms=p.kernel_ms,
+                    xchg_us=p.xchg_us, xchg_calls=p.xchg_calls)

@@ -13,10 +13,14 @@ It is a restatement of the reference:
 * ``get_measured_rays`` (``iterative_tracer.py:395-411``) and
   ``get_binned_data_angular`` (``iterative_tracer.py:534-562``).
 
-Parity status: pinned only by the SURVEY.md section-4 known-answer rows and
-the per-iteration ray / triangle counts SURVEY.md records for the reference
-scenes (``tests/test_oracle_pins.py``); otherwise UNPINNED, because the
-reference (OpenCL C + Python 2 + PyOpenCL) cannot be executed in this image.
+Parity status: pinned against the reference's OWN kernels -- the unmodified
+``kernel_reflect_refract_intersect.cl`` compiled for gfx950 with ROCm's OpenCL
+device libraries (``oracle/Makefile`` target ``ref`` -> ``oracle/_ref/``,
+launched by ``tests/ref_gpu.py``) -- within SURVEY.md section 8c's fp32
+tolerances (``tests/test_ref_parity.py``, on the GPU), and on the CPU by the
+SURVEY.md section-4 known-answer rows and the reference-scene counts
+(``tests/test_oracle_pins.py``).  The reference's Python-2 host loop cannot be
+imported; :func:`trace` restates it.
 """
 from __future__ import annotations
 
@@ -156,12 +160,15 @@ def f32_sorted_sum(a):
 
 
 def trace(light_source, meshes, trace_iterations=100, trace_until_dissipated=0.99,
-          max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True):
+          max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True, bounce_fn=None):
     """Restatement of CL_Tracer.iterative_tracer (iterative_tracer.py:77-393).
 
     Returns (results, info) where results is the list of per-iteration tuples
     (rays_origin, rays_dest, rays_pow, rays_meas) and info holds the per-iteration
-    ray counts and the per-mesh measured power (float64)."""
+    ray counts and the per-mesh measured power (float64).  ``bounce_fn`` replaces
+    the three kernels (default: :func:`bounce`, the C restatement); the GPU tests
+    pass the reference's own kernels (``tests/ref_gpu.py``) here."""
+    bounce_fn = bounce if bounce_fn is None else bounce_fn
     max_ray_len = np.float32(max_ray_len)
     ior_env = np.float32(ior_env)
     origin = dirs = power = None
@@ -187,7 +194,7 @@ def trace(light_source, meshes, trace_iterations=100, trace_until_dissipated=0.9
     mesh_power = np.zeros(scene.mesh_count, np.float64)
     for _ in range(int(trace_iterations)):                         # :241
         counts.append(ray_count)
-        out = bounce(scene, origin, dirs, rays_pow, rays_meas, cur_mid, max_ray_len, ior_env)
+        out = bounce_fn(scene, origin, dirs, rays_pow, rays_meas, cur_mid, max_ray_len, ior_env)
         rays_dest = out["dest"]
         rays_pow = out["pow"].reshape(np.shape(rays_pow))           # :347 keeps the input shape
         rays_meas = out["meas"]

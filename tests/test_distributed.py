@@ -80,3 +80,89 @@ def test_shard_bounds_cover():
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
             assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1
+
+
+# -- the library's intra-node all-reduce (lpc_shm_comm_*), CPU only ------------------
+def _shm_worker(rank, world, name, out_dir):
+    sys.path.insert(0, os.path.dirname(HERE))
+    from lightpycl_amd.distributed import ShmComm
+    c = ShmComm(name, rank, world, create=(rank == 0))
+    rng = np.random.default_rng(rank)
+    res = {}
+    for n in (0, 1, 5, 8192, 20000):            # 20000 > one exchange chunk (8192 doubles)
+        v = rng.normal(size=n)
+        res[n] = (v, c.allreduce_sum(v))
+    for rep in range(200):                      # many back-to-back exchanges (buffer parity reuse)
+        x = c.allreduce_sum([rank + rep, 1.0])
+        assert x[0] == sum(r + rep for r in range(world)) and x[1] == world
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **{f"in{n}": a for n, (a, _) in res.items()},
+             **{f"out{n}": b for n, (_, b) in res.items()})
+    c.close()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shm_allreduce_identical_bits(tmp_path, world):
+    """lpc_shm_allreduce: every rank receives the rank-order sum, bit for bit
+    (so every rank takes the identical termination decision)."""
+    import secrets
+    name = f"lpc_test_{os.getpid()}_{secrets.token_hex(4)}"
+    mp.spawn(_shm_worker, args=(world, name, str(tmp_path)), nprocs=world, join=True)
+    got = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+    for n in (0, 1, 5, 8192, 20000):
+        want = got[0][f"in{n}"].copy()
+        for r in range(1, world):
+            want = want + got[r][f"in{n}"]
+        for r in range(world):
+            np.testing.assert_array_equal(got[r][f"out{n}"], want)
+    assert not os.path.exists(f"/dev/shm/{name}")
+
+
+def test_shm_comm_errors():
+    sys.path.insert(0, os.path.dirname(HERE))
+    from lightpycl_amd import _lib
+    from lightpycl_amd.distributed import ShmComm
+    with pytest.raises(_lib.LpcError):
+        ShmComm("x", 3, 2, create=True)         # rank out of range
+    c = ShmComm(f"lpc_single_{os.getpid()}", 0, 1, create=True)
+    np.testing.assert_array_equal(c.allreduce_sum([1.5, 2.0]), [1.5, 2.0])
+    c.close()
+
+
+def _worker_shm(rank, world, port, name, n, out_path):
+    """The sharded driver with the library's shared-memory comm for the
+    per-iteration decisions and gloo for the trace-end histogram."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lightpycl_amd import scenes
+    from lightpycl_amd.distributed import ShardedTrace, ShmComm, TorchComm, shard_bounds
+    from oracle_engine import OracleEngine
+    shm = ShmComm.from_dist(dist)
+    sc = scenes.BUILDERS[name](n=n, seed=2)
+    o = np.asarray(sc.sources[0].rays_origin, np.float32)
+    d = np.asarray(sc.sources[0].rays_dir, np.float32)
+    p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
+    lo, hi = shard_bounds(len(p), rank, world)
+    eng = OracleEngine(sc.meshes, o[lo:hi], d[lo:hi], p[lo:hi], sc.max_ray_len, sc.ior_env)
+    r = ShardedTrace(eng, shm).run(sc.iterations, sc.tau, float(np.sum(p[lo:hi], dtype=np.float64)),
+                                   hist=(HIST_LIMITS, HIST_POINTS))
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(dict(counts=r["global_counts"], mesh_power=list(map(float, r["mesh_power"]))), f)
+    shm.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_trace_shm_comm(oracle_mod, tmp_path):
+    from lightpycl_amd import scenes
+    out = str(tmp_path / "r.json")
+    mp.spawn(_worker_shm, args=(3, _free_port(), "lens", 2500, out), nprocs=3, join=True)
+    got = json.load(open(out))
+    sc = scenes.lens(n=2500, seed=2)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                               keep_results=False)
+    assert got["counts"] == info["counts"]
+    np.testing.assert_allclose(got["mesh_power"], info["mesh_power"], rtol=1e-12, atol=1e-12)
