@@ -234,10 +234,9 @@ typedef struct {
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * traversal counters (2, diagnostic: adds atomics), timing plus per-wave
- * records of the k_intersect grid (3, diagnostic), only the hierarchy kernel's
- * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs),
- * per-item records of the work-queue kernel k_trav (5, diagnostic; read with
- * lpc_prof_waves as pairs of 4-word records), or disable (0). */
+ * records of the k_intersect grid (3, diagnostic; LPC_QUEUE=0's walk), only the
+ * walk kernel's launches (4: kernel_ms, launches and pairs; the lightest, for
+ * timed runs), or disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
 /* Level 3: the last k_intersect launch's per-(piece, packet) records, 4 uint32

@@ -38,37 +38,21 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 #define LPC_STATS_PIECES 4096
 #define LPC_STATS_WORDS (LPC_STATS_PIECE + LPC_STATS_PIECES)
 
-// Per-launch device words of the intersect stage (uint32, reset by k_slot_init):
-// [0..5] population origin box (k_bbox, coherence key modes 1-2), [6..13]
-// hand-over queue lengths (k_intersect -> k_spill level 0 -> level 1 ...),
-// from word 32 the work queue's control words (k_roots / k_trav), every group on
-// a 128-byte line of its own: a device-scope atomic evicts its line from the
-// L2, and one word serialises its atomics (~11 ns each), so counters are sharded.
+// Per-launch device words of the intersect stage (uint32, reset by k_slot_init
+// or k_stage_move): [6..13] hand-over queue lengths (k_intersect / k_rootwalk ->
+// k_spill level 0 -> level 1 ...), from word 32 the root-item shard counters
+// (k_roots*), each on a 128-byte line of its own: a device-scope atomic evicts its
+// line from the L2, and one word serialises its atomics (~11 ns each).
 #define LPC_MISC_SPILL 6                  // [6 + l]: items queued for hand-over level l (l < 8)
-#define LPC_Q_CSHARDS 8                   // root-item shards (k_roots block b -> b % 8, or packet-range eighths)
-#define LPC_Q_DSHARDS 32                  // hand-over queue shards (k_trav block b -> b % 32)
-#define LPC_Q_NINIT(c) (32 * (1 + (c)))   // root items k_roots wrote into shard c
-#define LPC_Q_CHEAD(c) (32 * (9 + (c)))   // claim head of root shard c
-// Hand-over shard d: a 64-bit word TP = slots reserved (low half) | items
-// handed over and not finished (high half), so one returning atomic reserves
-// slots and counts them before they are published; tickets taken by waiting
-// waves; and, on a line of its own, the shard's waves still in the root phase.
-#define LPC_Q_TP(d) (32 * (17 + 2 * (d)))
-#define LPC_Q_DHEAD(d) (32 * (17 + 2 * (d)) + 2)
-#define LPC_Q_RBUSY(d) (32 * (18 + 2 * (d)))
-#define LPC_MISC_WORDS (32 * (17 + 2 * LPC_Q_DSHARDS))
+#define LPC_Q_CSHARDS 8                   // root-item shards (k_roots* block b -> b % 8)
+#define LPC_Q_NINIT(c) (32 * (1 + (c)))   // root items k_roots* wrote into shard c
+#define LPC_MISC_WORDS (32 * (1 + LPC_Q_CSHARDS))
 
-// Work queue of the intersect stage (k_roots -> k_trav).  An item is one packet
-// (64 rays of the coherence order) against one subtree of a mesh run, packed in
-// 64 bits: packet (24 bits) | node (28 bits) | slot (12 bits).  k_roots writes the
-// (packet, piece root) pairs whose root test some ray passes (the test
-// k_intersect's waves start with); k_trav's waves claim them in batches and walk
-// them, and while waves of their shard wait for work they hand the bottom of
-// their stack over through the shard's queue.  A queue slot holds LPC_QEMPTY
-// until an item is published into it (8-byte agent-scope atomic store: data and
-// flag in one granule); its consumer writes LPC_QEMPTY back, so the queue is
-// empty again between launches.
-#define LPC_QEMPTY 0xffffffffffffffffull
+// Root items of the intersect stage (k_roots* -> k_rootwalk).  An item is one
+// packet (64 rays of the coherence order) against one subtree of a mesh run,
+// packed in 64 bits: packet (24 bits) | node (28 bits) | slot (12 bits).  k_roots*
+// write the (packet, piece root) pairs whose root test some ray passes (the test
+// k_intersect's waves start with); k_rootwalk walks them grid-stride.
 __host__ __device__ inline uint64_t q_item(uint32_t w, uint32_t node, uint32_t slot)
 {
     return ((uint64_t)w << 40) | ((uint64_t)node << 12) | (uint64_t)slot;
@@ -82,31 +66,13 @@ __host__ __device__ inline uint32_t q_slot(uint64_t it) { return (uint32_t)it & 
 
 struct QueueArgs {
     uint64_t *roots;                  // [LPC_Q_CSHARDS][rcap] root items
-    uint64_t *dq;                     // [LPC_Q_DSHARDS][dcap] hand-over slots (LPC_QEMPTY when free)
-    uint32_t *ctl;                    // misc words (LPC_Q_*)
-    uint32_t *err;                    // set when a wave gives up waiting (a bug: never expected)
-    uint32_t rcap, dcap;
-    uint32_t spin_max;                // polls before a waiting wave gives up
-    int32_t batch;                    // root items per claim
-    int32_t hunger;                   // hand work over to waiting waves (0: never, A/B only)
-    int32_t dshard;                   // set per wave by k_trav (-1: no hand-over)
-    uint32_t *irec;                   // per-item records (profiling, lpc_prof_enable(h, 5)) or NULL
-    uint32_t irec_cap;
-    // XCD-local walk (LPC_XCD_WALK): the root shards are contiguous eighths of the
-    // packet range (k_roots*), and k_rootwalk's waves on XCD x (blocks b % 8 == x,
-    // the hardware's round-robin dispatch) walk the x-th eighth of the item list,
-    // so each XCD's L2 holds the scene records of one eighth of the directions.
-    int32_t xcd;
-    int64_t npk;                      // packets of the launch (range shards)
+    uint32_t *ctl;                    // misc words (LPC_Q_NINIT)
+    uint32_t *err;                    // DevAcc::qerr: set if a shard overflows rcap (never expected; the
+                                      //   host then reports the launch as incomplete instead of losing hits)
+    uint32_t rcap;
 };
-// root shard of a k_roots* block whose first packet is w0
-__host__ __device__ inline int q_shard(const QueueArgs &Q, int64_t w0, uint32_t block)
-{
-    if (!Q.xcd) return (int)(block % LPC_Q_CSHARDS);
-    const int64_t c = (w0 * LPC_Q_CSHARDS) / (Q.npk > 0 ? Q.npk : 1);
-    return (int)(c < LPC_Q_CSHARDS - 1 ? c : LPC_Q_CSHARDS - 1);
-}
-#define LPC_Q_IREC_N 16                   // misc word: item records written this launch
+// root shard of a k_roots* block
+__host__ __device__ inline int q_shard(uint32_t block) { return (int)(block % LPC_Q_CSHARDS); }
 
 // Work hand-over: a k_intersect wave that has visited `budget` nodes with two or
 // more subtrees still on its stack queues each of them as one item; k_spill
@@ -121,13 +87,6 @@ struct SpillArgs {
     uint32_t cap;
     int budget;                       // cost before hand-over (0: never), in node visits
     int pair_shift;                   // exact pairs per node visit = 1 << pair_shift (31: not counted)
-};
-
-// A fan group met by a k_intersect wave (packet, piece): group id and the rays
-// that passed the group's test; k_groups processes them.
-struct GItem {
-    int32_t g, pad;
-    uint64_t m;
 };
 
 struct RaysIn {                       // a ray population (SoA)
@@ -160,10 +119,6 @@ struct ShadeArgs {
     const float *ior, *refl, *diss, *verts;
     float max_ray_len, ior_env;
     ShadeOutPtrs o;
-    // counts first (LPC_SHADE_CFIRST, traced iterations only, whose slots start in
-    // the uniform clean state): a slot's key is read only when its count is not 0
-    // (a count of 0 means the key is still slot_key(max_ray_len, -1))
-    int32_t cfirst;
 };
 
 #define LPC_MP_MAX 4                      // measure meshes whose power the traced path sums per tile
@@ -173,7 +128,7 @@ struct DevAcc {                       // device-side counters of one iteration
     unsigned long long nM_iter;       // measured this iteration
     double pow_next;                  // float64 sum of kept children power
     unsigned int dmax2_bits;          // max |dir|^2 of kept children (float bits)
-    unsigned int qerr;                // k_trav gave up waiting on its work queue (QueueArgs::err)
+    unsigned int qerr;                // a consistency check failed on the device (QueueArgs::err)
     unsigned int seq;                 // host copy only: iteration number, written last (k_scan)
     unsigned int pad;
     double mpow[LPC_MP_MAX];          // traced path: measured power of the trace so far per measure mesh
@@ -199,7 +154,6 @@ struct CompactArgs {
     double *blk_pow;                  // [nb]
     DevAcc *acc;
     RaysOut nR, nT;                   // next population: reflected block, refracted staging
-    int32_t *childR, *childT;         // order chaining: each parent's children's positions (or NULL)
     int direct_t;                     // single chunk: refracted children go straight after the
                                       // reflected block (offset acc->nR), no staging / k_append
     float *mx, *my, *mz, *mp;         // measured record
@@ -255,21 +209,6 @@ struct MoveArgs {
     int64_t ngroups;
     unsigned long long *gsum_next;    // the next launch's group counts: its first gdirty_next (left by the
     int64_t gdirty_next;              //   launch before this one) zeroed here
-};
-
-// Order chaining (k_ocount / k_oscan / k_oscatter): the next population's
-// coherence order = the kept children in their parents' traced order
-// ([reflected ; refracted]), with the rays copied into that order.
-struct OrderArgs {
-    int64_t n, nb;                    // parents, 1024-parent tiles
-    const int32_t *perm;              // traced order of the parents (position -> index)
-    const int32_t *childR, *childT;   // parent index -> child position (-1 none)
-    ShadeOutPtrs o;                   // parents' shade outputs (child rays)
-    int32_t *blk;                     // [2][nb] counts, then offsets
-    long long *totR;                  // reflected children total (device)
-    const DevAcc *acc;                // n_next = acc->nR + acc->nT
-    int32_t *perm_next;               // [n_next]
-    float *rs_next;                   // [6][n_next]
 };
 
 struct PostprocAosArgs {

@@ -1,15 +1,19 @@
 // lpc_kernels.hip -- gfx950 kernels of the LightPyCL per-bounce path.
 //
 //   k_packet         per-wave bound (origin ball + direction cone) of 64 or 128 rays.
-//   k_intersect      the hot loop (replaces __kernel intersect, .cl:243-289):
-//                    (packet, piece) waves walk a piece's sphere hierarchy for
-//                    64 rays at once, per-ray conservative tests, exact
-//                    Moller-Trumbore only for candidates -> per-slot nearest hit
-//                    (64-bit atomicMin) and hit count; fan groups met on the
-//                    way are deferred to k_groups.
-//   k_groups         fan groups (thin triangles around revolve poles) lane-
-//                    parallel per packet, exact tests one ray per lane.
-//   k_gather         rays into coherence order (after k_raykey + radix sort).
+//   k_roots*, k_rootwalk, k_spill
+//                    the hot loop (replaces __kernel intersect, .cl:243-289):
+//                    (packet, piece) items whose root test passes, walked one
+//                    wave each through the piece's sphere hierarchy for 64 rays
+//                    at once, per-ray conservative tests, exact Moller-Trumbore
+//                    only for candidates -> per-slot nearest hit (64-bit
+//                    atomicMin) and hit count; heavy items hand subtrees over
+//                    to k_spill levels.  k_intersect: the same walk, one wave
+//                    per (packet, piece) (alternative launch, LPC_QUEUE=0).
+//   k_packet, k_slivers
+//                    degenerate "sliver" triangles by a line filter.
+//   k_raykey, k_gather_aos
+//                    rays into coherence order (key + rocPRIM radix sort).
 //   k_slot_init/k_slot_export
 //                    per-mesh scratch slots (.cl:260-288): pieces flush their
 //                    nearest hit with 64-bit atomicMin (slot_key) and counts
@@ -46,9 +50,8 @@ __constant__ int lpc_dbg = 0;
 // sort + k_gather); every kernel flushes its per-ray nearest hit and count into
 // the per-mesh slots with order-independent atomics (slot_flush), so the kernels
 // and their pieces may run in any order:
-//   k_intersect  a mesh run's sphere hierarchy (filter_test), 64-ray packets;
-//   k_groups     the fan groups the traversal met;
-//   k_packet     per-wave bound of 64 / 128 rays (origin ball + direction cone);
+//   k_rootwalk   a mesh run's sphere hierarchy (filter_test), 64-ray packets;
+//   k_packet     per-wave bound of 128 rays (origin ball + direction cone);
 //   k_slivers    the runs' slivers: lane-parallel packet_sliver_test, then the
 //                per-ray line filter.
 // Every filter level is implied by the one below it and the lowest one by the
@@ -190,26 +193,6 @@ static __device__ __forceinline__ int select_bit(uint64_t m, int k)
     return pos;
 }
 
-// Publish one item per lane < k into the wave's hand-over shard (k_trav) and
-// return how many fit (lanes [0, fit) were published).  One returning 64-bit
-// atomic reserves the slots and counts the items as pending before any of them
-// is visible; each item is one 8-byte agent-scope store (data = flag).
-static __device__ __forceinline__ int q_publish(const QueueArgs &Q, int k, uint64_t item)
-{
-    const int lane = threadIdx.x & 63;
-    unsigned long long *tp = (unsigned long long *)(Q.ctl + LPC_Q_TP(Q.dshard));
-    unsigned long long old = 0;
-    if (lane == 0) old = atomicAdd(tp, ((unsigned long long)k << 32) | (unsigned long long)k);
-    const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)old);
-    const int fit = base >= Q.dcap ? 0 : (int)min((uint32_t)k, Q.dcap - base);
-    if (fit < k && lane == 0)     // full: the reserved slots beyond it stay empty, uncount them
-        atomicAdd(tp, (unsigned long long)(-(long long)((unsigned long long)(k - fit) << 32)));
-    if (lane < fit)
-        __hip_atomic_store(Q.dq + (size_t)Q.dshard * Q.dcap + base + (uint32_t)lane, item, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    return fit;
-}
-
 // LDS of one wave's traversal.
 struct WaveLds {
     int32_t stack[LPC_STACK];
@@ -226,15 +209,13 @@ struct WaveLds {
 // rays (filter form d <= 0, see filter_record; node data wave-uniform through
 // the scalar cache); a child node is pushed when any ray passes it, a child
 // triangle's (index, lane mask) is queued for the exact test.
-// QH: the persistent queue's hand-over to waiting waves (k_trav only); PROF:
-// the profiling counters / records and the LPC_DBG timing switches (compiled
-// out of the default launches: fewer live registers in the hot loop).
-template <int W, bool QH = false, bool PROF = true, class RL = RayPair, bool HALF = false>
+// PROF: the profiling counters / records and the LPC_DBG timing switches
+// (compiled out of the default launches: fewer live registers in the hot loop).
+template <int W, bool PROF = true, class RL = RayPair, bool HALF = false>
 static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                                                    int64_t n, const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
-                                                   const ExactRec *__restrict__ xrec, GItem *__restrict__ gitems,
-                                                   int32_t *__restrict__ gcount, int gmax, int64_t gslot,
+                                                   const ExactRec *__restrict__ xrec,
                                                    const Piece &P, int64_t w, int piece_id, float eps,
                                                    float max_ray_len,
                                                    unsigned long long *__restrict__ skey,
@@ -242,10 +223,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                                                    unsigned long long *__restrict__ stats,
                                                    uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0,
                                                    SpillArgs SP = SpillArgs{nullptr, nullptr, 0u, 0, 31},
-                                                   int32_t start = -1,
-                                                   const QueueArgs &Q = QueueArgs{nullptr, nullptr, nullptr, nullptr,
-                                                                                  0u, 0u, 0u, 1, 0, -1,
-                                                                                  nullptr, 0u})
+                                                   int32_t start = -1)
 {
     const int lane = threadIdx.x & 63;
     const int64_t s = w * 64 + lane;
@@ -256,10 +234,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
     const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
     // start >= 0: a k_spill item (subtree root `start`, its parent passed)
     if (start < 0 &&
-        !(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f))) {
-        if (gcount && lane == 0) gcount[gslot] = 0;
+        !(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f)))
         return;
-    }
     L.ray[0][lane] = O.x; L.ray[1][lane] = O.y; L.ray[2][lane] = O.z;
     L.ray[3][lane] = D.x; L.ray[4][lane] = D.y; L.ray[5][lane] = D.z;
     const unsigned long long key0 = slot_key(max_ray_len, -1);
@@ -312,9 +288,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
         }
         nq = 0;
     };
-    int ngr = 0;                                   // fan groups deferred to k_groups
     int budget = SP.budget;
-    uint32_t q_head = 0, q_tail = 0;               // work queue: last read of the shard's counters
     L.stack[top++] = start >= 0 ? start : P.root;
     while (top > 0) {
         // work hand-over: after `budget` nodes the subtrees left on the stack go
@@ -337,15 +311,6 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
             // queue full: void the part of the range inside it, carry on here
             if (lane < top && base + (uint32_t)lane < SP.cap) SP.items[base + lane].node = -1;
             budget = 0;
-        }
-        // work queue (k_trav): every 4th node the shard's waiting waves (tickets
-        // taken beyond the slots reserved) as read 4 nodes ago are acted on, and
-        // a new read is issued (its latency, ~1-2 us, overlaps the next nodes)
-        int waiting = 0;
-        if (QH && Q.hunger && Q.dshard >= 0 && (n_nodes & 3u) == 0u) {
-            waiting = (int)__builtin_amdgcn_readfirstlane((int)(q_head - q_tail));
-            q_tail = __hip_atomic_load(Q.ctl + LPC_Q_TP(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            q_head = __hip_atomic_load(Q.ctl + LPC_Q_DHEAD(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
         const NodeW<W> N = nodes[node];
@@ -376,38 +341,13 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
 #pragma unroll
             for (int k = 0; k < W; ++k)
                 if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
-        } else {                                   // leaf: triangles -> queue, fan groups -> k_groups
+        } else {                                   // leaf: triangles ~ref -> exact-test queue
 #pragma unroll
             for (int k = 0; k < W; ++k) {
                 const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
                 if (!m) continue;
-                const int32_t ref = N.ref[k];
-                if (ref >= LPC_GROUP_REF) {
-                    if (lane == 0) { L.qidx[nq] = ~ref; L.qmask[nq] = m; }
-                    if (++nq == 64) drain();
-                } else {
-                    // the host sizes gmax to the piece's group count: never full
-                    if (lane == 0 && ngr < gmax) {
-                        GItem gi;
-                        gi.g = LPC_GROUP_REF - 1 - ref; gi.pad = 0; gi.m = m;
-                        gitems[gslot * gmax + ngr] = gi;
-                    }
-                    ++ngr;
-                }
-            }
-        }
-        // hand the bottom of the stack (the largest subtrees) to waiting waves,
-        // at most one entry per waiting wave; keep the top entry
-        if (QH && waiting > 0 && top >= 2) {
-            const int k = min(min(top - 1, waiting), 63);
-            const int32_t ent = lane < k ? L.stack[lane] : 0;
-            const int fit = q_publish(Q, k, q_item((uint32_t)w, (uint32_t)ent, (uint32_t)P.slot));
-            if (fit > 0) {
-                const int32_t keep = lane + fit < top ? L.stack[lane + fit] : 0;
-                __builtin_amdgcn_wave_barrier();
-                if (lane + fit < top) L.stack[lane] = keep;
-                __builtin_amdgcn_wave_barrier();
-                top -= fit;
+                if (lane == 0) { L.qidx[nq] = ~N.ref[k]; L.qmask[nq] = m; }
+                if (++nq == 64) drain();
             }
         }
     }
@@ -433,7 +373,6 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
             if (piece_id < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + piece_id], (unsigned long long)dt);
         }
     }
-    if (gcount && lane == 0) gcount[gslot] = ngr;
     if (PROF && wrec) {                        // per-wave record (diagnostic, no contention)
         for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
         if (lane == 0) {
@@ -452,32 +391,22 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
 
 // k_intersect: grid = (ceil(n/256), pieces), block = 4 waves, one (packet,
 // piece) per wave.
-template <int W, int MINB>
-__global__ __launch_bounds__(256, MINB) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
+template <int W>
+__global__ __launch_bounds__(256, 6) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                    const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
                                                    const ExactRec *__restrict__ xrec,
-                                                   GItem *__restrict__ gitems, int32_t *__restrict__ gcount,
-                                                   int gmax, const Piece *__restrict__ pieces, float eps,
+                                                   const Piece *__restrict__ pieces, float eps,
                                                    float max_ray_len,
                                                    unsigned long long *__restrict__ skey,
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
                                                    uint32_t *__restrict__ wrec, SpillArgs SP, int pgroup,
-                                                   int npieces, int xcd_rows)
+                                                   int npieces)
 {
     __shared__ WaveLds lds[4];
     const int wv = threadIdx.x >> 6;
-    unsigned bx = blockIdx.x, by = blockIdx.y;
-    if (xcd_rows > 0) {
-        // XCD-aware order: blocks are dealt to the 8 XCDs round-robin in launch
-        // order, so XCD k gets rows k, k + 8, ... (grid.y padded to a multiple
-        // of 8; xcd_rows = real rows): each XCD's L2 holds only its pieces' records
-        const unsigned L = blockIdx.y * gridDim.x + blockIdx.x, j = L >> 3;
-        by = (j / gridDim.x) * 8u + (L & 7u);
-        bx = j % gridDim.x;
-        if ((int)by >= xcd_rows) return;
-    }
+    const unsigned bx = blockIdx.x, by = blockIdx.y;
     const int64_t w = (int64_t)bx * 4 + wv;
     if (w * 64 >= n) return;                       // whole wave past the end
     // grid.y = ceil(npieces / pgroup): the wave takes pgroup pieces in turn
@@ -488,79 +417,35 @@ __global__ __launch_bounds__(256, MINB) void k_intersect(RaysIn R, const float *
     for (int p = p0; p < p1; ++p) {
         const Piece P = pieces[p];
         const int64_t slot = (int64_t)p * ((n + 63) / 64) + w;
-        trav_packet<W>(lds[wv], RayPair{R, rs, n}, n, perm, nodes, xrec, gitems, gcount, gmax, slot, P, w, p, eps,
-                       max_ray_len,
-                    skey, scnt, stats, wrec, slot, SP);
+        trav_packet<W>(lds[wv], RayPair{R, rs, n}, n, perm, nodes, xrec, P, w, p, eps, max_ray_len,
+                       skey, scnt, stats, wrec, slot, SP);
     }
-}
-
-// k_lane: one ray per lane (incoherent populations: a 64-ray packet's union of
-// visited nodes is many times one ray's), grid = (ceil(n/256), pieces).  The lane
-// walks its piece's threaded entry list (LaneEntry, depth-first with skip links,
-// no stack): a node entry that its ray passes is entered (next entry), else
-// skipped; a triangle entry that passes gets the exact test at once.  Same tests,
-// same exact-test superset as k_intersect, same order-independent flush.
-__global__ __launch_bounds__(256) void k_lane(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                              const int32_t *__restrict__ perm, const LaneEntry *__restrict__ E,
-                                              const ExactRec *__restrict__ xrec, const Piece *__restrict__ pieces,
-                                              float eps, float max_ray_len, unsigned long long *__restrict__ skey,
-                                              int32_t *__restrict__ scnt)
-{
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const Piece P = pieces[blockIdx.y];
-    f3 O, D;
-    load_ray(R, rs, n, s, O, D);
-    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
-    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
-    float tmin = max_ray_len;
-    int32_t imin = -1, cnt = 0;
-    int32_t i = P.s_lo;
-    const int32_t end = P.s_hi;
-    while (i < end) {
-        const LaneEntry e = E[i];
-        const bool pass = filter_test(e.cx, e.cy, e.cz, e.negB, e.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f;
-        if (e.tri >= 0) {
-            if (pass) {
-                const ExactRec x = xrec[e.tri];
-                mt_accumulate(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z),
-                              e.tri, eps, tmin, imin, cnt);
-            }
-            ++i;
-        } else {
-            i = pass ? i + 1 : e.skip;
-        }
-    }
-    slot_flush(skey, scnt, (int64_t)P.slot * n, perm ? perm[s] : s, tmin, imin, cnt);
 }
 
 // k_spill: the subtrees handed over by the previous level (queue `in`), one item
 // per wave, grid-stride over the queue (its length is read on the device).  An
 // item that again exceeds the budget hands its remaining subtrees to the next
-// level's queue (`out`; budget 0 on the last level).  Only used without fan
-// groups (the host checks).
-// WPB waves per block (1: a wave's slot frees when its items end, see k_rootwalk).
-template <int W, int WPB, bool PROF = false, int MINW = 6, bool HALF = false>
-__global__ __launch_bounds__(64 * WPB, MINW) void k_spill(RayBase ray, int64_t n,
+// level's queue (`out`; budget 0 on the last level).  One wave per block (a
+// wave's slot frees when its items end, see k_rootwalk).
+template <int W, bool PROF = false, bool HALF = false>
+__global__ __launch_bounds__(64, 6) void k_spill(RayBase ray, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                unsigned long long *__restrict__ stats, SpillArgs SP,
                                                SpillArgs out)
 {
-    __shared__ WaveLds lds[WPB];
-    const int wv = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
+    __shared__ WaveLds lds;
     const uint32_t total = min(*SP.ctr, SP.cap);
-    const uint32_t stride = gridDim.x * (uint32_t)WPB;
-    for (uint32_t it = blockIdx.x * (uint32_t)WPB + (uint32_t)wv; it < total; it += stride) {
+    const uint32_t stride = gridDim.x;
+    for (uint32_t it = blockIdx.x; it < total; it += stride) {
         const SpillItem I = SP.items[it];
         if (I.node < 0) continue;
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
-        trav_packet<W, false, PROF, RayBase, HALF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, I.w,
-                                                   I.piece, eps,
-                    max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
+        trav_packet<W, PROF, RayBase, HALF>(lds, ray, n, perm, nodes, xrec, P, I.w, I.piece, eps,
+                                            max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
     }
 }
 
@@ -579,7 +464,7 @@ __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict
     __shared__ uint32_t s_cnt[4];
     __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = q_shard(Q, (int64_t)blockIdx.x * 4, blockIdx.x);
+    const int c = q_shard(blockIdx.x);
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     const bool live = w * 64 < n;
     {
@@ -617,6 +502,7 @@ __global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict
         if (pass) {
             const uint32_t pos = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
             if (pos < Q.rcap) Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)P.root, (uint32_t)P.slot);
+            else atomicOr(Q.err, 2u);             // would be lost: the host reports the launch
         }
         __syncthreads();                         // s_cnt / s_base reused by the next chunk
     }
@@ -632,7 +518,7 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     __shared__ uint32_t s_cnt[4];
     __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = q_shard(Q, (int64_t)blockIdx.x * 4, blockIdx.x);
+    const int c = q_shard(blockIdx.x);
     const int64_t w = (int64_t)blockIdx.x * 4 + wv;
     const bool live = w * 64 < n;
     const int64_t s = w * 64 + lane;
@@ -663,6 +549,7 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     if ((m >> lane) & 1ull) {
         const uint32_t pos = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
         if (pos < Q.rcap) Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)Pl.root, (uint32_t)Pl.slot);
+        else atomicOr(Q.err, 2u);                 // would be lost: the host reports the launch
     }
 }
 
@@ -682,7 +569,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = q_shard(Q, (int64_t)blockIdx.x * pb, blockIdx.x);
+    const int c = q_shard(blockIdx.x);
     const int ntask = S * pb;
     for (int t = wv; t < ntask; t += 4) {
         const int64_t w = (int64_t)blockIdx.x * pb + t / S;
@@ -723,6 +610,8 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
         const uint32_t pos = base + s_off[t] + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
         if (pos < Q.rcap)
             Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)pieces[p].root, (uint32_t)pieces[p].slot);
+        else
+            atomicOr(Q.err, 2u);                  // would be lost: the host reports the launch
     }
 }
 
@@ -730,11 +619,11 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
 // time -- k_intersect's (packet, piece) waves without the waves whose root test
 // fails.  A wave that exceeds the hand-over budget queues its remaining
 // subtrees for k_spill (`out`), as k_intersect does.
-// WPB waves per block: 1 by default -- a block's slots free as soon as its one
-// item ends, where a 4-wave block holds its LDS until its slowest item ends
-// (per-item records: ~2 800 of 6 144 wave slots walking on average with 4).
-template <int W, int WPB, bool PROF = false, int MINW = 6, bool HALF = false>
-__global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_t n,
+// One wave per block: a block's slots free as soon as its item ends, where a
+// 4-wave block holds its LDS until its slowest item ends (round 2 per-item
+// records: ~2 800 of 6 144 wave slots walking on average with 4).
+template <int W, bool PROF = false, bool HALF = false>
+__global__ __launch_bounds__(64, 6) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -742,24 +631,13 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_
                                                      unsigned long long *__restrict__ stats, QueueArgs Q,
                                                      SpillArgs out)
 {
-    __shared__ WaveLds lds[WPB];
-    const int wv = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
+    __shared__ WaveLds lds;
     uint32_t pre[LPC_Q_CSHARDS + 1];
     pre[0] = 0;
 #pragma unroll
     for (int c = 0; c < LPC_Q_CSHARDS; ++c) pre[c + 1] = pre[c] + min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-    uint32_t stride = gridDim.x * (uint32_t)WPB, i0 = blockIdx.x * (uint32_t)WPB + (uint32_t)wv,
-             iend = pre[LPC_Q_CSHARDS];
-    if (Q.xcd && (gridDim.x & 7u) == 0u) {
-        // XCD-local: block b runs on XCD b % 8 (round-robin dispatch) and walks the
-        // (b % 8)-th eighth of the items (range shards: an eighth of the packets);
-        // any placement still visits every item exactly once
-        const uint32_t x = blockIdx.x & 7u, T = iend;
-        i0 = (uint32_t)(((uint64_t)T * x) / 8u) + (blockIdx.x >> 3) * (uint32_t)WPB + (uint32_t)wv;
-        iend = (uint32_t)(((uint64_t)T * (x + 1u)) / 8u);
-        stride = (gridDim.x >> 3) * (uint32_t)WPB;
-    }
-    for (uint32_t i = i0; i < iend; i += stride) {
+    const uint32_t stride = gridDim.x, iend = pre[LPC_Q_CSHARDS];
+    for (uint32_t i = blockIdx.x; i < iend; i += stride) {
         int c = 0;
         while (i >= pre[c + 1]) ++c;
         const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - pre[c])];
@@ -767,214 +645,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_rootwalk(RayBase ray, int64_
         memset(&P, 0, sizeof(P));
         P.root = (int32_t)q_node(it);
         P.slot = (int32_t)q_slot(it);
-        // profiling (lpc_prof_enable(h, 5)): an 8-word record per item, by item
-        // index (no atomics): walk ticks, nodes, exact tests, slot, start time, 0, HW_ID, XCC_ID
-        uint32_t *rec = (PROF && Q.irec && i < Q.irec_cap) ? Q.irec + 8 * (size_t)i : nullptr;
-        if (rec && (threadIdx.x & 63) == 0) {
-            rec[4] = (uint32_t)wall_clock64(); rec[5] = rec[4];
-            rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
-            rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (1u << 8);
-        }
-        trav_packet<W, false, PROF, RayBase, HALF>(lds[wv], ray, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P,
-                                    (int64_t)q_w(it), P.slot, eps, max_ray_len, skey, scnt, stats, rec, 0, out, P.root);
+        trav_packet<W, PROF, RayBase, HALF>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot, eps,
+                                            max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
     }
-}
-
-// k_trav: persistent traversal of the work queue, 4 waves per block, every wave
-// on its own.  Root phase: claim `batch` root items at a time, own root shard
-// first, then the others; before each further item of a batch, if waves of the
-// hand-over shard wait, hand the rest of the batch over instead.  Hand-over
-// phase: take a ticket on the shard's queue, wait for its slot, walk the item;
-// leave when no wave of the shard is in its root phase and no handed-over item
-// is unfinished (seen twice in a row), or give up after spin_max polls (sets
-// *err; the host reports it and re-empties the queue).  trav_packet hands the
-// bottom of its stack over while waves of its shard wait.
-template <int W, int WPB>
-__global__ __launch_bounds__(64 * WPB, 6) void k_trav(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                 const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
-                                                 const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
-                                                 unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
-                                                 unsigned long long *__restrict__ stats, QueueArgs Q)
-{
-    __shared__ WaveLds lds[WPB];
-    const int wv = WPB == 1 ? 0 : (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    Q.dshard = (int32_t)(blockIdx.x % LPC_Q_DSHARDS);
-    uint32_t *rbusy = Q.ctl + LPC_Q_RBUSY(Q.dshard);
-    unsigned long long *tp = (unsigned long long *)(Q.ctl + LPC_Q_TP(Q.dshard));
-    auto walk = [&](uint64_t it, uint64_t t_claim, uint32_t phase) {
-        Piece P;
-        memset(&P, 0, sizeof(P));
-        P.root = (int32_t)q_node(it);
-        P.slot = (int32_t)q_slot(it);
-        // profiling: one 8-word record per item (trav_packet writes words 0-3:
-        // walk ticks, nodes, exact tests, slot; then claim and walk start times,
-        // the wave's HW_ID and XCC_ID | phase << 8)
-        uint32_t *rec = nullptr;
-        if (Q.irec) {
-            uint32_t ix = 0;
-            if (lane == 0) ix = atomicAdd(Q.ctl + LPC_Q_IREC_N, 1u);
-            ix = (uint32_t)__builtin_amdgcn_readfirstlane((int)ix);
-            if (ix < Q.irec_cap) {
-                rec = Q.irec + 8 * (size_t)ix;
-                if (lane == 0) {
-                    rec[4] = (uint32_t)t_claim;
-                    rec[5] = (uint32_t)wall_clock64();
-                    rec[6] = (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
-                    rec[7] = (uint32_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) | (phase << 8);
-                }
-            }
-        }
-        trav_packet<W, true, true>(lds[wv], RayPair{R, rs, n}, n, perm, nodes, xrec, nullptr, nullptr, 0, 0, P, (int64_t)q_w(it), P.slot,
-                       eps, max_ray_len, skey, scnt, stats, rec, 0, SpillArgs{nullptr, nullptr, 0u, 0, 31},
-                       P.root, Q);
-    };
-    // root phase (the increment is performed before the first claim)
-    uint32_t r0 = 0;
-    if (lane == 0) r0 = atomicAdd(rbusy, 1u);
-    asm volatile("" ::"v"(r0));                 // wait for the returned value
-    uint32_t exhausted = 0;                     // root shards found empty
-    int c = (int)(blockIdx.x % LPC_Q_CSHARDS);
-    bool root_phase = true;
-    uint64_t mine = 0;                          // claimed batch, one item per lane < cnt
-    int cnt = 0, next = 0;
-    uint32_t qt = 0, qh = 0;                    // the shard's counters, read one item ahead
-    uint32_t spins = 0;
-    // one walk site (two would double the code in the instruction cache)
-    for (;;) {
-        uint64_t it = LPC_QEMPTY, t_claim = 0;
-        uint32_t phase = 1;
-        if (root_phase) {
-            while (next >= cnt && exhausted != (1u << LPC_Q_CSHARDS) - 1u) {
-                if ((exhausted >> c) & 1u) { c = (c + 1) % LPC_Q_CSHARDS; continue; }
-                const uint32_t nr = min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-                // look before claiming: every wave finding every shard empty by an
-                // atomic would serialise ~8 atomics per wave on 8 words at the end
-                const uint32_t seen =
-                    __hip_atomic_load(Q.ctl + LPC_Q_CHEAD(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane((int)(seen >= nr))) { exhausted |= 1u << c; continue; }
-                uint32_t t = 0;
-                if (lane == 0) t = atomicAdd(Q.ctl + LPC_Q_CHEAD(c), (uint32_t)Q.batch);
-                t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-                if (t >= nr) { exhausted |= 1u << c; continue; }
-                cnt = (int)min((uint32_t)Q.batch, nr - t);
-                next = 0;
-                mine = lane < cnt ? Q.roots[(size_t)c * Q.rcap + t + (uint32_t)lane] : 0ull;
-            }
-            if (next < cnt && next > 0) {
-                const int waiting = __builtin_amdgcn_readfirstlane((int)(qh - qt));
-                if (waiting > 0) {      // waves wait: hand the rest of the batch over
-                    const uint64_t rest = __shfl(mine, min(lane + next, 63), 64);
-                    next += q_publish(Q, cnt - next, rest);
-                }
-            }
-            if (next < cnt) {
-                it = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), next) << 32) |
-                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, next);
-                ++next;
-                if (next < cnt && Q.hunger) {
-                    qt = __hip_atomic_load(Q.ctl + LPC_Q_TP(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    qh = __hip_atomic_load(Q.ctl + LPC_Q_DHEAD(Q.dshard), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (Q.irec) t_claim = wall_clock64();
-            } else {
-                root_phase = false;
-                if (lane == 0) atomicSub(rbusy, 1u);    // after this wave's publishes (returning atomics)
-                continue;
-            }
-        } else {
-            // hand-over phase: a ticket on the shard's queue, then its slot
-            phase = 2;
-            uint32_t tk = 0;
-            if (lane == 0) tk = atomicAdd(Q.ctl + LPC_Q_DHEAD(Q.dshard), 1u);
-            tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
-            if (Q.irec) t_claim = wall_clock64();
-            uint64_t *slot = tk < Q.dcap ? Q.dq + (size_t)Q.dshard * Q.dcap + tk : nullptr;
-            int idle = 0;
-            for (uint32_t poll = 0;; ++poll) {
-                if (slot) {
-                    const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    it = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
-                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-                    if (it != LPC_QEMPTY) break;
-                }
-                if ((poll & 3u) == 3u) {
-                    // relaxed: an acquire would invalidate the CU's L1 under the
-                    // traversing waves; the exit needs the state seen twice, polls apart
-                    const uint32_t rb = __hip_atomic_load(rbusy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long v = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const bool done =
-                        __builtin_amdgcn_readfirstlane((int)(rb == 0u && (uint32_t)(v >> 32) == 0u)) != 0;
-                    idle = done ? idle + 1 : 0;
-                    if (idle >= 2) return;       // nothing left in this shard, nothing that could add to it
-                }
-                if (++spins > Q.spin_max) {
-                    if (lane == 0) atomicOr(Q.err, 1u);
-                    return;
-                }
-                __builtin_amdgcn_s_sleep(8);
-            }
-            if (lane == 0) __hip_atomic_store(slot, LPC_QEMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        walk(it, t_claim, phase);
-        // a handed-over item is uncounted when finished (after its own publishes, which returned)
-        if (phase == 2 && lane == 0) atomicAdd(tp, (unsigned long long)(-(long long)(1ull << 32)));
-    }
-}
-
-// k_groups: the fan groups k_intersect's wave (packet w, piece y) met, same
-// grid.  Per group: members' filter and exact records load lane-parallel, the
-// members are tested against the packet bound (packet_sphere_test), then each
-// candidate per ray (only the rays of the item's mask can hit a member: the
-// group's own test is node_record() of its members) and the exact test runs
-// one ray per lane from the broadcast record -- no gather, no queue.
-__global__ __launch_bounds__(256) void k_groups(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                const int32_t *__restrict__ perm,
-                                                const FiltRec *__restrict__ grec,
-                                                const ExactRec *__restrict__ gxrec,
-                                                const PacketRec *__restrict__ pk64,
-                                                const Piece *__restrict__ pieces,
-                                                const GItem *__restrict__ gitems,
-                                                const int32_t *__restrict__ gcount, int gmax, float eps,
-                                                float max_ray_len, unsigned long long *__restrict__ skey,
-                                                int32_t *__restrict__ scnt)
-{
-    const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t npk = (n + 63) / 64;
-    if (w >= npk) return;
-    const int64_t gslot = (int64_t)blockIdx.y * npk + w;
-    const int items = min(gcount[gslot], gmax);
-    if (items == 0) return;
-    const int64_t s = w * 64 + lane;
-    f3 O, D;
-    load_ray(R, rs, n, s < n ? s : n - 1, O, D);
-    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
-    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
-    const PacketRec Q = pk64[w];
-    float tmin = max_ray_len;
-    int32_t imin = -1, cnt = 0;
-    for (int it = 0; it < items; ++it) {
-        const GItem I = gitems[gslot * gmax + it];
-        const int64_t gi = (int64_t)I.g * LPC_GROUP_SIZE + lane;
-        const FiltRec f = grec[gi];
-        uint64_t cm = __builtin_amdgcn_ballot_w64(packet_sphere_test(Q, f.cx, f.cy, f.cz, f.negB, f.negA));
-        if (!cm) continue;
-        const ExactRec x = gxrec[gi];
-        while (cm) {
-            const int j = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            const float dj = filter_test(bcast(f.cx, j), bcast(f.cy, j), bcast(f.cz, j), bcast(f.negB, j),
-                                         bcast(f.negA, j), O.x, O.y, O.z, nx, ny, nz);
-            const uint64_t mm = __builtin_amdgcn_ballot_w64(dj <= 0.0f) & I.m;
-            if (!mm) continue;
-            const int32_t idx = bcasti(f.idx, j);
-            const f3 V0 = mk3(bcast(x.v0x, j), bcast(x.v0y, j), bcast(x.v0z, j));
-            const f3 E1 = mk3(bcast(x.e1x, j), bcast(x.e1y, j), bcast(x.e1z, j));
-            const f3 E2 = mk3(bcast(x.e2x, j), bcast(x.e2y, j), bcast(x.e2z, j));
-            if ((mm >> lane) & 1ull) mt_accumulate(O, D, V0, E1, E2, idx, eps, tmin, imin, cnt);
-        }
-    }
-    if (s < n) slot_flush(skey, scnt, (int64_t)pieces[blockIdx.y].slot * n, perm ? perm[s] : s, tmin, imin, cnt);
 }
 
 // k_slivers: the run's slivers (line filter) for packets of 128 rays (two per
@@ -1058,85 +731,6 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
     }
 }
 
-// k_slivers1: k_slivers for 64-ray packets (one ray per lane, PacketRec of
-// k_packet<1>): tighter packet bounds, fewer slivers pass per ray.
-__global__ __launch_bounds__(256) void k_slivers1(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                  const int32_t *__restrict__ perm,
-                                                  const PacketRec *__restrict__ pk,
-                                                  const SliverRec *__restrict__ srec,
-                                                  const Piece *__restrict__ pieces, float eps, float max_ray_len,
-                                                  unsigned long long *__restrict__ skey,
-                                                  int32_t *__restrict__ scnt,
-                                                  unsigned long long *__restrict__ stats, int ppw,
-                                                 float dmax)
-{
-    const int lane = threadIdx.x & 63;
-    const int64_t npk = (n + 63) / 64;
-    const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
-    if (w0 >= npk) return;
-    const int64_t w1 = min(w0 + (int64_t)ppw, npk);
-    const Piece P = pieces[blockIdx.y];
-    const int32_t j = P.s_lo + lane;
-    SliverRec S;
-    if (j < P.s_hi) S = srec[j];
-    else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
-    if (!(S.dmin <= dmax)) S.a = NAN;             // no ray of the launch can pass its DEN test
-    const int64_t o = (int64_t)P.slot * n;
-    uint32_t n_tests = 0, n_exact = 0;
-    for (int64_t w = w0; w < w1; ++w) {
-        const PacketRec Q = pk[w];
-        uint64_t m = __builtin_amdgcn_ballot_w64(packet_sliver_test(Q, S));
-        if (!m) continue;
-        const int64_t s0 = w * 64 + lane;
-        f3 O, D;
-        load_ray(R, rs, n, s0 < n ? s0 : n - 1, O, D);
-        const float dl = sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
-        float t0 = max_ray_len;
-        int32_t i0 = -1, c0 = 0;
-        while (m) {
-            const int k = __builtin_ctzll(m);
-            m &= m - 1;
-            const float v0x = bcast(S.v0x, k), v0y = bcast(S.v0y, k), v0z = bcast(S.v0z, k);
-            const float e2x = bcast(S.e2x, k), e2y = bcast(S.e2y, k), e2z = bcast(S.e2z, k);
-            const float sa = bcast(S.a, k), sbb = bcast(S.b, k);
-            const float tx = O.x - v0x, ty = O.y - v0y, tz = O.z - v0z;
-            const float cx = e2y * tz - e2z * ty, cy = e2z * tx - e2x * tz, cz = e2x * ty - e2y * tx;
-            const float x = D.x * cx + D.y * cy + D.z * cz;
-            const float tm = fmaxf(fmaxf(fabsf(tx), fabsf(ty)), fabsf(tz));
-            const float rhs = dl * (sa + sbb * tm);
-            ++n_tests;
-            const bool r0 = x * x - rhs * rhs <= 0.0f;
-            if (!any_lane(r0)) continue;
-            const int32_t idx = bcasti(S.idx, k);
-            const f3 V0 = mk3(v0x, v0y, v0z);
-            const f3 E1 = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
-            const f3 E2 = mk3(e2x, e2y, e2z);
-            if (r0) mt_accumulate(O, D, V0, E1, E2, idx, eps, t0, i0, c0);
-            n_exact += (uint32_t)r0;
-        }
-        if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
-    }
-    if (stats) {
-        for (int q = 32; q >= 1; q >>= 1) n_exact += __shfl_xor(n_exact, q, 64);
-        if (lane == 0) {
-            atomicAdd(&stats[1], (unsigned long long)n_tests);
-            atomicAdd(&stats[3], (unsigned long long)n_exact);
-        }
-    }
-}
-
-// Rays in coherence order, SoA [6][n] (ox oy oz dx dy dz), read coalesced by
-// every piece of k_intersect.
-__global__ __launch_bounds__(256) void k_gather(RaysIn R, int64_t n, const int32_t *__restrict__ perm,
-                                                float *__restrict__ rs)
-{
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const int64_t q = perm[s];
-    rs[s] = R.ox[q]; rs[n + s] = R.oy[q]; rs[2 * n + s] = R.oz[q];
-    rs[3 * n + s] = R.dx[q]; rs[4 * n + s] = R.dy[q]; rs[5 * n + s] = R.dz[q];
-}
-
 // k_gather from the 32-byte rows k_raykey wrote: one cache line per ray instead
 // of one per component (the permutation is random with respect to memory).
 // full: also the power and previous mesh (the rows' last two words, k_raykey),
@@ -1216,71 +810,14 @@ static __device__ __forceinline__ uint32_t spread3(uint32_t x)   // 5 bits -> ev
     return x;
 }
 
-// Origin box of the population (finite origins) as order-preserving uint
-// encodings in misc[0..5] (min xyz, max xyz; k_slot_init empties it).
-static __device__ __forceinline__ uint32_t ord_enc(float f)
-{
-    const uint32_t u = __builtin_bit_cast(uint32_t, f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-static __device__ __forceinline__ float ord_dec(uint32_t u)
-{
-    return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
-}
-
-__global__ __launch_bounds__(256) void k_bbox(RaysIn R, int64_t n, uint32_t *__restrict__ bb)
-{
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float o[3] = {R.ox[i], R.oy[i], R.oz[i]};
-        if (!(fabsf(o[0]) < INFINITY && fabsf(o[1]) < INFINITY && fabsf(o[2]) < INFINITY)) continue;
-        for (int k = 0; k < 3; ++k) { mn[k] = fminf(mn[k], o[k]); mx[k] = fmaxf(mx[k], o[k]); }
-    }
-    for (int k = 0; k < 3; ++k) { mn[k] = wave_red(mn[k], 0); mx[k] = wave_red(mx[k], 1); }
-    // block-level reduction, then one atomic per word per block (device atomics on
-    // one word serialise: the grid is kept small)
-    __shared__ float s_b[6][4];
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < 3; ++k) { s_b[k][wv] = mn[k]; s_b[3 + k][wv] = mx[k]; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < 3; ++k) {
-            mn[k] = fminf(fminf(s_b[k][0], s_b[k][1]), fminf(s_b[k][2], s_b[k][3]));
-            mx[k] = fmaxf(fmaxf(s_b[3 + k][0], s_b[3 + k][1]), fmaxf(s_b[3 + k][2], s_b[3 + k][3]));
-        }
-        if (mn[0] <= mx[0])
-            for (int k = 0; k < 3; ++k) { atomicMin(&bb[k], ord_enc(mn[k])); atomicMax(&bb[3 + k], ord_enc(mx[k])); }
-    }
-}
-
-// Key = [class 1 bit][origin cell 15 bits][direction 16 bits] (dir_major: the
-// direction bits above the origin cell's).  bb != NULL: the
-// origin grid spans the population's origin box (k_bbox), so secondary rays that
-// leave one small object still spread over the 32^3 cells (otherwise the scene
-// box bx0.., sx..).  class = (i >= split): the refracted block of a population
-// ([reflected ; refracted], k_append) sorts apart from the reflected one.
+// Key = [origin cell 15 bits][direction 16 bits] over the scene box (bx0.., sx..).
 static __device__ __forceinline__ uint32_t raykey_ray(const RaysIn &R, int64_t i, float bx0, float by0, float bz0,
-                                                      float sx, float sy, float sz, const uint32_t *__restrict__ bb,
-                                                      int64_t split, int dir_major, float4 *__restrict__ aos)
+                                                      float sx, float sy, float sz, float4 *__restrict__ aos)
 {
     if (aos) {          // the ray as one 32-byte row: k_gather_aos reads it with one line per ray
         aos[2 * i] = make_float4(R.ox[i], R.oy[i], R.oz[i], R.dx[i]);
         aos[2 * i + 1] = make_float4(R.dy[i], R.dz[i], R.pw ? R.pw[i] : 0.0f,
                                      R.pmid ? __int_as_float(R.pmid[i]) : 0.0f);
-    }
-    if (bb) {
-        const float lo[3] = {ord_dec(bb[0]), ord_dec(bb[1]), ord_dec(bb[2])};
-        const float hi[3] = {ord_dec(bb[3]), ord_dec(bb[4]), ord_dec(bb[5])};
-        float sc[3];
-        for (int k = 0; k < 3; ++k) {
-            const float ext = hi[k] - lo[k];
-            sc[k] = (ext > 0.0f && ext < INFINITY) ? 32.0f / ext : 0.0f;
-        }
-        bx0 = lo[0] <= hi[0] ? lo[0] : 0.0f;
-        by0 = lo[1] <= hi[1] ? lo[1] : 0.0f;
-        bz0 = lo[2] <= hi[2] ? lo[2] : 0.0f;
-        sx = sc[0]; sy = sc[1]; sz = sc[2];
     }
     const float dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
     const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
@@ -1297,121 +834,18 @@ static __device__ __forceinline__ uint32_t raykey_ray(const RaysIn &R, int64_t i
     const uint32_t oz = (uint32_t)fminf(fmaxf((R.oz[i] - bz0) * sz, 0.0f), 31.0f);
     const uint32_t okey = spread3(ox) | (spread3(oy) << 1) | (spread3(oz) << 2);
     const uint32_t dkey = spread2(du) | (spread2(dv) << 1);
-    return (i >= split ? 0x80000000u : 0u) | (dir_major ? (dkey << 15) | okey : (okey << 16) | dkey);
+    return (okey << 16) | dkey;
 }
 
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
-                                                float sx, float sy, float sz, const uint32_t *__restrict__ bb,
-                                                int64_t split, int dir_major, uint32_t *__restrict__ keys,
+                                                float sx, float sy, float sz, uint32_t *__restrict__ keys,
                                                 int32_t *__restrict__ vals, float4 *__restrict__ aos,
                                                 SlotInit SI)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (SI.skey || SI.misc || SI.acc) slot_init_ray(SI, n, i);     // k_slot_init folded in (one launch fewer)
     if (i >= n) return;
-    keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, bb, split, dir_major, aos);
-    vals[i] = (int32_t)i;
-}
-
-// Adaptive 16-bit coherence key (LPC_SORT=2): a 5-D Morton code, coarse to fine,
-// of the origin cell (scene box, 256 cells per axis) and the octahedral direction
-// (256 x 256), 40 bits; the key is its 16 most significant bits that vary over
-// the population (k_keymask), so a point source spends them all on direction and
-// a population spread over a small region on its own scale.  Sorted with a
-// 2-pass radix sort; any order is correct (results are order independent).
-static __device__ __forceinline__ uint64_t ray_morton5(float ox, float oy, float oz, float dx, float dy, float dz,
-                                                       float bx0, float by0, float bz0, float sx, float sy, float sz)
-{
-    const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
-    float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
-    if (dz < 0.0f) {
-        const float tx = (1.0f - fabsf(py)) * (px >= 0.0f ? 1.0f : -1.0f);
-        const float ty = (1.0f - fabsf(px)) * (py >= 0.0f ? 1.0f : -1.0f);
-        px = tx; py = ty;
-    }
-    uint32_t c[5];
-    c[0] = (uint32_t)fminf(fmaxf((ox - bx0) * sx, 0.0f), 255.0f);
-    c[1] = (uint32_t)fminf(fmaxf((oy - by0) * sy, 0.0f), 255.0f);
-    c[2] = (uint32_t)fminf(fmaxf((oz - bz0) * sz, 0.0f), 255.0f);
-    c[3] = (uint32_t)fminf(fmaxf((px * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
-    c[4] = (uint32_t)fminf(fmaxf((py * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
-    uint64_t k = 0;
-#pragma unroll
-    for (int b = 7; b >= 0; --b)
-#pragma unroll
-        for (int d = 0; d < 5; ++d) k = (k << 1) | (uint64_t)((c[d] >> b) & 1u);
-    return k;
-}
-
-// Key pass 1: the ray's 32-byte row (k_gather_aos) and the block's OR / AND of
-// the 40-bit codes (part[2 b], part[2 b + 1]).
-__global__ __launch_bounds__(256) void k_raykey16a(RaysIn R, int64_t n, float bx0, float by0, float bz0, float sx,
-                                                   float sy, float sz, float4 *__restrict__ aos,
-                                                   unsigned long long *__restrict__ part)
-{
-    __shared__ unsigned long long s_or[4], s_and[4];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long vo = 0ull, va = ~0ull;
-    if (i < n) {
-        const float ox = R.ox[i], oy = R.oy[i], oz = R.oz[i], dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
-        aos[2 * i] = make_float4(ox, oy, oz, dx);
-        aos[2 * i + 1] = make_float4(dy, dz, R.pw ? R.pw[i] : 0.0f, R.pmid ? __int_as_float(R.pmid[i]) : 0.0f);
-        vo = va = ray_morton5(ox, oy, oz, dx, dy, dz, bx0, by0, bz0, sx, sy, sz);
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-        vo |= __shfl_xor(vo, o, 64);
-        va &= __shfl_xor(va, o, 64);
-    }
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { s_or[wv] = vo; s_and[wv] = va; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        part[2 * blockIdx.x] = s_or[0] | s_or[1] | s_or[2] | s_or[3];
-        part[2 * blockIdx.x + 1] = s_and[0] & s_and[1] & s_and[2] & s_and[3];
-    }
-}
-
-// Key pass 2 (one block): the bits that vary over the population and the 16 most
-// significant of them (sel[0..15], -1 = unused).
-__global__ __launch_bounds__(1024) void k_keymask(const unsigned long long *__restrict__ part, int64_t nb,
-                                                  int32_t *__restrict__ sel)
-{
-    __shared__ unsigned long long s_or[16], s_and[16];
-    unsigned long long vo = 0ull, va = ~0ull;
-    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) { vo |= part[2 * b]; va &= part[2 * b + 1]; }
-    for (int o = 32; o >= 1; o >>= 1) {
-        vo |= __shfl_xor(vo, o, 64);
-        va &= __shfl_xor(va, o, 64);
-    }
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { s_or[wv] = vo; s_and[wv] = va; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long o = 0ull, a = ~0ull;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { o |= s_or[w]; a &= s_and[w]; }
-        const unsigned long long vary = o & ~a;
-        int j = 0;
-        for (int b = 39; b >= 0 && j < 16; --b)
-            if ((vary >> b) & 1ull) sel[j++] = b;
-        for (; j < 16; ++j) sel[j] = -1;
-    }
-}
-
-// Key pass 3: the 16-bit key of each ray (its code's selected bits).
-__global__ __launch_bounds__(256) void k_keypack(RaysIn R, int64_t n, float bx0, float by0, float bz0, float sx,
-                                                 float sy, float sz, const int32_t *__restrict__ sel,
-                                                 uint32_t *__restrict__ keys, int32_t *__restrict__ vals)
-{
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t k = ray_morton5(R.ox[i], R.oy[i], R.oz[i], R.dx[i], R.dy[i], R.dz[i], bx0, by0, bz0, sx, sy, sz);
-    uint32_t key = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int b = sel[j];
-        key = (key << 1) | (b >= 0 ? (uint32_t)((k >> b) & 1ull) : 0u);
-    }
-    keys[i] = key;
+    keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
     vals[i] = (int32_t)i;
 }
 
@@ -1433,12 +867,7 @@ static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_
     if constexpr (KU > 0) {
         unsigned long long kr[KU];
         int32_t cr[KU];
-        if (A.cfirst) {
-#pragma unroll
-            for (int j = 0; j < KU; ++j) cr[j] = j < A.K ? A.sc[(int64_t)j * n + r] : 0;
-#pragma unroll
-            for (int j = 0; j < KU; ++j) kr[j] = (j < A.K && cr[j] != 0) ? A.skey[(int64_t)j * n + r] : k0;
-        } else {
+        {
 #pragma unroll
             for (int j = 0; j < KU; ++j) {
                 kr[j] = k0; cr[j] = 0;
@@ -1543,55 +972,6 @@ __global__ __launch_bounds__(256) void k_count(CompactArgs A)
         }
     }
     // wave reductions (fixed order -> deterministic)
-    for (int o = 32; o >= 1; o >>= 1) {
-        cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); cM += __shfl_xor(cM, o, 64);
-    }
-    pk = wave_sum(pk);
-    dm = wave_max(dm);
-    if (lane == 0) {
-        s_cnt[0][wv] = cR; s_cnt[1][wv] = cT; s_cnt[2][wv] = cM; s_pow[wv] = pk; s_dm[wv] = dm;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int64_t b = blockIdx.x, nb = A.nb;
-        A.blk_cnt[0 * nb + b] = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
-        A.blk_cnt[1 * nb + b] = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
-        A.blk_cnt[2 * nb + b] = s_cnt[2][0] + s_cnt[2][1] + s_cnt[2][2] + s_cnt[2][3];
-        A.blk_pow[b] = ((s_pow[0] + s_pow[1]) + s_pow[2]) + s_pow[3];
-        const float m = fmaxf(fmaxf(s_dm[0], s_dm[1]), fmaxf(s_dm[2], s_dm[3]));
-        atomicMax(&A.acc->dmax2_bits, __float_as_uint(m));
-    }
-}
-
-// k_shade + k_count in one pass: a block shades its 1024-ray tile (4 rays per
-// thread, the k_count tile order) and reduces the tile's counts, kept power and
-// max |dir|^2 from registers, in k_count's fixed order (same bits).
-__global__ __launch_bounds__(256) void k_shade_count(ShadeArgs S, CompactArgs A)
-{
-    __shared__ int32_t s_cnt[3][4];
-    __shared__ double s_pow[4];
-    __shared__ float s_dm[4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t tile = (int64_t)blockIdx.x * 1024;
-    int32_t cR = 0, cT = 0, cM = 0;
-    double pk = 0.0;
-    float dm = 0.0f;
-    for (int sub = 0; sub < 4; ++sub) {
-        const int64_t r = tile + sub * 256 + threadIdx.x;
-        if (r < A.n) {
-            const ShadeOut o = shade_ray(S, r);
-            const bool fR = o.r_meas == 0, fT = o.t_meas == 0, fM = o.meas == 1;
-            cR += fR; cT += fT; cM += fM;
-            if (fR) {
-                pk += (double)o.r_pow;
-                dm = fmaxf(dm, o.r_dir.x * o.r_dir.x + o.r_dir.y * o.r_dir.y + o.r_dir.z * o.r_dir.z);
-            }
-            if (fT) {
-                pk += (double)o.t_pow;
-                dm = fmaxf(dm, o.t_dir.x * o.t_dir.x + o.t_dir.y * o.t_dir.y + o.t_dir.z * o.t_dir.z);
-            }
-        }
-    }
     for (int o = 32; o >= 1; o >>= 1) {
         cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); cM += __shfl_xor(cM, o, 64);
     }
@@ -1718,10 +1098,6 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
         if (fR || fT || fM) {
             const float dx = A.o.destx[r], dy = A.o.desty[r], dz = A.o.destz[r];
             const int32_t mid = A.o.imid[r];
-            if (A.childR) {
-                A.childR[r] = fR ? (int32_t)(base[0] + wo[0] + pR) : -1;
-                A.childT[r] = fT ? (int32_t)(base[1] + wo[1] + pT) : -1;
-            }
             if (fR) {
                 const int64_t q = base[0] + wo[0] + pR;
                 A.nR.ox[q] = dx; A.nR.oy[q] = dy; A.nR.oz[q] = dz;
@@ -1739,7 +1115,6 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
                 A.mx[q] = dx; A.my[q] = dy; A.mz[q] = dz; A.mp[q] = A.o.pw[r]; A.mm[q] = mid;
             }
         }
-        if (A.childR && in && !(fR || fT || fM)) { A.childR[r] = -1; A.childT[r] = -1; }
         for (int f = 0; f < 3; ++f) base[f] += tot[f];
         __syncthreads();
     }
@@ -1989,101 +1364,6 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         const int64_t d = (int64_t)A.m_base + s_pre[2] + t;
 #pragma unroll
         for (int a = 0; a < 5; ++a) A.mrec[a * cm + d] = mrow[a];
-    }
-}
-
-// Order chaining.  Tiles of 1024 parents in their traced order: counts of kept
-// reflected / refracted children, single-block scan, scatter of the children's
-// positions (perm_next) and rays (rs_next) in [reflected ; refracted] order.
-__global__ __launch_bounds__(256) void k_ocount(OrderArgs A)
-{
-    __shared__ int32_t s_c[2][4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int32_t cR = 0, cT = 0;
-    for (int sub = 0; sub < 4; ++sub) {
-        const int64_t s = (int64_t)blockIdx.x * 1024 + sub * 256 + threadIdx.x;
-        if (s < A.n) {
-            const int32_t r = A.perm[s];
-            cR += A.childR[r] >= 0;
-            cT += A.childT[r] >= 0;
-        }
-    }
-    for (int o = 32; o >= 1; o >>= 1) { cR += __shfl_xor(cR, o, 64); cT += __shfl_xor(cT, o, 64); }
-    if (lane == 0) { s_c[0][wv] = cR; s_c[1][wv] = cT; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        A.blk[blockIdx.x] = s_c[0][0] + s_c[0][1] + s_c[0][2] + s_c[0][3];
-        A.blk[A.nb + blockIdx.x] = s_c[1][0] + s_c[1][1] + s_c[1][2] + s_c[1][3];
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_oscan(OrderArgs A)
-{
-    __shared__ long long s_sc[2][1024];
-    const int t = threadIdx.x;
-    const int64_t nb = A.nb, per = (nb + 1023) / 1024, lo = t * per, hi = min(nb, lo + per);
-    long long loc[2] = {0, 0};
-    for (int64_t i = lo; i < hi; ++i) { loc[0] += A.blk[i]; loc[1] += A.blk[nb + i]; }
-    s_sc[0][t] = loc[0]; s_sc[1][t] = loc[1];
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        long long v0 = 0, v1 = 0;
-        if (t >= off) { v0 = s_sc[0][t - off]; v1 = s_sc[1][t - off]; }
-        __syncthreads();
-        s_sc[0][t] += v0; s_sc[1][t] += v1;
-        __syncthreads();
-    }
-    long long run[2] = {s_sc[0][t] - loc[0], s_sc[1][t] - loc[1]};     // exclusive
-    for (int64_t i = lo; i < hi; ++i) {
-        const int32_t a = A.blk[i], b = A.blk[nb + i];
-        A.blk[i] = (int32_t)run[0]; A.blk[nb + i] = (int32_t)run[1];
-        run[0] += a; run[1] += b;
-    }
-    if (t == 1023) *A.totR = s_sc[0][1023];
-}
-
-__global__ __launch_bounds__(256) void k_oscatter(OrderArgs A)
-{
-    __shared__ int32_t s_w[2][4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t nn = (int64_t)A.acc->nR + (int64_t)A.acc->nT;
-    const int64_t totR = *A.totR;
-    int64_t base[2] = {A.blk[blockIdx.x], totR + A.blk[A.nb + blockIdx.x]};
-    for (int sub = 0; sub < 4; ++sub) {
-        const int64_t s = (int64_t)blockIdx.x * 1024 + sub * 256 + threadIdx.x;
-        const bool in = s < A.n;
-        const int32_t r = in ? A.perm[s] : 0;
-        const int32_t qR = in ? A.childR[r] : -1, qT = in ? A.childT[r] : -1;
-        const bool fR = qR >= 0, fT = qT >= 0;
-        const uint64_t bR = __ballot(fR), bT = __ballot(fT);
-        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        if (lane == 0) { s_w[0][wv] = __popcll(bR); s_w[1][wv] = __popcll(bT); }
-        __syncthreads();
-        int32_t wo[2] = {0, 0}, tot[2] = {0, 0};
-        for (int w = 0; w < 4; ++w)
-            for (int f = 0; f < 2; ++f) {
-                if (w < wv) wo[f] += s_w[f][w];
-                tot[f] += s_w[f][w];
-            }
-        if (fR || fT) {
-            const float ox = A.o.destx[r], oy = A.o.desty[r], oz = A.o.destz[r];
-            if (fR) {
-                const int64_t j = base[0] + wo[0] + __popcll(bR & below);
-                A.perm_next[j] = qR;
-                A.rs_next[j] = ox; A.rs_next[nn + j] = oy; A.rs_next[2 * nn + j] = oz;
-                A.rs_next[3 * nn + j] = A.o.rdx[r]; A.rs_next[4 * nn + j] = A.o.rdy[r];
-                A.rs_next[5 * nn + j] = A.o.rdz[r];
-            }
-            if (fT) {
-                const int64_t j = base[1] + wo[1] + __popcll(bT & below);
-                A.perm_next[j] = qT;
-                A.rs_next[j] = ox; A.rs_next[nn + j] = oy; A.rs_next[2 * nn + j] = oz;
-                A.rs_next[3 * nn + j] = A.o.tdx[r]; A.rs_next[4 * nn + j] = A.o.tdy[r];
-                A.rs_next[5 * nn + j] = A.o.tdz[r];
-            }
-        }
-        for (int f = 0; f < 2; ++f) base[f] += tot[f];
-        __syncthreads();
     }
 }
 

@@ -370,6 +370,7 @@ LPC_HD float filter_testh(float cx, float cy, float cz, float negB, float negA, 
 // node_record() of ALL triangles below it, so a ray whose line Moller-Trumbore
 // accepts against some triangle passes every test on the way down.  Unused
 // children: never.  128 B (W 4) / 256 B (W 8): whole scalar-load lines.
+// ref >= 0: child node; ref < 0: triangle ~ref.
 template <int W>
 struct NodeW {
     float cx[W], cy[W], cz[W], negB[W], negA[W];
@@ -378,25 +379,6 @@ struct NodeW {
 };
 typedef NodeW<4> Node4;
 typedef NodeW<8> Node8;
-
-// The same hierarchy as a threaded depth-first entry list (k_lane): a node's
-// entry is followed by its children's entries (and their subtrees); skip = the
-// entry after the subtree.  tri >= 0: a triangle (its filter record), else an
-// internal node (its node_record test).  32 B.
-struct LaneEntry {
-    float cx, cy, cz, negB, negA;
-    int32_t skip, tri, pad;
-};
-
-// Leaf children are triangles or "fan groups".  A fan group holds up to
-// LPC_GROUP_SIZE thin triangles whose filter spheres pile up around a common
-// point (revolve_curve's poles): reached through the hierarchy, a wave tests all
-// of them lane-parallel against its packet bound (packet_sphere_test) and then
-// each candidate per ray, instead of walking the many subtrees that share the
-// pole.  A group's own test is node_record() of its members.
-//   ref >= LPC_GROUP_REF: triangle ~ref;  ref < LPC_GROUP_REF: group LPC_GROUP_REF - 1 - ref.
-#define LPC_GROUP_REF (-(1 << 30))
-#define LPC_GROUP_SIZE 64
 
 // A "sliver": a triangle whose sphere test degenerates (B >= 0.5, e.g.
 // revolve_curve's pole triangles with two vertices 1e-11 apart).  For it

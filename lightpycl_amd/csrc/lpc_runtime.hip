@@ -57,10 +57,9 @@ struct Pop {
 };
 
 struct PieceTable {
-    DBuf pieces, spieces;              // hierarchy pieces (k_intersect), sliver pieces (k_slivers)
+    DBuf pieces, spieces;              // hierarchy pieces (k_rootwalk / k_intersect), sliver pieces (k_slivers)
     int32_t npieces = 0, nspieces = 0;
     std::vector<float> sdmin;          // per sliver piece (ascending): min dmin of its slivers
-    int32_t gmax = 0;                  // most fan groups under one piece (k_groups item slots)
 };
 
 const int kShadeF = 12;   // float arrays of the shade outputs
@@ -81,11 +80,7 @@ struct lpc_handle {
     std::vector<std::vector<int32_t>> run_levels;    // per run: (first node, count) per level, root first
     std::vector<FiltRec> node_self;                  // each node's own test (piece roots)
     std::vector<float> sliver_dmin_host;             // SliverRec::dmin, host copy
-    std::vector<int32_t> node_entry, node_end;       // a node's LaneEntry and the entry after its subtree
-    DBuf d_lane;                                     // LaneEntry list (k_lane)
-    bool lane_ok = false;                            // entry list built (no fan groups)
     double pop_dmax2 = INFINITY, init_dmax2 = INFINITY;   // max |D|^2 of the trace population / emitted rays
-    std::vector<int32_t> node_groups;                // fan groups in each node's subtree
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
@@ -93,40 +88,19 @@ struct lpc_handle {
     std::vector<int32_t> slot_run;
     std::vector<int32_t> meas_meshes;
     DBuf d_nodes, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
-    DBuf d_grec, d_gxrec;                            // fan-group member filter / exact records
-    double flat_ratio = 0.0;                         // fan-group threshold on rho^2 / area (0: no groups)
-    int64_t n_groups = 0, n_grouped = 0;
     double dcap = 16.0;
-    std::map<int32_t, PieceTable> ptabs;
+    std::map<std::vector<int32_t>, PieceTable> ptabs;   // by the hierarchy level each live run is cut at
     // workspace
     int64_t chunk = 0;                              // rays per chunk (0 -> default)
     int64_t ws_rays = 0;
     DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf w_aos;                                     // rays as 32-byte rows for the coherence gather
-    DBuf w_keypart;                                 // per-block OR/AND of the 40-bit codes + selected bits
-    int sort_mode = 1;                              // 1: 32-bit key (rocPRIM default), 2: adaptive 16-bit
-    int64_t onesweep_min = 500000;                  // 32-bit key: onesweep from this many rays
-    int xcd_min_rows = 0;                           // k_intersect XCD-aware order from this many rows (0 off)
+    int64_t onesweep_min = 500000;                  // onesweep radix sort from this many rays (merge sort below)
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
-    bool order_chain = false;                       // children inherit their parents' traced order (no sort)
-    bool order_ready = false;                       // w_perm2/w_rs2[order_buf] hold the next launch's order
-    bool order_pending = false;                     // written this iteration; ready once n_next is known
-    int order_buf = 0;
-    int64_t order_n = -1;
-    const int32_t *last_perm = nullptr;             // order of the last intersect launch (NULL: unsorted)
-    DBuf w_chR, w_chT, w_oblk, w_perm2[2], w_rs2[2];
     int64_t acc_pending_total = 0;
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
-    int64_t roots_tasks = 0;                        // LPC_ROOTS_TASKS: k_roots_s splits each packet's pieces into up to 16
-                                                    //   classes so that a launch has about this many tasks (0: fewest classes)
-    bool fork_late = false;                         // LPC_FORK_LATE: side-stream fork event after k_roots (measured: no gain)
-    bool fork_pending = false;                      // run_intersect -> run_queue: the fork event is still to record
-    bool ev_sysfence = true;                        // LPC_EV_SYSFENCE=0: events without the system-scope fence (measured slower)
-    int xcd_walk = 0;                               // LPC_XCD_WALK: packet-range root shards, XCD-local k_rootwalk (QueueArgs::xcd)
-    int shade_cfirst = 0;                           // LPC_SHADE_CFIRST: traced shading reads a slot's key only if its count > 0 (measured neutral)
     int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
-    bool fuse_shade = false;                        // k_shade_count instead of k_shade + k_count (fewer waves: slower)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
     DBuf w_gsum;                                    // per 256-tile group counts, two buffers (zero when unused)
@@ -137,25 +111,18 @@ struct lpc_handle {
     float slots_mrl = 0.0f;
     bool misc_clean = false;                        // the launch words were reset for the next launch
     bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
-    int walk_waves = 6;                             // LPC_WALK_WAVES: k_rootwalk / k_spill launch bounds (6-8 waves/SIMD)
     int half = 3;                                   // LPC_HALF: half-line cull (see run_intersect; 3: piece roots, not for emitted rays)
     bool half_now = false;                          // ... for the launch in progress
     bool half_roots = false;                        // ... at the piece roots (k_roots)
-    bool gather_aos = true;
+    bool in_trace = false;                          // run_intersect called from lpc_trace_iterate
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
-    DBuf w_pk64;                                    // PacketRec per 64-ray packet (k_groups)
-    DBuf w_gitems, w_gcount;                        // k_intersect -> k_groups fan-group items
     DBuf d_misc;                                    // LPC_MISC_WORDS per-launch words
     size_t sort_tmp_bytes = 0;
     bool sort_rays = true;
     int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
-    int64_t lane_max = 0;                           // populations up to this many rays: k_lane
-    int64_t lane_g = 1;                             // k_lane pieces: nodes per run (1: the run roots)
-    int isect_minb = 6;                             // k_intersect launch bounds: min blocks per CU (1 or 6)
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
-    int key_mode = 0;                               // coherence key, see run_intersect
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 24;                          // node visits before a wave hands over (0 off)
     int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
@@ -169,33 +136,20 @@ struct lpc_handle {
     int spill_shrink = 1;                           // level l grid = spill_blocks >> (shrink * l) ...
     int64_t spill_min_blocks = 256;                 // ... but at least this
     int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
-    bool piece_loop = false;                        // k_intersect: waves loop over the pieces
-    int64_t loop_min_packets = 8192;                //   ... when the population has this many packets
     int64_t wave_target = 131072;                   // k_intersect: group pieces per wave above this many waves
     int node_w = 8;                                 // hierarchy width for the next build (4 or 8)
     int built_w = 4;                                // width of the records in d_nodes
     int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
     int64_t sliver_ppw = 0;                         // k_slivers: packets per wave (0: from sliver_waves)
-    int sliver_rays = 128;                          // k_slivers packet size (64 or 128 rays)
     DBuf w_spill;                                   // k_spill queue
-    // work queue (k_roots + persistent k_trav) instead of k_intersect + k_spill
     bool traced = true;                             // LPC_TRACED: aggregate iterations in coherence order
-    bool traced_resort = false;                     // LPC_TRACED_SORT: sort the children again
     bool pop_traced = false;                        // the population is in its parents' traced order
     bool pop_emitted = false;                       // the population is the emitted rays (set_rays)
     int init_key_lo = 0, init_key_hi = 32;          // key bits that vary over the emitted rays (set_rays)
-    int queue = 2;                                  // LPC_QUEUE: 0 k_intersect, 1 persistent k_trav, 2 k_rootwalk
+    int queue = 2;                                  // LPC_QUEUE: 2 root items + k_rootwalk (default), 0 k_intersect
     int64_t q_walk_blocks = 16384;                  // k_rootwalk grid in 4-wave units (grid-stride)
-    int q_walk_wpb = 1;                             // LPC_Q_WALK_WPB: waves per k_rootwalk block (1 or 4)
-    int spill_wpb = 1;                              // LPC_SPILL_WPB: waves per k_spill block (1 or 4)
     int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
-    int q_batch = 2;                                // root items per claim
-    int q_hunger = 1;                               // hand work over to waiting waves
-    int64_t q_blocks = 0;                           // k_trav grid (0: CUs x resident blocks per CU)
-    int q_per_cu = 6;                               // ... at most this many per CU
-    int64_t q_dcap = 1 << 16;                       // hand-over slots per shard
-    int64_t q_spin = 1 << 22;                       // polls before a waiting wave gives up
-    DBuf w_qroots, d_qdq;                           // root items, hand-over slots (kept LPC_QEMPTY)
+    DBuf w_qroots;                                  // root items
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
     DevAcc *acc_map = nullptr, *acc_map_dev = nullptr;   // mapped pinned copy k_scan publishes (+ device address)
     unsigned int acc_seq = 0;
@@ -204,7 +158,6 @@ struct lpc_handle {
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
     hipEvent_t ev_side[2] = {nullptr, nullptr};     // rays ready (main -> side), slivers done (side -> main)
     double host_last = 0.0, t_first = 0.0;
-    int64_t split = INT64_MAX;                      // population rows [0, split) = reflected block
     bool pop_init = false;                          // the population is I (the emitted rays, set_rays)
     bool mp_valid = false;                          // mp_last = the trace's measured power per measure mesh
     DBuf d_mrun;                                    // its running sums on the device (k_stage_move)
@@ -223,7 +176,7 @@ struct lpc_handle {
     DBuf d_wrec;                                    // per-wave records of the last k_intersect (level 3)
     int64_t wrec_count = 0;
     // profiling
-    bool prof = false, prof_stats = false, prof_waves = false, prof_light = false, prof_items = false;
+    bool prof = false, prof_stats = false, prof_waves = false, prof_light = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
@@ -380,27 +333,20 @@ static int build_records(lpc_handle *h)
     const size_t node_bytes = W == 8 ? sizeof(Node8) : sizeof(Node4);
     std::vector<uint8_t> nodes;                     // NodeW<W> records
     int32_t n_nodes = 0;
-    std::vector<LaneEntry> lane;                    // threaded entry list (k_lane)
-    bool lane_ok = true;
-    h->node_entry.clear(); h->node_end.clear();
     std::vector<SliverRec> slivers;
     h->run_levels.clear();
     h->node_self.clear();
-    h->node_groups.clear();
     h->run_slo.clear(); h->run_shi.clear();
     h->sliver_dmin_host.clear();
     h->n_slivers = 0;
     const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 0.0f, INFINITY);
-    std::vector<FiltRec> grec;                      // fan-group members, LPC_GROUP_SIZE per group
-    std::vector<ExactRec> gxrec;                    // their exact records
-    h->n_groups = h->n_grouped = 0;
     auto vptr = [&](int32_t t, int v) -> const float * {
         return v == 0 ? &h->hv0[4 * (size_t)t] : v == 1 ? &h->hv1[4 * (size_t)t] : &h->hv2[4 * (size_t)t];
     };
     for (size_t r = 0; r < h->run_lo.size(); ++r) {
         const int32_t lo = h->run_lo[r], cnt_all = h->run_hi[r] - lo;
-        std::vector<FiltRec> fr, fl;                 // plain triangles, fan (thin) triangles
-        std::vector<double> cen, fcen;
+        std::vector<FiltRec> fr;                     // hierarchy triangles
+        std::vector<double> cen;
         std::vector<int32_t> sl;
         for (int32_t i = 0; i < cnt_all; ++i) {
             const int32_t t = lo + i;
@@ -408,20 +354,8 @@ static int build_records(lpc_handle *h)
             const FiltRec f = filter_record(V0, V1, V2, t, h->dcap, h->scene_scale);
             if (f.negA == INFINITY) continue;                     // never a candidate
             if (f.negB < -1e29f) { sl.push_back(t); continue; }
-            // thin triangles (filter sphere radius^2 / area above flat_ratio) pile
-            // their spheres around shared points: they go to fan groups
-            double rho2 = 0.0, e1[3], e2[3];
-            for (int k = 0; k < 3; ++k) { e1[k] = (double)V1[k] - V0[k]; e2[k] = (double)V2[k] - V0[k]; }
-            for (const float *V : {V0, V1, V2}) {
-                const double x = V[0] - (double)f.cx, y = V[1] - (double)f.cy, z = V[2] - (double)f.cz;
-                rho2 = std::max(rho2, x * x + y * y + z * z);
-            }
-            const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2],
-                         cz = e1[0] * e2[1] - e1[1] * e2[0];
-            const double area = 0.5 * sqrt(cx * cx + cy * cy + cz * cz);
-            const bool flat = h->flat_ratio > 0.0 && area > 0.0 && rho2 > h->flat_ratio * area;
-            (flat ? fl : fr).push_back(f);
-            for (int k = 0; k < 3; ++k) (flat ? fcen : cen).push_back(((double)V0[k] + V1[k] + V2[k]) / 3.0);
+            fr.push_back(f);
+            for (int k = 0; k < 3; ++k) cen.push_back(((double)V0[k] + V1[k] + V2[k]) / 3.0);
         }
         h->run_slo.push_back((int32_t)slivers.size());
         // slivers ordered by dmin, so a 64-sliver piece holds similar ones
@@ -447,8 +381,8 @@ static int build_records(lpc_handle *h)
         h->run_shi.push_back((int32_t)slivers.size());
         h->n_slivers += (int64_t)sl.size();
         h->run_levels.push_back(std::vector<int32_t>());
-        // hierarchy entries: plain triangles and fan groups (each with its test,
-        // child ref, centroid and triangle list)
+        // hierarchy entries: the triangles (each with its test, child ref,
+        // centroid and triangle list)
         struct Entry { FiltRec t; int32_t ref; double c[3]; int32_t t0, t1; };
         std::vector<Entry> E;
         std::vector<int32_t> etri;                   // triangle ids of the entries, [t0, t1) each
@@ -458,48 +392,6 @@ static int build_records(lpc_handle *h)
             for (int k = 0; k < 3; ++k) e.c[k] = cen[3 * i + k];
             e.t0 = (int32_t)etri.size(); etri.push_back(fr[i].idx); e.t1 = (int32_t)etri.size();
             E.push_back(e);
-        }
-        if (!fl.empty()) {
-            const int64_t nf = (int64_t)fl.size();
-            std::vector<int32_t> pf((size_t)nf);
-            for (int64_t i = 0; i < nf; ++i) pf[(size_t)i] = (int32_t)i;
-            int64_t capf = 4;
-            while (capf < nf) capf *= 4;
-            split_order(pf.data(), nf, capf, fcen);
-            for (int64_t c0 = 0; c0 < nf; c0 += LPC_GROUP_SIZE) {
-                const int64_t c1 = std::min<int64_t>(nf, c0 + LPC_GROUP_SIZE);
-                const int32_t g = (int32_t)(grec.size() / LPC_GROUP_SIZE);
-                Entry e;
-                e.c[0] = e.c[1] = e.c[2] = 0.0;
-                e.t0 = (int32_t)etri.size();
-                std::vector<const float *> gv;
-                for (int64_t j = c0; j < c0 + LPC_GROUP_SIZE; ++j) {
-                    gxrec.push_back(ExactRec{});               // zero edges: never accepts
-                    if (j >= c1) { grec.push_back(never); continue; }
-                    const FiltRec &f = fl[(size_t)pf[(size_t)j]];
-                    grec.push_back(f);
-                    {
-                        const float *A = vptr(f.idx, 0), *B = vptr(f.idx, 1), *C = vptr(f.idx, 2);
-                        ExactRec x;
-                        x.v0x = A[0]; x.v0y = A[1]; x.v0z = A[2];
-                        x.e1x = B[0] - A[0]; x.e1y = B[1] - A[1]; x.e1z = B[2] - A[2];
-                        x.e2x = C[0] - A[0]; x.e2y = C[1] - A[1]; x.e2z = C[2] - A[2];
-                        x.pad0 = x.pad1 = x.pad2 = 0.0f;
-                        gxrec[gxrec.size() - 1] = x;
-                    }
-                    etri.push_back(f.idx);
-                    for (int v = 0; v < 3; ++v) gv.push_back(vptr(f.idx, v));
-                    for (int k = 0; k < 3; ++k) e.c[k] += fcen[3 * (size_t)pf[(size_t)j] + k] / (double)(c1 - c0);
-                }
-                e.t1 = (int32_t)etri.size();
-                e.t = never;
-                node_record(gv.data(), (int)(c1 - c0), h->scene_scale, &e.t.cx, &e.t.cy, &e.t.cz, &e.t.negB,
-                            &e.t.negA);
-                e.ref = LPC_GROUP_REF - 1 - g;
-                E.push_back(e);
-                h->n_groups += 1;
-                h->n_grouped += c1 - c0;
-            }
         }
         const int32_t cnt = (int32_t)E.size();
         if (cnt == 0) continue;
@@ -552,16 +444,10 @@ static int build_records(lpc_handle *h)
                 }
                 const int32_t a = ent[i].a, b = ent[std::min(i + (size_t)W - 1, ent.size() - 1)].b;
                 const FiltRec self = range_test(a, b);
-                int32_t ng = 0;
-                for (int k = 0; k < W && i + k < ent.size(); ++k) {
-                    const int32_t ref = ent[i + k].ref;
-                    ng += ref >= 0 ? h->node_groups[(size_t)ref] : ref < LPC_GROUP_REF ? 1 : 0;
-                }
                 up.push_back({self, n_nodes, a, b});
                 nodes.insert(nodes.end(), (const uint8_t *)N.data(), (const uint8_t *)N.data() + node_bytes);
                 ++n_nodes;
                 h->node_self.push_back(self);
-                h->node_groups.push_back(ng);
             }
             levels.push_back({first, (int32_t)up.size()});
             ent.swap(up);
@@ -572,62 +458,7 @@ static int build_records(lpc_handle *h)
             h->run_levels.back().push_back(it->first);
             h->run_levels.back().push_back(it->second);
         }
-        // threaded entry list of this run (k_lane): root entry, then depth first
-        {
-            const int32_t root = levels.back().first;
-            auto rec_at = [&](int32_t node, int k, LaneEntry &e) -> int32_t {
-                const uint32_t *Nw = (const uint32_t *)(nodes.data() + (size_t)node * node_bytes);
-                float f5[5];
-                for (int q = 0; q < 5; ++q) memcpy(&f5[q], &Nw[(size_t)q * W + k], 4);
-                int32_t ref;
-                memcpy(&ref, &Nw[(size_t)5 * W + k], 4);
-                e.cx = f5[0]; e.cy = f5[1]; e.cz = f5[2]; e.negB = f5[3]; e.negA = f5[4]; e.pad = 0;
-                return ref;
-            };
-            std::function<void(int32_t)> emit = [&](int32_t node) {
-                for (int k = 0; k < W; ++k) {
-                    LaneEntry e;
-                    const int32_t ref = rec_at(node, k, e);
-                    if (!(e.negA < INFINITY)) continue;                 // unused child / never
-                    if (ref >= 0) {
-                        const int32_t at = (int32_t)lane.size();
-                        e.tri = -1; e.skip = 0;
-                        lane.push_back(e);
-                        h->node_entry[(size_t)ref] = at;
-                        emit(ref);
-                        lane[(size_t)at].skip = (int32_t)lane.size();
-                        h->node_end[(size_t)ref] = (int32_t)lane.size();
-                    } else if (ref >= LPC_GROUP_REF) {
-                        e.tri = ~ref; e.skip = (int32_t)lane.size() + 1;
-                        lane.push_back(e);
-                    } else {
-                        lane_ok = false;                                // fan group: no lane path
-                    }
-                }
-            };
-            h->node_entry.resize((size_t)n_nodes, -1);
-            h->node_end.resize((size_t)n_nodes, -1);
-            const FiltRec &rs0 = h->node_self[(size_t)root];
-            LaneEntry e0;
-            e0.cx = rs0.cx; e0.cy = rs0.cy; e0.cz = rs0.cz; e0.negB = rs0.negB; e0.negA = rs0.negA;
-            e0.tri = -1; e0.skip = 0; e0.pad = 0;
-            const int32_t at = (int32_t)lane.size();
-            lane.push_back(e0);
-            h->node_entry[(size_t)root] = at;
-            emit(root);
-            lane[(size_t)at].skip = (int32_t)lane.size();
-            h->node_end[(size_t)root] = (int32_t)lane.size();
-        }
     }
-    h->lane_ok = lane_ok && !lane.empty();
-    if (lane.empty()) { LaneEntry z; memset(&z, 0, sizeof(z)); z.negA = INFINITY; z.tri = -1; lane.push_back(z); }
-    RETIF(dalloc(h, h->d_lane, lane.size() * sizeof(LaneEntry)));
-    HIPCHK(h, hipMemcpy(h->d_lane.p, lane.data(), lane.size() * sizeof(LaneEntry), hipMemcpyHostToDevice));
-    if (grec.empty()) { grec.assign(LPC_GROUP_SIZE, never); gxrec.assign(LPC_GROUP_SIZE, ExactRec{}); }
-    RETIF(dalloc(h, h->d_grec, grec.size() * sizeof(FiltRec)));
-    RETIF(dalloc(h, h->d_gxrec, gxrec.size() * sizeof(ExactRec)));
-    HIPCHK(h, hipMemcpy(h->d_grec.p, grec.data(), grec.size() * sizeof(FiltRec), hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->d_gxrec.p, gxrec.data(), gxrec.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
     // spare records so no buffer is empty
     if (n_nodes == 0) { nodes.assign(node_bytes, 0); n_nodes = 1; }
     if (slivers.empty()) {
@@ -666,28 +497,33 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
     int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (target_blocks + bx * live_runs - 1) /
                                                                         (bx * live_runs)));
     if (g_force > 0) g = g_force;
-    auto it = h->ptabs.find(g);
+    // the level each live run is cut at: the shallowest with >= g nodes (many g
+    // give the same cut, so a scene builds only a few tables)
+    std::vector<int32_t> cut(nr, -1);
+    for (size_t r = 0; r < nr; ++r) {
+        if (run_slot[r] < 0) continue;
+        const std::vector<int32_t> &L = h->run_levels[r];
+        size_t lv = 0;
+        while (lv + 1 < L.size() / 2 && L[2 * lv + 1] < g) ++lv;
+        cut[r] = L.empty() ? -2 : (int32_t)lv;
+    }
+    auto it = h->ptabs.find(cut);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
     std::vector<Piece> pcs, spc;
     std::vector<float> sdm;
-    int32_t gmax = 0;
     for (size_t r = 0; r < nr; ++r) {
         if (run_slot[r] < 0) continue;
         const std::vector<int32_t> &L = h->run_levels[r];
         if (!L.empty()) {
-            size_t lv = 0;
-            while (lv + 1 < L.size() / 2 && L[2 * lv + 1] < g) ++lv;
+            const size_t lv = (size_t)cut[r];
             for (int32_t i = 0; i < L[2 * lv + 1]; ++i) {
                 Piece p;
                 memset(&p, 0, sizeof(p));
                 p.root = L[2 * lv] + i;
                 const FiltRec &t = h->node_self[(size_t)p.root];
                 p.cx = t.cx; p.cy = t.cy; p.cz = t.cz; p.negB = t.negB; p.negA = t.negA;
-                p.s_lo = h->node_entry.empty() ? 0 : h->node_entry[(size_t)p.root];   // k_lane entry range
-                p.s_hi = h->node_end.empty() ? 0 : h->node_end[(size_t)p.root];
                 p.slot = run_slot[r];
                 pcs.push_back(p);
-                gmax = std::max(gmax, h->node_groups[(size_t)p.root]);
             }
         }
         for (int32_t a = h->run_slo[r]; a < h->run_shi[r]; a += 64) {
@@ -702,10 +538,9 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
         }
     }
     if (pcs.size() > 65535 || spc.size() > 65535) return set_err(h, LPC_E_ARG, "too many triangle pieces");
-    PieceTable &t = h->ptabs[g];
+    PieceTable &t = h->ptabs[cut];
     t.npieces = (int32_t)pcs.size();
     t.nspieces = (int32_t)spc.size();
-    t.gmax = gmax;
     {   // sliver pieces in ascending dmin: a launch takes the prefix its rays can reach
         std::vector<size_t> o(spc.size());
         for (size_t i = 0; i < o.size(); ++i) o[i] = i;
@@ -728,13 +563,12 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
 }
 
 // Coherence sort: rocPRIM's default algorithm choice (block merge sort up to
-// 1 Mi items, onesweep above).  Forcing onesweep at every size measured slower
-// (189 vs 131 us per 1 M-ray iteration incl. k_raykey/k_gather: 4 digit passes +
-// histogram + lookback-state fills, each latency-bound).
+// 1 Mi items, onesweep above) below onesweep_min rays, onesweep from there
+// (RaySortOnesweep: 8-bit digit passes; forcing it at every size measured slower,
+// 189 vs 131 us per 1 M-ray iteration incl. k_raykey/k_gather).
 using RaySortCfg = rocprim::default_config;
-// The 16-bit adaptive key (LPC_SORT=2): two 8-bit onesweep passes at every size.
-using RaySortCfg16 = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                rocprim::default_config, 0>;
+using RaySortOnesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                   rocprim::default_config, 0>;
 
 // Rays per chunk.  Default: as many as ~32 GB of per-chunk workspace holds (slots
 // 12 B per mesh + ~200 B of coherence copies, shade outputs and sort buffers per
@@ -759,7 +593,6 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_sc, (size_t)h->K * C * 4));
         RETIF(dalloc(h, h->w_rs, (size_t)8 * C * 4));
         RETIF(dalloc(h, h->w_pk, (size_t)((C + 127) / 128) * sizeof(PacketRec)));
-        RETIF(dalloc(h, h->w_pk64, (size_t)((C + 63) / 64) * sizeof(PacketRec)));
         RETIF(dalloc(h, h->d_misc, LPC_MISC_WORDS * 4));
         RETIF(dalloc(h, h->w_shf, (size_t)kShadeF * C * 4));
         RETIF(dalloc(h, h->w_shi, (size_t)kShadeI * C * 4));
@@ -775,16 +608,12 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                                         (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)C, 0,
                                                         32, h->stream));
-        size_t tb16 = 0, tb32 = 0;
-        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(nullptr, tb16, (const uint32_t *)nullptr,
-                                                          (uint32_t *)nullptr, (const int32_t *)nullptr,
-                                                          (int32_t *)nullptr, (size_t)C, 0, 16, h->stream));
-        HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(nullptr, tb32, (const uint32_t *)nullptr,
-                                                          (uint32_t *)nullptr, (const int32_t *)nullptr,
-                                                          (int32_t *)nullptr, (size_t)C, 0, 32, h->stream));
-        tb = std::max(tb, std::max(tb16, tb32));
+        size_t tb1 = 0;
+        HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(nullptr, tb1, (const uint32_t *)nullptr,
+                                                             (uint32_t *)nullptr, (const int32_t *)nullptr,
+                                                             (int32_t *)nullptr, (size_t)C, 0, 32, h->stream));
+        tb = std::max(tb, tb1);
         RETIF(dalloc(h, h->w_sort_tmp, tb));
-        RETIF(dalloc(h, h->w_keypart, (size_t)((C + 255) / 256) * 16 + 64 * 4));
         const int64_t nt = (C + LPC_ST_TILE - 1) / LPC_ST_TILE;
         RETIF(dalloc(h, h->w_fc, (size_t)nt * (8 + 4 + 4 + 8 * LPC_MP_MAX) + 64));   // staging tiles' power, counts,
                                                                                       // max |dir|^2, measured power
@@ -824,10 +653,7 @@ static hipEvent_t ev_get(lpc_handle *h)
         return e;
     }
     hipEvent_t e;
-    // LPC_EV_SYSFENCE=0: profiling events without the system-scope fence (measured:
-    // the timed stage shortens, the step does not)
-    if (hipEventCreateWithFlags(&e, h->ev_sysfence ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess)
-        return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDefault) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -917,37 +743,22 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
     for (int l = 0; l < levels; ++l) {
         SpillArgs I, O;
         spill_level_args(h, SP, l, levels, &I, &O);
-        // later levels hold fewer items (and often none): smaller grids
-        // grid in 4-wave units, launched as single-wave blocks unless LPC_SPILL_WPB=4
-        const unsigned sb = (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l));
-        const int wpb = h->spill_wpb;
-        const unsigned g = sb * 4u / (unsigned)wpb;
-#define LPC_LAUNCH_SPILL(WW, PB, NT, PF)                                                                         \
-    hipLaunchKernelGGL((k_spill<WW, PB, PF>), dim3(g), dim3(64 * PB), 0, h->stream, ray, n, perm,                \
+        // later levels hold fewer items (and often none): smaller grids, in
+        // 4-wave units, launched as single-wave blocks
+        const unsigned g =
+            (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l)) * 4u;
+#define LPC_LAUNCH_SPILL(WW, NT, PF, HF)                                                                         \
+    hipLaunchKernelGGL((k_spill<WW, PF, HF>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,                        \
                        (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
                        I, O)
         // profiling counters only in the PROF instantiation (fewer live registers without)
-        if (stats) {
-            if (h->built_w == 8) { if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8, true); else LPC_LAUNCH_SPILL(8, 1, Node8, true); }
-            else { if (wpb == 4) LPC_LAUNCH_SPILL(4, 4, Node4, true); else LPC_LAUNCH_SPILL(4, 1, Node4, true); }
+        if (h->built_w == 8) {
+            if (stats) LPC_LAUNCH_SPILL(8, Node8, true, false);
+            else if (h->half_now) LPC_LAUNCH_SPILL(8, Node8, false, true);   // the half-line cull (LPC_HALF 1/2)
+            else LPC_LAUNCH_SPILL(8, Node8, false, false);
         } else {
-            if (h->built_w == 8) {
-                if (wpb == 4) LPC_LAUNCH_SPILL(8, 4, Node8, false);
-                else if (h->half_now)             // the half-line cull (LPC_HALF)
-                    hipLaunchKernelGGL((k_spill<8, 1, false, 6, true>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
-                                       (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
-                                       skey, scnt, stats, I, O);
-                else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
-                    hipLaunchKernelGGL((k_spill<8, 1, false, 7>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
-                                       (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
-                                       skey, scnt, stats, I, O);
-                else if (h->walk_waves == 8)
-                    hipLaunchKernelGGL((k_spill<8, 1, false, 8>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
-                                       (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len,
-                                       skey, scnt, stats, I, O);
-                else LPC_LAUNCH_SPILL(8, 1, Node8, false);
-            }
-            else { if (wpb == 4) LPC_LAUNCH_SPILL(4, 4, Node4, false); else LPC_LAUNCH_SPILL(4, 1, Node4, false); }
+            if (stats) LPC_LAUNCH_SPILL(4, Node4, true, false);
+            else LPC_LAUNCH_SPILL(4, Node4, false, false);
         }
 #undef LPC_LAUNCH_SPILL
     }
@@ -968,34 +779,15 @@ static int32_t q_level(const lpc_handle *h, int64_t n)
                                                                       (npk * live_runs)));
 }
 
-// k_trav grid: every block resident at once (CUs x blocks per CU from the
-// occupancy query) unless LPC_Q_BLOCKS says otherwise.  Correctness does not
-// depend on residency (a block that starts late finds no root item left).
-template <int W>
-static int q_grid(lpc_handle *h, unsigned *grid)
-{
-    if (h->q_blocks > 0) { *grid = (unsigned)h->q_blocks; return 0; }
-    int per_cu = 0;
-    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trav<W, 1>, 64, 0));
-    // the hardware admits fewer 256-thread blocks than the API says when the
-    // kernel uses ~100 SGPRs (MI355X_MICROARCH.md, residency): k_trav's launch
-    // bounds ask for 6 per CU; a block that is not resident starts only when
-    // another exits, at the end of the launch
-    per_cu = std::min(per_cu, 4 * h->q_per_cu);          // single-wave blocks: 4 per SIMD row of 6
-    *grid = (unsigned)std::max(1, per_cu) * (unsigned)std::max(1, h->cus);
-    return 0;
-}
-
-// A k_trav wave gave up waiting (QueueArgs::err, kept in DevAcc::qerr): the
-// launch's results are incomplete.  Re-empty the hand-over slots, clear the flag
-// and report.  Never expected; the bound only keeps a logic error from hanging
-// the GPU.
+// A device-side consistency check failed (QueueArgs::err / the compaction's
+// prefix check, kept in DevAcc::qerr): the launch's results are incomplete.
+// Clear the flag and report.  Never expected; the checks keep a sizing error from
+// silently losing intersections.
 static int q_failed(lpc_handle *h)
 {
     (void)hipStreamSynchronize(h->stream);
-    if (h->d_qdq.p) (void)hipMemset(h->d_qdq.p, 0xff, h->d_qdq.bytes);
     (void)hipMemset((char *)h->d_acc.p + offsetof(DevAcc, qerr), 0, sizeof(uint32_t));
-    return set_err(h, LPC_E_HIP, "device-side consistency check failed (work queue wait or compaction prefix): "
+    return set_err(h, LPC_E_HIP, "device-side consistency check failed (root-item capacity or compaction prefix): "
                                  "results incomplete");
 }
 
@@ -1006,61 +798,31 @@ static int check_qerr(lpc_handle *h)
     return e ? q_failed(h) : 0;
 }
 
-// The work-queue form of the hierarchy stage: k_roots writes the (packet, piece)
-// items whose root test passes, the persistent k_trav walks them.
+// The root-item form of the hierarchy stage (default): k_roots* write the
+// (packet, piece) items whose root test passes, k_rootwalk walks them grid-stride
+// and hands heavy subtrees to the k_spill levels.
 static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
                      const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
                      unsigned long long *stats)
 {
     const int64_t npk = (n + 63) / 64;
     const int64_t rblocks = (npk + 3) / 4;
-    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 16), pb packets per block
-    // small populations (few packets): more piece classes per packet, so that the
-    // launch has ~roots_tasks waves' worth of tasks instead of a few long loops
-    int rs_S = (int)((pt->npieces + 63) / 64);
+    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 4), pb packets per block
+    const int rs_S = (int)((pt->npieces + 63) / 64);
     const bool roots_s = h->roots_s > 0 && rs_S <= 4;
-    if (roots_s && h->roots_tasks > 0)
-        rs_S = (int)std::max<int64_t>(rs_S, std::min<int64_t>({(h->roots_tasks + npk - 1) / npk,
-                                                                (int64_t)LPC_ROOTS_TASKS, (int64_t)pt->npieces}));
     const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? 1 : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
     const int64_t rs_blocks = roots_s ? (npk + rs_pb - 1) / rs_pb : 0;
-    // packet-range shards (xcd): a shard takes the blocks whose first packet lies in
-    // its eighth of [0, npk), at most npk / 8 + 1 blocks' packets
-    const bool xcd = h->xcd_walk != 0 && h->queue == 2;
-    const int64_t pbmax = std::max<int64_t>(4, rs_pb);
-    const int64_t rcap = std::max({((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
-                                   ((rs_blocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces,
-                                   xcd ? (npk / LPC_Q_CSHARDS + 2 * pbmax) * (int64_t)pt->npieces : (int64_t)0});
-    if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "work queue: too many root items per shard");
+    // per shard: at most its blocks' packets x pieces items (k_roots* flag an
+    // overflow through Q.err instead of dropping items silently)
+    const int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
+                                  ((rs_blocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+    if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "root items: too many per shard");
     RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
-    const size_t dq_bytes = (size_t)LPC_Q_DSHARDS * (size_t)h->q_dcap * 8;
-    if (h->d_qdq.bytes < dq_bytes) {
-        RETIF(dalloc(h, h->d_qdq, dq_bytes));
-        HIPCHK(h, hipMemsetAsync(h->d_qdq.p, 0xff, h->d_qdq.bytes, h->stream));
-    }
     QueueArgs Q;
     Q.roots = (uint64_t *)h->w_qroots.p;
-    Q.dq = (uint64_t *)h->d_qdq.p;
     Q.ctl = (uint32_t *)h->d_misc.p;
     Q.err = (uint32_t *)((char *)h->d_acc.p + offsetof(DevAcc, qerr));
     Q.rcap = (uint32_t)rcap;
-    Q.dcap = (uint32_t)(h->d_qdq.bytes / 8 / LPC_Q_DSHARDS);
-    Q.spin_max = (uint32_t)h->q_spin;
-    Q.batch = h->q_batch;
-    Q.hunger = h->q_hunger;
-    Q.dshard = -1;
-    Q.irec = nullptr;
-    Q.irec_cap = 0;
-    Q.xcd = xcd ? 1 : 0;
-    Q.npk = npk;
-    if (h->prof_items) {              // per-item records of this launch (the last one is kept)
-        const int64_t cap = (int64_t)1 << 21;
-        RETIF(dalloc(h, h->d_wrec, (size_t)cap * 32));
-        HIPCHK(h, hipMemsetAsync(h->d_wrec.p, 0, (size_t)cap * 32, h->stream));
-        h->wrec_count = 2 * cap;      // lpc_prof_waves hands them out as 4-word halves
-        Q.irec = (uint32_t *)h->d_wrec.p;
-        Q.irec_cap = (uint32_t)cap;
-    }
     if (h->host_prof)
         fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d S %d pb %d blocks %lld rcap %lld\n",
                 (long long)n, (long long)npk, (int)pt->npieces, rs_S, rs_pb, (long long)rs_blocks, (long long)rcap);
@@ -1073,75 +835,39 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     else
         hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
-    if (h->fork_pending) {                  // the side stream's fork (run_intersect, LPC_FORK_LATE)
-        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
-        h->fork_pending = false;
-    }
+    RayBase ray;
+    RETIF(ray_base(h, in, rs, n, &ray));
+    SpillArgs SP;
+    RETIF(spill_setup(h, n, &SP));
+    // the grid in waves (LPC_Q_WALK_BLOCKS x 4), single-wave blocks
+    const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4);
+    // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
+    // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
-    if (h->queue == 2) {        // grid-stride walk of the root items, k_spill levels for the rest
-        RayBase ray;
-        RETIF(ray_base(h, in, rs, n, &ray));
-        SpillArgs SP;
-        RETIF(spill_setup(h, n, &SP));
-        // the grid in waves (LPC_Q_WALK_BLOCKS x 4), in blocks of q_walk_wpb waves
-        const int wpb = h->q_walk_wpb;
-        const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4 / wpb);
-        // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
-        // event packets between the kernels
-        if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
-#define LPC_LAUNCH_WALK(WW, PB, NT, PF)                                                                          \
-    hipExtLaunchKernelGGL((k_rootwalk<WW, PB, PF>), dim3(grid), dim3(64 * PB), 0, h->stream, k0, k1, 0, ray, n,    \
-                          perm, (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,   \
-                          scnt, stats, Q, SP)
-        if (stats || Q.irec) {
-            if (h->built_w == 8) { if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8, true); else LPC_LAUNCH_WALK(8, 1, Node8, true); }
-            else { if (wpb == 4) LPC_LAUNCH_WALK(4, 4, Node4, true); else LPC_LAUNCH_WALK(4, 1, Node4, true); }
-        } else {
-            if (h->built_w == 8) {
-                if (wpb == 4) LPC_LAUNCH_WALK(8, 4, Node8, false);
-                else if (h->half_now)             // the half-line cull (LPC_HALF)
-                    hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 6, true>), dim3(grid), dim3(64), 0, h->stream, k0,
-                                          k1, 0, ray, n, perm, (const Node8 *)h->d_nodes.p,
-                                          (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, Q, SP);
-                else if (h->walk_waves == 7)      // launch bounds: waves per SIMD (LPC_WALK_WAVES)
-                    hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 7>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
-                                          ray, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
-                                          eps, max_ray_len, skey, scnt, stats, Q, SP);
-                else if (h->walk_waves == 8)
-                    hipExtLaunchKernelGGL((k_rootwalk<8, 1, false, 8>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0,
-                                          ray, n, perm, (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p,
-                                          eps, max_ray_len, skey, scnt, stats, Q, SP);
-                else LPC_LAUNCH_WALK(8, 1, Node8, false);
-            }
-            else { if (wpb == 4) LPC_LAUNCH_WALK(4, 4, Node4, false); else LPC_LAUNCH_WALK(4, 1, Node4, false); }
-        }
-#undef LPC_LAUNCH_WALK
-        if (h->prof) h->ev_kern.push_back({k0, k1});
-        return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP);
+    if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
+#define LPC_LAUNCH_WALK(WW, NT, PF, HF)                                                                          \
+    hipExtLaunchKernelGGL((k_rootwalk<WW, PF, HF>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,    \
+                          (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,   \
+                          stats, Q, SP)
+    if (h->built_w == 8) {
+        if (stats) LPC_LAUNCH_WALK(8, Node8, true, false);
+        else if (h->half_now) LPC_LAUNCH_WALK(8, Node8, false, true);        // the half-line cull (LPC_HALF 1/2)
+        else LPC_LAUNCH_WALK(8, Node8, false, false);
+    } else {
+        if (stats) LPC_LAUNCH_WALK(4, Node4, true, false);
+        else LPC_LAUNCH_WALK(4, Node4, false, false);
     }
-    unsigned grid = 0;
-    if (h->built_w == 8) RETIF(q_grid<8>(h, &grid));
-    else RETIF(q_grid<4>(h, &grid));
-    if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
-    if (h->built_w == 8)
-        hipLaunchKernelGGL((k_trav<8, 1>), dim3(grid), dim3(64), 0, h->stream, in, rs, n, perm,
-                           (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
-                           stats, Q);
-    else
-        hipLaunchKernelGGL((k_trav<4, 1>), dim3(grid), dim3(64), 0, h->stream, in, rs, n, perm,
-                           (const Node4 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
-                           stats, Q);
-    if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
-    HIPCHK(h, hipGetLastError());
-    return 0;
+#undef LPC_LAUNCH_WALK
+    if (h->prof) h->ev_kern.push_back({k0, k1});
+    return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP);
 }
 
 // intersect for n rays of `in` into the slot arrays, and optionally into a
 // caller's [ray][mesh] buffers (st_user != NULL, the reference's scratch layout).
-// split: rows [0, split) of `in` are a population's reflected block (key class
-// bit, k_raykey); INT64_MAX when the rows are not a trace population.
+// traced != NULL (trace iterations without per-ray exports): the launch works in
+// its coherence order and *traced receives the rays in that order.
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
-                         float *st_user, int32_t *si_user, int32_t *sc_user, int64_t split = INT64_MAX,
+                         float *st_user, int32_t *si_user, int32_t *sc_user,
                          double dmax2 = INFINITY, RaysIn *traced = nullptr)
 {
     RETIF(ensure_ws(h, n));
@@ -1158,25 +884,25 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     SI.m_total = (unsigned long long)h->acc_pending_total;
     SI.uniform = 0;
     h->acc_pending = false;
-    // traced mode (trace_iterate without per-ray exports): the slots, shading and
-    // compaction work in the launch's coherence order, so the children come out
-    // in their parents' traced order and need no sort of their own (unless
-    // LPC_TRACED_SORT); *traced receives the rays in that order
-    const bool chained_pop = traced && h->pop_traced && !h->traced_resort;
+    // traced mode: the children come out in their parents' traced order and need
+    // no sort of their own
+    const bool chained_pop = traced && h->pop_traced;
     const bool sorted = h->sort_rays && n >= h->sort_min && !chained_pop;
     // the slot reset rides on k_raykey when it runs before everything that reads misc
-    const bool fold_init = sorted && h->sort_mode == 1 && n >= LPC_MISC_WORDS &&
-                           !(h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX)) &&
-                           !(h->order_ready && n == h->order_n);
+    const bool fold_init = sorted && n >= LPC_MISC_WORDS;
     // Traced single-chunk iterations (k_shade_stage) leave every slot they read in
     // the clean state (max_ray_len, idx -1, count 0), so once the whole slot array
     // is clean no slot needs a reset; only the launch words do (k_stage_move
     // reset them for the next launch; the emitted rays' k_raykey does).
     // LPC_HALF 1 / 2: every node test (not for the emitted rays / for all); 3 / 4:
-    // the piece roots only (k_roots items), not for the emitted rays / for all
-    const bool emitted = traced && h->pop_emitted;
-    h->half_now = h->half == 2 || (h->half == 1 && !emitted);
-    h->half_roots = h->half_now || h->half == 4 || (h->half == 3 && !emitted);
+    // the piece roots only (k_roots items), not for the emitted rays / for all.
+    // "Emitted" = the trace's first population, whatever the export mode; the
+    // drop-in kernels (lpc_intersect, lpc_bounce_host: traced == NULL, no trace
+    // population) are never culled.
+    const bool in_trace = h->in_trace;
+    const bool emitted = h->pop_emitted;
+    h->half_now = in_trace && (h->half == 2 || (h->half == 1 && !emitted));
+    h->half_roots = in_trace && (h->half_now || h->half == 4 || (h->half == 3 && !emitted));
     const bool restore = traced && h->fuse_compact;
     const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
     const bool misc_clean = restore && h->misc_clean;
@@ -1203,70 +929,30 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (h->host_prof && h->t_first == 0.0) h->t_first = host_us();
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
-    const bool chained = !traced && h->order_ready && n == h->order_n;
-    h->order_ready = false;
-    if (chained) {                      // the previous iteration wrote this order (k_oscatter)
-        perm = (const int32_t *)h->w_perm2[h->order_buf].p;
-        rs = (const float *)h->w_rs2[h->order_buf].p;
-    } else if (sorted) {
+    if (sorted) {
         // coherence order: rays of one wave share origin cell and direction
+        // (key [scene-box origin cell | direction], k_raykey), gathered from the
+        // 32-byte rows k_raykey wrote
         const size_t C = (size_t)h->ws_rays;
         uint32_t *kin = (uint32_t *)h->w_sort.p, *kout = kin + C;
         int32_t *vin = (int32_t *)(kout + C), *vout = vin + C;
-        // key_mode: 0 [scene-box origin cell | direction], 1 population origin box,
-        // 2 = 1 + refracted-block bit, 3 [direction | scene-box origin cell],
-        // 4 = 3 + refracted-block bit
-        // 5: population box for populations that are not a trace's children (the
-        // emitted rays: a collimated beam gets fine origin cells), scene box after
-        const bool pop_box = h->key_mode == 1 || h->key_mode == 2 || (h->key_mode == 5 && split == INT64_MAX);
-        const bool cls = h->key_mode == 2 || h->key_mode == 4;
-        if (h->sort_mode == 2) {
-            // adaptive 16-bit key: 3 small kernels + a 2-pass radix sort
-            const int64_t nb = (n + 255) / 256;
-            unsigned long long *part = (unsigned long long *)h->w_keypart.p;
-            int32_t *sel = (int32_t *)((char *)h->w_keypart.p + (size_t)nb * 16);
-            const float f8 = 8.0f;     // box_scale is for 32 cells per axis
-            hipLaunchKernelGGL(k_raykey16a, dim3((unsigned)nb), dim3(256), 0, h->stream, in, n, h->box_lo[0],
-                               h->box_lo[1], h->box_lo[2], h->box_scale[0] * f8, h->box_scale[1] * f8,
-                               h->box_scale[2] * f8, (float4 *)h->w_aos.p, part);
-            hipLaunchKernelGGL(k_keymask, dim3(1), dim3(1024), 0, h->stream, (const unsigned long long *)part, nb, sel);
-            hipLaunchKernelGGL(k_keypack, dim3((unsigned)nb), dim3(256), 0, h->stream, in, n, h->box_lo[0],
-                               h->box_lo[1], h->box_lo[2], h->box_scale[0] * f8, h->box_scale[1] * f8,
-                               h->box_scale[2] * f8, (const int32_t *)sel, kin, vin);
-            size_t tb = h->sort_tmp_bytes;
-            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
-                                                              0, 16, h->stream));
-            perm = vout;
-            hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
-                               perm, (float *)h->w_rs.p, traced ? 1 : 0);
-            rs = (const float *)h->w_rs.p;
-        } else {
-        if (pop_box)
-            hipLaunchKernelGGL(k_bbox, dim3((unsigned)std::min<int64_t>(grid1(n), 256)), dim3(256), 0, h->stream,
-                               in, n, misc);
-        // the emitted rays' varying key bits (set_rays) under key mode 0
+        // the emitted rays' varying key bits (set_rays)
         int b0 = 0, b1 = 32;
-        if (traced && h->pop_emitted && h->key_mode == 0 && !cls) { b0 = h->init_key_lo; b1 = h->init_key_hi; }
+        if (traced && h->pop_emitted) { b0 = h->init_key_lo; b1 = h->init_key_hi; }
         hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
-                           h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2],
-                           pop_box ? (const uint32_t *)misc : nullptr, cls ? split : (int64_t)INT64_MAX,
-                           (h->key_mode == 3 || h->key_mode == 4) ? 1 : 0, kin, vin,
-                           (h->gather_aos || traced) ? (float4 *)h->w_aos.p : nullptr, SIk);
+                           h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
+                           (float4 *)h->w_aos.p, SIk);
         size_t tb = h->sort_tmp_bytes;
         if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
-            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg16>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
-                                                              b0, b1, h->stream));
+            HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
+                                                                 (size_t)n, b0, b1, h->stream));
         else
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, b0,
                                                             b1, h->stream));
         perm = vout;
-        if (h->gather_aos || traced)
-            hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
-                               perm, (float *)h->w_rs.p, traced ? 1 : 0);
-        else
-            hipLaunchKernelGGL(k_gather, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, perm, (float *)h->w_rs.p);
+        hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
+                           perm, (float *)h->w_rs.p, traced ? 1 : 0);
         rs = (const float *)h->w_rs.p;
-        }
     }
     if (traced) {
         // positions of the coherence order are the rays' indices from here on
@@ -1281,7 +967,6 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         }
         perm = nullptr;
     }
-    h->last_perm = perm;
     unsigned long long *stats = h->prof_stats ? (unsigned long long *)h->d_stats.p : nullptr;
     // sliver pieces the launch's rays can reach: dmin <= max |D| (sliver_dmin)
     if (!(dmax2 >= 0.0)) dmax2 = INFINITY;          // NaN bound (a NaN direction): no culling
@@ -1293,77 +978,49 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // add to the slots with order-independent atomics); joined at the end
     hipStream_t ss = h->stream;
     const bool side = nsp > 0 && h->stream2 && h->ev_side[0];
-    // the fork event: recorded here, or (LPC_FORK_LATE, work-queue path with late
-    // slivers) right after k_roots, so the marker's fence does not sit between the
-    // previous iteration's compaction and the root tests
-    bool fork_pending = false;
     if (side) {
         ss = h->stream2;
-        fork_pending = h->fork_late && h->sliver_late && h->queue == 2;
-        if (!fork_pending) HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
     }
-    h->fork_pending = fork_pending;
     // on the side stream the sliver kernels are launched after the hierarchy
     // stage's (the host reaches k_roots / k_rootwalk sooner; the slivers still
     // run beside k_rootwalk)
     auto launch_slivers = [&]() -> int {
-    if (side && h->fork_pending) {          // no k_roots launched (no pieces): record it now
-        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
-        h->fork_pending = false;
-    }
-    if (side) HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
-    if (nsp > 0) {
-        // packets per wave: enough (packet, piece) waves to fill the GPU, no more
-        const int rpl = h->sliver_rays == 64 ? 1 : 2;
-        const int64_t npkx = (n + 64 * rpl - 1) / (64 * rpl);
-        const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
-                                              : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
-        const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
-        if (rpl == 1) {
-            hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
-                               (PacketRec *)h->w_pk64.p);
-            hipLaunchKernelGGL(k_slivers1, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk64.p,
-                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw, dmax_k);
-        } else {
+        if (side) HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
+        if (nsp > 0) {
+            // packets per wave: enough (packet, piece) waves to fill the GPU, no more
+            const int64_t npkx = (n + 127) / 128;
+            const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
+                                                  : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
+            const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
             hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
                                (PacketRec *)h->w_pk.p);
             hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
                                (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
                                scnt, stats, (int)ppw, dmax_k);
+            HIPCHK(h, hipGetLastError());
         }
-        HIPCHK(h, hipGetLastError());
-    }
-    if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
-    return 0;
+        if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
+        return 0;
     };
     const bool late = side && h->sliver_late;
     if (!late) RETIF(launch_slivers());
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-    const bool lane_path = h->lane_max > 0 && n <= h->lane_max && h->lane_ok && pt->gmax == 0 && !h->prof_waves;
-    // work queue (default): needs no fan groups and the item encoding's bounds
+    // root items (default): the item encoding's bounds
     bool qpath = false;
-    if (h->queue && !h->prof_waves && !lane_path) {
+    if (h->queue == 2 && !h->prof_waves) {
         PieceTable *ptq;
         RETIF(piece_table(h, n, &ptq, q_level(h, n)));
-        qpath = ptq->gmax == 0 && (n + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
-                (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES && h->K <= LPC_Q_MAX_SLOTS;
+        qpath = (n + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS && (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES &&
+                h->K <= LPC_Q_MAX_SLOTS;
         if (qpath) {
             pt = ptq;                   // same sliver pieces at every level
             if (pt->npieces > 0) RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats));
         }
     }
-    if (pt->npieces > 0 && lane_path) {
-        // incoherent (small) populations: one ray per lane, threaded traversal
-        PieceTable *pl;
-        RETIF(piece_table(h, n, &pl, (int32_t)h->lane_g));
-        hipLaunchKernelGGL(k_lane, dim3((unsigned)((n + 255) / 256), (unsigned)pl->npieces), dim3(256), 0, h->stream,
-                           in, rs, n, perm, (const LaneEntry *)h->d_lane.p, (const ExactRec *)h->d_xrec.p,
-                           (const Piece *)pl->pieces.p, eps, max_ray_len, skey, scnt);
-        HIPCHK(h, hipGetLastError());
-    }
-    if (pt->npieces > 0 && !lane_path && !qpath) {
+    if (pt->npieces > 0 && !qpath) {
+        // k_intersect: one wave per (packet, piece) (LPC_QUEUE=0, per-wave records)
         uint32_t *wrec = nullptr;
         if (h->prof_waves) {
             h->wrec_count = (int64_t)pt->npieces * ((n + 63) / 64);
@@ -1371,58 +1028,29 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             HIPCHK(h, hipMemsetAsync(h->d_wrec.p, 0, (size_t)h->wrec_count * 16, h->stream));
             wrec = (uint32_t *)h->d_wrec.p;
         }
-        const int64_t npk = (n + 63) / 64;
-        const int gmax = pt->gmax;
-        GItem *gitems = nullptr;
-        int32_t *gcount = nullptr;
-        if (gmax > 0) {               // fan-group item slots: one list per (piece, packet) wave
-            RETIF(dalloc(h, h->w_gcount, (size_t)pt->npieces * npk * 4));
-            RETIF(dalloc(h, h->w_gitems, (size_t)pt->npieces * npk * gmax * sizeof(GItem)));
-            gitems = (GItem *)h->w_gitems.p;
-            gcount = (int32_t *)h->w_gcount.p;
-        }
-        // work hand-over (not with fan groups: a k_spill item has no group slots)
         SpillArgs SP{nullptr, nullptr, 0u, 0, 31};
-        if (gmax == 0 && !wrec) RETIF(spill_setup(h, n, &SP));
-        // pieces per wave: all of them (LPC_LOOP) or enough that the grid has
-        // about wave_target waves
+        if (!wrec) RETIF(spill_setup(h, n, &SP));
+        // pieces per wave: enough that the grid has about wave_target waves
         const int64_t bxw = (n + 255) / 256;
         int pgroup = 1;
-        if (h->piece_loop && (n + 63) / 64 >= h->loop_min_packets) pgroup = pt->npieces;
-        else if (h->wave_target > 0)
-            pgroup = (int)std::max<int64_t>(1, (4 * bxw * pt->npieces) / h->wave_target);
+        if (h->wave_target > 0) pgroup = (int)std::max<int64_t>(1, (4 * bxw * pt->npieces) / h->wave_target);
         pgroup = std::max(1, std::min(pgroup, (int)pt->npieces));
         const int rows = (pt->npieces + pgroup - 1) / pgroup;
-        const int xrows = (h->xcd_min_rows > 0 && rows >= h->xcd_min_rows) ? rows : 0;
-        const dim3 grid((unsigned)bxw, (unsigned)(xrows ? (rows + 7) / 8 * 8 : rows));
+        const dim3 grid((unsigned)bxw, (unsigned)rows);
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
-#define LPC_LAUNCH_ISECT(WW, MB)                                                                               \
-    hipLaunchKernelGGL((k_intersect<WW, MB>), grid, dim3(256), 0, h->stream, in, rs, n, perm,                       \
-                       (const NodeW<WW> *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, gitems, gcount, gmax,        \
-                       (const Piece *)pt->pieces.p, eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup,         \
-                       (int)pt->npieces, xrows)
-        if (h->built_w == 8) {
-            if (h->isect_minb == 6) LPC_LAUNCH_ISECT(8, 6);
-            else LPC_LAUNCH_ISECT(8, 1);
-        } else {
-            if (h->isect_minb == 6) LPC_LAUNCH_ISECT(4, 6);
-            else LPC_LAUNCH_ISECT(4, 1);
-        }
+#define LPC_LAUNCH_ISECT(WW)                                                                                   \
+    hipLaunchKernelGGL((k_intersect<WW>), grid, dim3(256), 0, h->stream, in, rs, n, perm,                           \
+                       (const NodeW<WW> *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, (const Piece *)pt->pieces.p, \
+                       eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup, (int)pt->npieces)
+        if (h->built_w == 8) LPC_LAUNCH_ISECT(8);
+        else LPC_LAUNCH_ISECT(4);
 #undef LPC_LAUNCH_ISECT
         if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
         RETIF(run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP));
-        if (gmax > 0) {
-            hipLaunchKernelGGL(k_packet<1>, dim3((unsigned)((npk + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
-                               (PacketRec *)h->w_pk64.p);
-            hipLaunchKernelGGL(k_groups, dim3((unsigned)bxw, (unsigned)pt->npieces), dim3(256), 0, h->stream, in, rs, n, perm, (const FiltRec *)h->d_grec.p,
-                               (const ExactRec *)h->d_gxrec.p, (const PacketRec *)h->w_pk64.p,
-                               (const Piece *)pt->pieces.p, (const GItem *)gitems, (const int32_t *)gcount, gmax,
-                               eps, max_ray_len, skey, scnt);
-        }
         HIPCHK(h, hipGetLastError());
     }
-    if (h->prof) {      // the intersect stage: k_intersect (+ k_packet, k_slivers)
+    if (h->prof) {      // the intersect stage: the walk (+ k_packet, k_slivers)
         if (!h->prof_light) {
             (void)hipEventRecord(e1, h->stream);
             h->ev_isect.push_back({e0, e1});
@@ -1452,7 +1080,6 @@ static ShadeArgs shade_args(lpc_handle *h, const RaysIn &in, const int32_t *meas
     A.verts = (const float *)h->d_verts.p;
     A.max_ray_len = max_ray_len; A.ior_env = ior_env;
     A.o = shade_ptrs(h, extra);
-    A.cfirst = 0;
     return A;
 }
 
@@ -1467,7 +1094,6 @@ static int run_shade(lpc_handle *h, const RaysIn &in, const int32_t *meas_in, in
     A.verts = (const float *)h->d_verts.p;
     A.max_ray_len = max_ray_len; A.ior_env = ior_env;
     A.o = shade_ptrs(h, extra);
-    A.cfirst = 0;                           // slots may hold the reference's non-uniform initial state
     LPC_KU_LAUNCH(h, k_shade, dim3(grid1(n)), dim3(256), h->stream, A);
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -1532,31 +1158,17 @@ int lpc_open(int device, lpc_handle **out)
         const char *v = getenv(k);
         return (v && *v) ? strtoll(v, nullptr, 10) : dflt;
     };
-    h->key_mode = (int)env_int("LPC_KEY", h->key_mode);
     h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
-    h->sort_mode = env_int("LPC_SORT", h->sort_mode) == 2 ? 2 : 1;
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
-    h->fuse_shade = env_int("LPC_FUSE_SHADE", h->fuse_shade) != 0;
     h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
     h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
-    h->walk_waves = (int)std::min<int64_t>(8, std::max<int64_t>(6, env_int("LPC_WALK_WAVES", h->walk_waves)));
     h->half = (int)env_int("LPC_HALF", h->half);
-    h->xcd_min_rows = (int)env_int("LPC_XCD_ROWS", h->xcd_min_rows);
-    h->order_chain = env_int("LPC_CHAIN", h->order_chain) != 0;
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
-    h->gather_aos = env_int("LPC_GATHER_AOS", h->gather_aos) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
-    h->shade_cfirst = (int)env_int("LPC_SHADE_CFIRST", h->shade_cfirst);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
-    h->xcd_walk = (int)env_int("LPC_XCD_WALK", h->xcd_walk);
-    h->roots_tasks = env_int("LPC_ROOTS_TASKS", h->roots_tasks);
-    h->lane_max = env_int("LPC_LANE_MAX", h->lane_max);
-    h->lane_g = std::max<int64_t>(1, env_int("LPC_LANE_G", h->lane_g));
-    h->isect_minb = env_int("LPC_ISECT_MINB", h->isect_minb) == 1 ? 1 : 6;
-    if (const char *v = getenv("LPC_FLAT")) h->flat_ratio = atof(v);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
     h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
@@ -1568,38 +1180,22 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_shrink = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_int("LPC_SPILL_SHRINK", h->spill_shrink)));
     h->spill_min_blocks = std::max<int64_t>(1, env_int("LPC_SPILL_MIN_BLOCKS", h->spill_min_blocks));
     h->spill_pair_shift = (int)std::min<int64_t>(31, std::max<int64_t>(0, env_int("LPC_PAIR_SHIFT", h->spill_pair_shift)));
-    h->piece_loop = env_int("LPC_LOOP", h->piece_loop) != 0;
-    h->loop_min_packets = env_int("LPC_LOOP_MIN", h->loop_min_packets);
     h->wave_target = env_int("LPC_WAVE_TARGET", h->wave_target);
     h->node_w = env_int("LPC_NODE_W", h->node_w) == 4 ? 4 : 8;
     h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
     h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
-    h->sliver_rays = env_int("LPC_SLIVER_RAYS", h->sliver_rays) == 64 ? 64 : 128;
-    h->queue = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_QUEUE", h->queue)));
+    h->queue = env_int("LPC_QUEUE", h->queue) == 0 ? 0 : 2;
     h->traced = env_int("LPC_TRACED", h->traced) != 0;
-    h->traced_resort = env_int("LPC_TRACED_SORT", h->traced_resort) != 0;
-    h->q_walk_blocks = env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks);
-    h->q_walk_wpb = env_int("LPC_Q_WALK_WPB", h->q_walk_wpb) == 4 ? 4 : 1;
-    h->spill_wpb = env_int("LPC_SPILL_WPB", h->spill_wpb) == 4 ? 4 : 1;
+    h->q_walk_blocks = std::max<int64_t>(1, env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks));
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
     }
     h->q_target = std::max<int64_t>(1, env_int("LPC_Q_TARGET", h->q_target));
-    h->q_batch = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_int("LPC_Q_BATCH", h->q_batch)));
-    h->q_hunger = env_int("LPC_Q_HUNGER", h->q_hunger) != 0;
-    h->q_blocks = std::max<int64_t>(0, env_int("LPC_Q_BLOCKS", h->q_blocks));
-    h->q_per_cu = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_int("LPC_Q_PER_CU", h->q_per_cu)));
-    h->q_dcap = std::min<int64_t>((int64_t)1 << 26, std::max<int64_t>(64, env_int("LPC_Q_DCAP", h->q_dcap)));
-    h->q_spin = std::min<int64_t>(0xffffffffLL, std::max<int64_t>(1024, env_int("LPC_Q_SPIN", h->q_spin)));
     h->early_acc = env_int("LPC_EARLY_ACC", h->early_acc) != 0;
     h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
-    h->ev_sysfence = env_int("LPC_EV_SYSFENCE", 1) != 0;
-    h->fork_late = env_int("LPC_FORK_LATE", 0) != 0;
     if (env_int("LPC_SIDE_STREAM", 1) != 0) {
-        // the side stream's join events (LPC_EV_SYSFENCE=0: device-scope release only,
-        // measured 4-8 % slower per step)
-        const unsigned evf = hipEventDisableTiming | (h->ev_sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
+        const unsigned evf = hipEventDisableTiming;   // the side stream's fork / join events
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
@@ -1634,8 +1230,8 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->w_pk64, &h->w_gitems, &h->w_gcount, &h->d_misc, &h->d_wrec, &h->d_grec, &h->d_gxrec, &h->w_spill, &h->w_qroots, &h->d_qdq, &h->w_aos, &h->d_lane, &h->w_keypart, &h->w_chR, &h->w_chT, &h->w_oblk,
-                    &h->w_perm2[0], &h->w_perm2[1], &h->w_rs2[0], &h->w_rs2[1], &h->w_fc, &h->d_mrun, &h->w_gsum};
+                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->d_misc, &h->d_wrec, &h->w_spill, &h->w_qroots,
+                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1671,8 +1267,8 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     if (tri_count <= 0 || mesh_count <= 0 || !v0 || !v1 || !v2 || !mesh_id || !mat_type || !ior ||
         !refl || !diss)
         return set_err(h, LPC_E_ARG, "scene needs >= 1 triangle, >= 1 mesh and all tables");
-    if (tri_count >= (1 << 30) - 1)   // child refs: ~idx above LPC_GROUP_REF
-        return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^30 - 2)");
+    if (tri_count >= (1 << 28) - 1)   // root items encode node ids in 28 bits (LPC_Q_MAX_NODES)
+        return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^28 - 2)");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const int32_t M = tri_count, K = mesh_count;
@@ -1824,7 +1420,7 @@ int lpc_bounce_host(lpc_handle *h, int64_t n, const float *origin4, const float 
         rc = upload_rays(h, P, nc, origin4 + 4 * base, dir4 + 4 * base, pow + base, prev_mid + base);
         if (rc) break;
         if (hipMemcpy(dmeas.p, meas + base, (size_t)nc * 4, hipMemcpyHostToDevice) != hipSuccess) { rc = set_err(h, LPC_E_HIP, "meas upload"); break; }
-        rc = run_intersect(h, P.in(), nc, max_ray_len, nullptr, nullptr, nullptr, INT64_MAX, bdmax2);
+        rc = run_intersect(h, P.in(), nc, max_ray_len, nullptr, nullptr, nullptr, bdmax2);
         if (!rc) rc = run_shade(h, P.in(), (const int32_t *)dmeas.p, nc, max_ray_len, ior_env, true);
         if (rc) break;
         ShadeOutPtrs o = shade_ptrs(h, true);
@@ -2028,8 +1624,6 @@ int lpc_trace_reset(lpc_handle *h)
     h->n_cur = h->n_init;
     h->pop_traced = false;
     h->pop_emitted = true;
-    h->order_ready = h->order_pending = false;
-    h->split = INT64_MAX;                       // emitted rays: one class
     h->pop_dmax2 = h->init_dmax2;
     h->m_total = 0;                             // measured record emptied (the first iteration resets the counters)
     return 0;
@@ -2234,12 +1828,11 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     // traced mode: one chunk, no per-ray export (the population then comes out in
     // its parents' coherence order; measured rays per iteration likewise)
     const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow;
-    const bool traced = h->traced && C >= N && !exports && !h->order_chain;
+    const bool traced = h->traced && C >= N && !exports;
     // the counters come back through the mapped host copy k_scan writes, so the
     // host decides and launches the next iteration while k_scatter still runs
     // (profiling: only the light level, whose events end before k_scan)
-    const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && (!h->prof || h->prof_light) &&
-                       !h->order_chain;
+    const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && (!h->prof || h->prof_light);
     if (early) ++h->acc_seq;
     // traced single chunk: k_shade_stage + k_stage_move
     const bool fused = traced && h->fuse_compact && C >= N;
@@ -2247,10 +1840,12 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         RaysIn in = (h->pop_init ? h->I : h->A).in(base);
-        const int64_t split = h->split == INT64_MAX ? INT64_MAX : std::max<int64_t>(0, h->split - base);
         RaysIn tin;
-        RETIF(run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, split, h->pop_dmax2,
-                            traced ? &tin : nullptr));
+        h->in_trace = true;
+        const int rc_i = run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, h->pop_dmax2,
+                                       traced ? &tin : nullptr);
+        h->in_trace = false;
+        RETIF(rc_i);
         if (traced) in = tin;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
@@ -2266,19 +1861,11 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         A.mm = (int32_t *)(mf + 4 * mc);
         A.host_acc = early ? h->acc_map_dev : nullptr;
         A.seq = h->acc_seq;
-        const bool chain = h->order_chain && A.direct_t && h->last_perm != nullptr;
-        A.childR = A.childT = nullptr;
-        if (chain) {
-            RETIF(dalloc(h, h->w_chR, (size_t)nc * 4));
-            RETIF(dalloc(h, h->w_chT, (size_t)nc * 4));
-            A.childR = (int32_t *)h->w_chR.p; A.childT = (int32_t *)h->w_chT.p;
-        }
         if (fused) {                  // shade + staged compaction, two kernels (k_shade_stage, k_stage_move)
             const int64_t nt = (nc + LPC_ST_TILE - 1) / LPC_ST_TILE;
             const size_t Cs = (size_t)h->ws_rays;
             StageArgs G;
             G.S = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
-            G.S.cfirst = h->shade_cfirst ? 1 : 0;        // the slots start uniform-clean here
             G.stR = (float *)h->w_shf.p;                // the 20 shade-output arrays hold the staging rows
             G.stT = (float *)h->w_shi.p;
             G.stM = (float *)h->w_soa.p;
@@ -2327,14 +1914,8 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             if (h->prof && !h->prof_light) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
             continue;
         }
-        if (h->fuse_shade) {          // postproc + Fresnel + the tile counts in one pass
-            const ShadeArgs SA = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
-            hipLaunchKernelGGL(k_shade_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, SA, A);
-            HIPCHK(h, hipGetLastError());
-        } else {
-            RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
-            hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
-        }
+        RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
+        hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         if (out_origin4 || out_dest4 || out_pow || out_meas) {
             // the copies below run on the null stream: the shading on h->stream first
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2353,26 +1934,6 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, h->stream, A);
         hipLaunchKernelGGL(k_scatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
         HIPCHK(h, hipGetLastError());
-        if (chain) {                    // the next population's order: children in their parents' order
-            const int tgt = (h->last_perm == (const int32_t *)h->w_perm2[0].p) ? 1 : 0;
-            RETIF(dalloc(h, h->w_perm2[tgt], (size_t)2 * N * 4));
-            RETIF(dalloc(h, h->w_rs2[tgt], (size_t)2 * N * 6 * 4));
-            RETIF(dalloc(h, h->w_oblk, (size_t)2 * A.nb * 4 + 64));
-            OrderArgs Ob;
-            Ob.n = nc; Ob.nb = A.nb; Ob.perm = h->last_perm;
-            Ob.childR = A.childR; Ob.childT = A.childT; Ob.o = o;
-            Ob.blk = (int32_t *)h->w_oblk.p;
-            Ob.totR = (long long *)((char *)h->w_oblk.p + (size_t)2 * A.nb * 4 + 8 - ((size_t)2 * A.nb * 4) % 8);
-            Ob.acc = (const DevAcc *)h->d_acc.p;
-            Ob.perm_next = (int32_t *)h->w_perm2[tgt].p;
-            Ob.rs_next = (float *)h->w_rs2[tgt].p;
-            hipLaunchKernelGGL(k_ocount, dim3((unsigned)A.nb), dim3(256), 0, h->stream, Ob);
-            hipLaunchKernelGGL(k_oscan, dim3(1), dim3(1024), 0, h->stream, Ob);
-            hipLaunchKernelGGL(k_oscatter, dim3((unsigned)A.nb), dim3(256), 0, h->stream, Ob);
-            HIPCHK(h, hipGetLastError());
-            h->order_buf = tgt;
-            h->order_pending = true;
-        }
         if (h->prof && !h->prof_light) { (void)hipEventRecord(e1, h->stream); h->ev_rest.push_back({e0, e1}); }
     }
     // refracted block after the reflected one (k_append reads the counts on the
@@ -2411,10 +1972,6 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     h->pop_traced = traced;
     h->pop_emitted = false;
     h->n_cur = nR + nT;
-    h->order_ready = h->order_pending;
-    h->order_pending = false;
-    h->order_n = nR + nT;
-    h->split = nR;
     h->m_total = (int64_t)acc.m_total;
     // the running per-mesh measured power stays valid while every iteration sums it
     h->mp_valid = h->mp_valid && mp_fused;
@@ -2556,7 +2113,6 @@ int lpc_prof_enable(lpc_handle *h, int on)
     h->prof_stats = on == 2;
     h->prof_waves = on == 3;
     h->prof_light = on == 4;                        // k_intersect events only (bench timed region)
-    h->prof_items = on == 5;                        // k_trav per-item records (lpc_prof_waves, 8 words each)
     if (h->prof_stats && !h->d_stats.p) {
         RETIF(dalloc(h, h->d_stats, LPC_STATS_WORDS * 8));
         HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));

@@ -274,8 +274,8 @@ class Engine:
         return (H, xe, ye) if not want_xy else (H, xe, ye, x, y, pc)
 
     # -- profiling -------------------------------------------------------------
-    def prof_enable(self, on=True, counters=False, waves=False, light=False, items=False):
-        level = (5 if items else 4 if light else 3 if waves else 2 if counters else 1) if on else 0
+    def prof_enable(self, on=True, counters=False, waves=False, light=False):
+        level = (4 if light else 3 if waves else 2 if counters else 1) if on else 0
         self._c(self.L.lpc_prof_enable(self.h, level))
 
     def prof_waves(self):
@@ -287,14 +287,6 @@ class Engine:
         if c.value:
             self._c(self.L.lpc_prof_waves(self.h, ptr(rec), c.value, ctypes.byref(c)))
         return rec
-
-    def prof_items(self):
-        """Per-item records of the last work-queue launch (prof level 5): uint32
-        (count, 8) = walk ticks (100 MHz), nodes, exact tests, slot, claim time
-        and walk start (low 32 bits of the 100 MHz clock), HW_ID, XCC_ID | phase << 8
-        (phase 1 root item, 2 handed over)."""
-        r = self.prof_waves().reshape(-1, 8)
-        return r[r[:, 7] != 0] if len(r) else r
 
     def prof_read(self, reset=True):
         p = _lib.Prof()

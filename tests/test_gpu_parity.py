@@ -73,46 +73,32 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, name, n):
 
 
 _OLD = dict(LPC_QUEUE="0")          # k_intersect + k_spill levels instead of the root items
-_TRAV = dict(LPC_QUEUE="1")         # the persistent work-queue kernel
 _POLICIES = [
-    # both paths
-    dict(LPC_FLAT="0"), dict(LPC_KEY="3"), dict(LPC_KEY="1"), dict(LPC_SORT="0"), dict(LPC_SORT="2"),
-    dict(LPC_GATHER_AOS="0"), dict(LPC_SLIVER_CULL="0"), dict(LPC_FUSE_SHADE="1"), dict(LPC_CHAIN="1"),
-    dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_SLIVER_RAYS="64"), dict(LPC_NODE_W="4"),
-    # root items walked by k_rootwalk (default): piece level, grid, block shape
+    # coherence sort off / onesweep at every size, sliver culling off, packets per sliver wave
+    dict(LPC_SORT="0"), dict(LPC_ONESWEEP_MIN="0"), dict(LPC_SLIVER_CULL="0"),
+    dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_NODE_W="4"),
+    # root items walked by k_rootwalk (default): piece level, grid, root-test kernels
     dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"), dict(LPC_Q_WALK_BLOCKS="1"),
-    dict(LPC_Q_WALK_WPB="4", LPC_SPILL_WPB="4"), dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"),
-    dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_WALK_WAVES="7"), dict(LPC_SHADE_KU="0"), dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
-    dict(LPC_XCD_WALK="1"), dict(LPC_XCD_WALK="1", LPC_Q_WALK_BLOCKS="2"), dict(LPC_XCD_WALK="1", LPC_Q_WALK_BLOCKS="3"),
-    dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_EV_SYSFENCE="0"), dict(LPC_FORK_LATE="1"), dict(LPC_SHADE_CFIRST="1"),
-    dict(LPC_ROOTS_TASKS="0"), dict(LPC_ROOTS_TASKS="100000000"), dict(LPC_ROOTS_TASKS="1000000", LPC_Q_TARGET="1"),
-    dict(LPC_XCD_WALK="1", LPC_ROOTS_S="0", LPC_Q_TARGET="10000000"), dict(LPC_XCD_WALK="1", LPC_ROOTS_S="0"),
-    # persistent work queue (k_roots + k_trav): claim batch, piece level, hand-over
-    # queue that overflows, grids of one block, of a few blocks and far beyond residency
-    dict(_TRAV, LPC_Q_BATCH="1"), dict(_TRAV, LPC_Q_BATCH="7"), dict(_TRAV, LPC_Q_TARGET="1"),
-    dict(_TRAV, LPC_Q_TARGET="10000000"), dict(_TRAV, LPC_Q_DCAP="64"), dict(_TRAV, LPC_Q_BLOCKS="1"),
-    dict(_TRAV, LPC_Q_BLOCKS="3", LPC_Q_DCAP="64"), dict(_TRAV, LPC_Q_BLOCKS="20000"),
-    dict(_TRAV, LPC_Q_BLOCKS="37", LPC_Q_BATCH="3", LPC_NODE_W="4"), dict(_TRAV, LPC_Q_HUNGER="0"),
-    # fan groups fall back to k_intersect
-    dict(LPC_FLAT="1.5", LPC_TARGET_BLOCKS="65536"), dict(LPC_FLAT="20", LPC_KEY="2"),
-    # the k_intersect path's own knobs
-    dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"), dict(_OLD, LPC_ISECT_MINB="1"),
-    dict(_OLD, LPC_XCD_ROWS="1"), dict(_OLD, LPC_XCD_ROWS="1", LPC_WAVE_TARGET="0"),
-    dict(LPC_LANE_MAX="100000000"), dict(LPC_LANE_MAX="100000000", LPC_LANE_G="8"),
-    dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="4"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
-    dict(_OLD, LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
-    dict(_OLD, LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"),
-    dict(_OLD, LPC_LOOP="1", LPC_LOOP_MIN="1"), dict(_OLD, LPC_LOOP="1", LPC_BUDGET="8", LPC_TARGET_BLOCKS="1"),
+    dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"), dict(LPC_SLIVER_LATE="0"),
+    dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_SHADE_KU="0"),
+    dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
+    # work hand-over: budgets, a queue that overflows
+    dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_BUDGET="0"),
+    dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
+    dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"),
+    dict(LPC_LARGE_N="1000"), dict(LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3"),
+    # the k_intersect alternative and its knobs
+    dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
+    dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
     dict(_OLD, LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536"),
-    dict(_OLD, LPC_LARGE_N="1000"), dict(_OLD, LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3"),
 ]
 
 
 @pytest.mark.parametrize("cfg", _POLICIES)
 def test_launch_policies_bitexact(oracle_mod, monkeypatch, cfg):
-    """The launch policies (work queue or k_intersect, fan-group threshold,
-    piece granularity, coherence key, no sort, hand-over budgets and queues
-    that overflow, grid sizes) change only speed."""
+    """The launch policies (root items or k_intersect, piece granularity, no
+    sort, hand-over budgets and queues that overflow, grid sizes) change only
+    speed."""
     from lightpycl_amd.engine import Engine
     for k, v in cfg.items():
         monkeypatch.setenv(k, v)
