@@ -208,6 +208,16 @@ int lpc_project_hist(lpc_handle *h, int mode, int64_t n, const float *pos4, cons
                      const double *yedges, int ny, double weight_div, double *H,
                      float *x, float *y, float *pwr_cor);
 
+/* ---- diagnostics ---------------------------------------------------------- */
+/* The device's own conservative-filter code on n (ray, record) pairs, host
+ * arrays: origin3/dir3 (n,3), rec5 (n,5) = centre xyz, negB, negA (filter_record /
+ * node_record).  mode 0 filter_test, 1 filter_test2 (packed, record i with
+ * record i^1), 2 filter_test2h (packed + half-line cull), 3 filter_testh (the
+ * piece-root cull).  out_d[n]: the test value (pass = d <= 0).  Used by
+ * tests/test_gpu_filter.py to check the superset property on the GPU's code. */
+int lpc_filter_eval(lpc_handle *h, int64_t n, const float *origin3, const float *dir3, const float *rec5,
+                    int mode, float *out_d);
+
 /* ---- profiling ------------------------------------------------------------ */
 typedef struct {
     double intersect_ms;     /* sum of k_intersect durations (HIP events)       */

@@ -75,6 +75,7 @@ _PROTOS = {
     "lpc_prof_enable": [_P, _INT],
     "lpc_prof_read": [_P, _P, _INT],
     "lpc_prof_waves": [_P, _P, _I64, _P],
+    "lpc_filter_eval": [_P, _I64, _P, _P, _P, _INT, _P],
     "lpc_set_allreduce": [_P, _P, _P],
     "lpc_trace_global_stats": [_P, _P, _I32, _P],
     "lpc_shm_comm_open": [ctypes.c_char_p, _I32, _I32, _I32, _P],

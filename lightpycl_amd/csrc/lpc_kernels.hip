@@ -178,6 +178,14 @@ struct RayBase {
     }
 };
 
+// Unit direction for the filter tests (its rounding is inside the filter's
+// margin); one definition for every kernel that filters, and k_filter_eval.
+static __device__ __forceinline__ void unit_dir(const f3 &D, float &nx, float &ny, float &nz)
+{
+    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
+    nx = D.x * u; ny = D.y * u; nz = D.z * u;
+}
+
 // Stack depth per wave (node refs); the host checks every hierarchy fits.
 #define LPC_STACK 64
 
@@ -229,9 +237,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
     const int64_t s = w * 64 + lane;
     f3 O, D;
     ray.load(s < n ? s : n - 1, O, D);
-    // unit direction for the filter only (its rounding is inside the margin)
-    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);
-    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+    float nx, ny, nz;
+    unit_dir(D, nx, ny, nz);
     // start >= 0: a k_spill item (subtree root `start`, its parent passed)
     if (start < 0 &&
         !(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f)))
@@ -524,8 +531,8 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     const int64_t s = w * 64 + lane;
     f3 O = mk3(0.0f, 0.0f, 0.0f), D = mk3(0.0f, 0.0f, 1.0f);
     if (live) load_ray(R, rs, n, s < n ? s : n - 1, O, D);
-    const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);   // as trav_packet
-    const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+    float nx, ny, nz;
+    unit_dir(D, nx, ny, nz);
     const Piece Pl = pieces[min(lane, npieces - 1)];
     uint64_t m = 0;
     if (live)
@@ -579,8 +586,8 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
             const int64_t s = w * 64 + lane;
             f3 O, D;
             load_ray(R, rs, n, s < n ? s : n - 1, O, D);
-            const float u = 1.0f / sqrtf(D.x * D.x + D.y * D.y + D.z * D.z);   // as trav_packet
-            const float nx = D.x * u, ny = D.y * u, nz = D.z * u;
+            float nx, ny, nz;
+            unit_dir(D, nx, ny, nz);
             const int np = (npieces - cls + S - 1) / S;                       // this class's pieces
             const Piece Pl = pieces[min(cls + S * lane, npieces - 1)];
             for (int k = 0; k < np; ++k) {
@@ -847,6 +854,39 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     if (i >= n) return;
     keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
     vals[i] = (int32_t)i;
+}
+
+// Test entry (lpc_filter_eval, tests/test_gpu_filter.py): the device's own
+// filter code paths on given (ray, record) pairs, so the superset property
+// (every pair Moller-Trumbore accepts passes the filter) is checked on the code
+// the GPU runs.  mode 0: filter_test (k_roots_r / k_intersect root tests);
+// 1: filter_test2 (the packed child tests of the walk), record i packed with
+// record i ^ 1 against ray i; 2: filter_test2h (the same with the half-line
+// cull, LPC_HALF 1/2); 3: filter_testh (the piece-root half-line cull of
+// k_roots*, LPC_HALF 3, the default).  rec: cx cy cz negB negA per pair.
+__global__ __launch_bounds__(256) void k_filter_eval(int64_t n, const float *__restrict__ O,
+                                                     const float *__restrict__ D, const float *__restrict__ rec,
+                                                     int mode, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const f3 o = mk3(O[3 * i], O[3 * i + 1], O[3 * i + 2]);
+    const f3 d = mk3(D[3 * i], D[3 * i + 1], D[3 * i + 2]);
+    float nx, ny, nz;
+    unit_dir(d, nx, ny, nz);
+    const int64_t j = (i ^ 1) < n ? (i ^ 1) : i;
+    const float *a = rec + 5 * i, *b = rec + 5 * j;
+    float r;
+    if (mode == 1 || mode == 2) {
+        const lpc_f2 cx = {a[0], b[0]}, cy = {a[1], b[1]}, cz = {a[2], b[2]}, nb = {a[3], b[3]}, na = {a[4], b[4]};
+        r = mode == 1 ? filter_test2(cx, cy, cz, nb, na, o.x, o.y, o.z, nx, ny, nz).x
+                      : filter_test2h(cx, cy, cz, nb, na, o.x, o.y, o.z, nx, ny, nz).x;
+    } else if (mode == 3) {
+        r = filter_testh(a[0], a[1], a[2], a[3], a[4], o.x, o.y, o.z, nx, ny, nz);
+    } else {
+        r = filter_test(a[0], a[1], a[2], a[3], a[4], o.x, o.y, o.z, nx, ny, nz);
+    }
+    out[i] = r;
 }
 
 // ---------------------------------------------------------------------------

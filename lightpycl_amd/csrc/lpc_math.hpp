@@ -3,9 +3,12 @@
 //
 // Two kinds of code live here:
 //  * EXACT functions: the reference's arithmetic (kernel_reflect_refract_intersect.cl)
-//    operation for operation, compiled with FP contraction OFF, single-precision
-//    constants, IEEE division/sqrt.  Decisions (hit/miss, entering, n1/n2, TIR)
-//    and values (t, dest, children) are therefore bit-identical to the CPU oracle.
+//    operation for operation as ROCm's OpenCL compiler builds it for gfx950 with
+//    IEEE division/sqrt and no FP contraction in the kernel's own expressions
+//    (oracle/_ref/lpc_ref_ieee.co), single-precision constants, the OpenCL
+//    library's dot/cross/length/normalize (below).  Decisions (hit/miss,
+//    entering, n1/n2, TIR) and values (t, dest, children) are therefore
+//    bit-identical to the reference's own kernels and to the CPU oracle.
 //  * the CONSERVATIVE bounding-sphere filter used by the hot loop: a cheap test
 //    that is a superset of the exact Moller-Trumbore acceptance (see
 //    filter_record() for the margin derivation); only pairs that pass it are
@@ -36,14 +39,79 @@ LPC_HD f3 add3(f3 a, f3 b) { LPC_EXACT return mk3(a.x + b.x, a.y + b.y, a.z + b.
 LPC_HD f3 sub3(f3 a, f3 b) { LPC_EXACT return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
 LPC_HD f3 scl3(f3 a, float s) { LPC_EXACT return mk3(a.x * s, a.y * s, a.z * s); }
 LPC_HD f3 neg3(f3 a) { return mk3(-a.x, -a.y, -a.z); }
-// OpenCL dot/cross for float3 (sum order x, y, z).
-LPC_HD float dot3(f3 a, f3 b) { LPC_EXACT return a.x * b.x + a.y * b.y + a.z * b.z; }
+// OpenCL's geometric builtins for float3 exactly as ROCm's OpenCL device library
+// (the library the reference's kernels link when built for an AMD GPU,
+// oracle/Makefile `ref`) evaluates them: dot = fma(z, z', fma(y, y', x x')),
+// cross.x = fma(a.y, b.z, -(a.z b.y)) (and cyclic), length = the hardware square
+// root of that dot, normalize = v times the hardware reciprocal square root,
+// each with the library's rescaling outside the normal range.  fma is exactly
+// rounded on every target, so the host build (gcc fmaf) computes the same bits.
+LPC_HD float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 LPC_HD f3 cross3(f3 a, f3 b) {
-    LPC_EXACT
-    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return mk3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
-LPC_HD float len3(f3 a) { LPC_EXACT return sqrtf(dot3(a, a)); }
-LPC_HD f3 nrm3(f3 a) { LPC_EXACT float l = len3(a); return mk3(a.x / l, a.y / l, a.z / l); }
+// gfx950 v_sqrt_f32 / v_rsq_f32 (ldexp-scaled for denormal inputs as the library
+// does).  Host: correctly rounded, which tools/rsq_check.py measures the
+// hardware to be on every float in [1, 4).
+LPC_HD float hw_sqrt(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+LPC_HD float hw_rsq(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rsqf(x);
+#else
+    return (float)(1.0 / sqrt((double)x));
+#endif
+}
+// length(v): __ocml_len3_f32
+LPC_HD float len3(f3 a)
+{
+    LPC_EXACT
+    const float s = dot3(a, a);
+    if (s >= 1.17549435e-38f || s != s) {
+        if (s != INFINITY) return hw_sqrt(s);
+        const f3 b = mk3(a.x * 0x1p-66f, a.y * 0x1p-66f, a.z * 0x1p-66f);   // rescale (overflow)
+        const float t = dot3(b, b);
+        const bool sc = t < 1.17549435e-38f;
+        const float q = hw_sqrt(sc ? ldexpf(t, 32) : t);
+        return (sc ? ldexpf(q, -16) : q) * 0x1p66f;
+    }
+    const f3 b = mk3(a.x * 0x1p86f, a.y * 0x1p86f, a.z * 0x1p86f);          // rescale (underflow)
+    const float t = dot3(b, b);
+    const bool sc = t < 1.17549435e-38f;
+    const float q = hw_sqrt(sc ? ldexpf(t, 32) : t);
+    return (sc ? ldexpf(q, -16) : q) * 0x1p-86f;
+}
+// normalize(v): OpenCL library normalize for float3
+LPC_HD f3 nrm3(f3 a)
+{
+    LPC_EXACT
+    float s = dot3(a, a);
+    if (s >= 1.17549435e-38f || s != s) {
+        if (s == INFINITY) {
+            a = mk3(a.x * 0x1p-66f, a.y * 0x1p-66f, a.z * 0x1p-66f);
+            s = dot3(a, a);
+            if (s == INFINITY) {          // infinite components -> +-1, the rest +-0
+                a = mk3(copysignf(isinf(a.x) ? 1.0f : 0.0f, a.x), copysignf(isinf(a.y) ? 1.0f : 0.0f, a.y),
+                        copysignf(isinf(a.z) ? 1.0f : 0.0f, a.z));
+                s = dot3(a, a);
+            }
+        }
+    } else {
+        a = mk3(a.x * 0x1p86f, a.y * 0x1p86f, a.z * 0x1p86f);
+        s = dot3(a, a);
+    }
+    const bool sc = s < 1.17549435e-38f;
+    float r = hw_rsq(sc ? s * 0x1p24f : s);
+    if (sc) r = r * 0x1p12f;
+    return mk3(a.x * r, a.y * r, a.z * r);
+}
 
 // ---------------------------------------------------------------------------
 // Moller-Trumbore exactly as intersect_triangle (.cl:50-101), with the two edge

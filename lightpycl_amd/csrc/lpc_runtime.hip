@@ -2105,6 +2105,28 @@ int lpc_project_hist(lpc_handle *h, int mode, int64_t n, const float *pos4, cons
     return 0;
 }
 
+int lpc_filter_eval(lpc_handle *h, int64_t n, const float *origin3, const float *dir3, const float *rec5,
+                    int mode, float *out_d)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (n < 0 || mode < 0 || mode > 3 || (n > 0 && (!origin3 || !dir3 || !rec5 || !out_d)))
+        return set_err(h, LPC_E_ARG, "filter_eval: bad argument");
+    RETIF(settle(h));
+    HIPCHK(h, hipSetDevice(h->device));
+    if (n == 0) return 0;
+    RETIF(dalloc(h, h->d_tmp, (size_t)n * 48));
+    float *dO = (float *)h->d_tmp.p, *dD = dO + 3 * n, *dR = dD + 3 * n, *dOut = dR + 5 * n;
+    HIPCHK(h, hipMemcpy(dO, origin3, (size_t)n * 12, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(dD, dir3, (size_t)n * 12, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(dR, rec5, (size_t)n * 20, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_filter_eval, dim3(grid1(n)), dim3(256), 0, h->stream, n, (const float *)dO,
+                       (const float *)dD, (const float *)dR, mode, dOut);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(out_d, dOut, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int lpc_prof_enable(lpc_handle *h, int on)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");

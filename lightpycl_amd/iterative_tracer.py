@@ -157,35 +157,47 @@ class CL_Tracer:
         self.hist_data = np.histogram2d(x=pos[:, 0], y=pos[:, 1], bins=points, range=limits, weights=pwr)
         return self.hist_data
 
-    def _project(self, mode, limits, points, rot=None):
+    def _project(self, mode, limits, points, rot=None, want_xy=False):
         if self._aggregate:
-            H, xe, ye = self.engine.project_hist(None, None, limits, points, mode=mode, rot=rot)
-        else:
-            pos, pwr = self.get_measured_rays()
-            H, xe, ye = self.engine.project_hist(pos, np.asarray(pwr).reshape(-1), limits, points,
-                                                 mode=mode, rot=rot)
-        return H, xe, ye
+            return self.engine.project_hist(None, None, limits, points, mode=mode, rot=rot, want_xy=want_xy)
+        pos, pwr = self.get_measured_rays()
+        return self.engine.project_hist(pos, np.asarray(pwr).reshape(-1), limits, points, mode=mode, rot=rot,
+                                        want_xy=want_xy)
 
     def get_binned_data_angular(self, limits=((-1, 1), (-1, 1)), points=500):
         """angular_project on the GPU + histogram2d binning on the GPU (:534-562)."""
-        self.hist_data = self._project(0, limits, points)
+        self.hist_data = tuple(self._project(0, limits, points))
         return self.hist_data
 
     def get_binned_data_stereographic(self, limits=((-1, 1), (-1, 1)), points=500):
         """stereograph_project on the GPU + binning (:503-531)."""
-        self.hist_data = self._project(1, limits, points)
+        self.hist_data = tuple(self._project(1, limits, points))
         return self.hist_data
 
     def replicate_lightsources_and_plot(self, limits=((-10, 10), (-10, 10)), points=500, axis="z", sources=36,
                                         use_3D=True, plot=True):
         """Emulate ``sources`` rotated copies of the source by rotating the measured rays
-        (:564-657); the histogram is accumulated on the GPU per rotation."""
+        (:564-657): angular_project on the GPU per rotation (R(ang) rows as the
+        reference's R_dev, :601), the projected points of all rotations
+        concatenated and binned once with np.histogram2d, as the reference does
+        (:608-627)."""
         R = _rot(axis)
-        H = None
+        xs, ys, ps = [], [], []
         for k in np.arange(sources):
             ang = k * 2.0 * np.pi / sources
-            h, xe, ye = self._project(0, limits, points, rot=np.asarray(R(ang), dtype=np.float32))
-            H = h if H is None else H + h
+            _, _, _, x, y, pc = self._project(0, limits, points, rot=np.asarray(R(ang), dtype=np.float32),
+                                              want_xy=True)
+            xs.append(x)
+            ys.append(y)
+            ps.append(np.float64(pc))
+        x = np.concatenate(xs) if xs else np.zeros(0, np.float32)
+        y = np.concatenate(ys) if ys else np.zeros(0, np.float32)
+        pwr = np.concatenate(ps) if ps else np.zeros(0, np.float64)
+        dx = np.float64(limits[0][1] - limits[0][0]) / np.float64(points)
+        dy = np.float64(limits[1][1] - limits[1][0]) / np.float64(points)
+        pwr = pwr / (dx * dy)                                           # :622-624
+        H, xe, ye = np.histogram2d(x=x.flatten(), y=y.flatten(), bins=points, range=limits,
+                                   weights=pwr.flatten())              # :627
         self.hist_data = (H, xe, ye)
         if plot:
             self._plot(H, xe * 180.0 / np.pi, ye * 180.0 / np.pi, use_3D, "replicated_sources")
@@ -262,22 +274,31 @@ class CL_Tracer:
         within = np.sum(pwr0[np.where(elevation0 < el)])
         return sum(pwr0), el / np.pi * 180.0, within / sum(pwr0) * 100.0
 
-    def pickle_results(self):
-        """Pickle (results, meshes) to ./<timestamp>-tracer_results.txt (:711-733)."""
-        fname = "./{0}-tracer_results.txt".format(time.strftime("%Y.%m.%d.%H.%M.%S"))
+    def pickle_results(self, fname=None):
+        """Pickle (results, meshes) with protocol 1 to ./<timestamp>-tracer_results.txt,
+        as the reference writes them (``pickle.dumps((results, meshes), 1)``, :711-733).
+        Aggregate-mode traces have no per-ray results: they are fetched first."""
+        if fname is None:
+            fname = "./{0}-tracer_results.txt".format(time.strftime("%Y.%m.%d.%H.%M.%S"))
         try:
+            data = pickle.dumps((self.results, self.meshes), 1)
             with open(fname, "wb") as f:
-                pickle.dump((self.results, self.meshes), f, protocol=pickle.HIGHEST_PROTOCOL)
+                f.write(data)
         except Exception:
             print("Pickling results failed.")
             return None
         return fname
 
     def load_pickle_results(self, path):
-        """Load results written by :meth:`pickle_results` (only load files you wrote)."""
+        """Load a results file written by :meth:`pickle_results` or by the reference
+        (Python 2 cPickle, :735-751): byte strings decoded as latin-1 (numpy arrays of
+        Python-2 pickles), the reference's module names (``geo_optical_elements``,
+        ``light_source``) mapped to this package's.  Unpickling runs code named in
+        the file: only load files you (or your reference runs) wrote."""
         with open(path, "rb") as f:
-            (self.results, self.meshes) = pickle.load(f)
+            (self.results, self.meshes) = _RefUnpickler(f, encoding="latin1").load()
         self._aggregate = False
+        return self.results
 
     def save_traced_scene(self, dxf_file):
         """DXF export of rays and facets; needs the optional ``dxfwrite`` package."""
@@ -291,6 +312,16 @@ class CL_Tracer:
         for t0, t1, t2 in zip(*self.geometry):
             drawing.add(dxf.face3d([t0[0:3], t1[0:3], t2[0:3]], layer="Geometry"))
         drawing.save()
+
+
+class _RefUnpickler(pickle.Unpickler):
+    """Maps the reference's top-level module names to this package's modules."""
+    _MAP = {"geo_optical_elements": "lightpycl_amd.geo_optical_elements",
+            "light_source": "lightpycl_amd.light_source",
+            "iterative_tracer": "lightpycl_amd.iterative_tracer"}
+
+    def find_class(self, module, name):
+        return super().find_class(self._MAP.get(module, module), name)
 
 
 # alias with the north star's spelling

@@ -9,21 +9,24 @@
  * reference (kernel_reflect_refract_intersect.cl) with the reference's
  * arithmetic order.  Every function cites the reference lines it follows.
  *
- * Numeric conventions (the reference is OpenCL C and can be built several
- * ways; these are the choices DESIGN.md section "Numerics" documents):
+ * Numeric conventions: the reference's kernels as ROCm's OpenCL compiler
+ * builds them for gfx950 with IEEE division/sqrt and no FP contraction in the
+ * kernel's own expressions (oracle/_ref/lpc_ref_ieee.co):
  *   - single-precision constants everywhere (the .cl only compiles with
  *     -cl-single-precision-constant);
- *   - no FMA contraction (build with -ffp-contract=off);
- *   - dot(a,b) = (a.x*b.x + a.y*b.y) + a.z*b.z, cross as written in the
- *     OpenCL spec, length(v) = sqrt(dot(v,v)), normalize(v) = v / length(v),
- *     pown(x,2) = x*x;  exp/acos/atan2/sin/cos are the C library's.
+ *   - no FMA contraction in the kernel expressions (build with -ffp-contract=off);
+ *   - the OpenCL library's builtins as ROCm's device library evaluates them:
+ *     dot(a,b) = fma(a.z,b.z, fma(a.y,b.y, a.x*b.x)), cross.x =
+ *     fma(a.y,b.z, -(a.z*b.y)) (cyclic), length = sqrt of that dot,
+ *     normalize = v * rsqrt(dot) (the hardware's sqrt / rsqrt, which
+ *     tools/rsq_check.py measures as correctly rounded; computed here through
+ *     double), pown(x,2) = x*x;  exp/acos/atan2/sin/cos are the C library's
+ *     (1-2 ulp from the device library's).
  *
- * Parity status: the reference cannot be executed in this image (OpenCL C
- * with no OpenCL device and no x86 OpenCL builtin library; Python 2 host
- * code).  This oracle is pinned by the known-answer rows recorded in
- * SURVEY.md section 4 and by the per-iteration ray counts / triangle counts
- * SURVEY.md records for the reference scenes (tests/test_oracle_pins.py).
- * Scene-level parity beyond those pins is UNPINNED.
+ * Parity status: pinned against the reference's own kernels compiled for
+ * gfx950 (tests/test_ref_parity.py, on the GPU) and by the known-answer rows
+ * recorded in SURVEY.md section 4 and the reference-scene counts
+ * (tests/test_oracle_pins.py).
  *
  * Layouts follow the reference exactly: float3 buffers are (n,4) float32
  * arrays (16-byte stride, w ignored on read, written as 0), per-ray/per-mesh
@@ -42,12 +45,51 @@ static inline v3 add3(v3 a, v3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z);
 static inline v3 sub3(v3 a, v3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline v3 scl3(v3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
 static inline v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
-static inline float dot3(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* OpenCL dot / cross / length / normalize (ROCm device library forms) */
+static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline v3 cross3(v3 a, v3 b) {
-    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return mk3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
-static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
-static inline v3 nrm3(v3 a) { float l = len3(a); return mk3(a.x / l, a.y / l, a.z / l); }
+static inline float rsq(float x) { return (float)(1.0 / sqrt((double)x)); }
+static inline float len3(v3 a)
+{
+    const float s = dot3(a, a);
+    if (s >= 1.17549435e-38f || s != s) {
+        if (s != INFINITY) return sqrtf(s);
+        const v3 b = mk3(a.x * 0x1p-66f, a.y * 0x1p-66f, a.z * 0x1p-66f);
+        const float t = dot3(b, b);
+        const int sc = t < 1.17549435e-38f;
+        const float q = sqrtf(sc ? ldexpf(t, 32) : t);
+        return (sc ? ldexpf(q, -16) : q) * 0x1p66f;
+    }
+    const v3 b = mk3(a.x * 0x1p86f, a.y * 0x1p86f, a.z * 0x1p86f);
+    const float t = dot3(b, b);
+    const int sc = t < 1.17549435e-38f;
+    const float q = sqrtf(sc ? ldexpf(t, 32) : t);
+    return (sc ? ldexpf(q, -16) : q) * 0x1p-86f;
+}
+static inline v3 nrm3(v3 a)
+{
+    float s = dot3(a, a);
+    if (s >= 1.17549435e-38f || s != s) {
+        if (s == INFINITY) {
+            a = mk3(a.x * 0x1p-66f, a.y * 0x1p-66f, a.z * 0x1p-66f);
+            s = dot3(a, a);
+            if (s == INFINITY) {
+                a = mk3(copysignf(isinf(a.x) ? 1.0f : 0.0f, a.x), copysignf(isinf(a.y) ? 1.0f : 0.0f, a.y),
+                        copysignf(isinf(a.z) ? 1.0f : 0.0f, a.z));
+                s = dot3(a, a);
+            }
+        }
+    } else {
+        a = mk3(a.x * 0x1p86f, a.y * 0x1p86f, a.z * 0x1p86f);
+        s = dot3(a, a);
+    }
+    const int sc = s < 1.17549435e-38f;
+    float r = rsq(sc ? s * 0x1p24f : s);
+    if (sc) r = r * 0x1p12f;
+    return mk3(a.x * r, a.y * r, a.z * r);
+}
 
 /* Moller-Trumbore, kernel_reflect_refract_intersect.cl:50-101.  Returns 1 and
  * *t when u,v tests pass (t itself is not range-checked here, as in .cl:98). */

@@ -295,3 +295,14 @@ extern "C" void sliver_den(int n, const float *D, const float *V, float *dmin_ou
         den_fma[i] = fmaf(fz, e1[2], fmaf(fy, e1[1], fx * e1[0]));
     }
 }
+
+// node_record of m triangles as one record (cx, cy, cz, negB, negA): the test a
+// hierarchy node / piece root carries (tests/test_gpu_filter.py evaluates it on
+// the device).
+extern "C" void node_rec(int m, const float *V, double S, float *out)
+{
+    std::vector<const float *> tv((size_t)m * 3);
+    for (int j = 0; j < m; ++j)
+        for (int v = 0; v < 3; ++v) tv[3 * (size_t)j + v] = V + 9 * j + 3 * v;
+    node_record(tv.data(), m, S, &out[0], &out[1], &out[2], &out[3], &out[4]);
+}

@@ -33,12 +33,15 @@ def bounce_stats(a, b, max_ray_len):
         y = np.asarray(b[k], np.float32)[same, :3]
         out[k + "_maxabs"] = float(np.max(np.abs(x.astype(np.float64) - y))) if x.size else 0.0
         out[k + "_exact"] = float(np.mean(np.all(x == y, axis=1))) if x.size else 1.0
+    # powers relative to the ray's own (post-dissipation) power, so that a child
+    # carrying a near-zero share (R ~ 0) is not judged by its own tiny magnitude
+    ref_pow = np.abs(np.asarray(b["pow"], np.float64).reshape(-1)[same])
     for k in ("pow", "r_pow", "t_pow"):
         x = np.asarray(a[k], np.float64).reshape(-1)[same]
         y = np.asarray(b[k], np.float64).reshape(-1)[same]
-        den = np.maximum(np.abs(y), 1e-30)
+        den = np.maximum(np.maximum(np.abs(y), ref_pow), 1e-30)
         rel = np.abs(x - y) / den
-        out[k + "_maxrel"] = float(rel[np.abs(y) > 1e-30].max()) if np.any(np.abs(y) > 1e-30) else 0.0
+        out[k + "_maxrel"] = float(rel.max()) if rel.size else 0.0
         out[k + "_exact"] = float(np.mean(x == y)) if x.size else 1.0
     out["all_exact"] = bool(out["id_mismatch"] == 0 and all(out[k] == 1.0 for k in out if k.endswith("_exact")))
     out["max_ray_len"] = float(max_ray_len)

@@ -147,3 +147,39 @@ def test_c_abi_errors_without_device():
     assert L.lpc_last_error(None)                 # message for the failed open
     assert L.lpc_close(None) == 0
     assert L.lpc_trace_reset(None) != 0
+
+
+def test_pickle_results_protocol1_and_reference_module_names(tmp_path):
+    """pickle_results writes (results, meshes) with protocol 1 as the reference
+    (iterative_tracer.py:711-733); load_pickle_results reads it back and also a
+    file naming the reference's own modules (geo_optical_elements, as a pickle
+    written by the reference's Python 2 code does)."""
+    import pickle
+
+    import numpy as np
+    from lightpycl_amd import scenes
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    sc = scenes.cube(n=16, seed=1)
+    rng = np.random.default_rng(0)
+    results = [(rng.random((16, 4)).astype(np.float32), rng.random((16, 4)).astype(np.float32),
+                rng.random((16, 1)).astype(np.float32), rng.integers(-1, 2, 16).astype(np.int32))]
+    tr = CL_Tracer.__new__(CL_Tracer)          # no GPU needed for the file format
+    tr.results, tr.meshes, tr._aggregate = results, sc.meshes, False
+    fname = tr.pickle_results(str(tmp_path / "r.txt"))
+    raw = open(fname, "rb").read()
+    assert raw[:1] != b"\x80"                   # protocol 1 has no PROTO opcode
+    tr2 = CL_Tracer.__new__(CL_Tracer)
+    tr2.load_pickle_results(fname)
+    for a, b in zip(tr2.results[0], results[0]):
+        np.testing.assert_array_equal(a, b)
+    assert [len(m.tribuf()[0]) for m in tr2.meshes] == [len(m.tribuf()[0]) for m in sc.meshes]
+    # the reference's module name in the GLOBAL opcodes
+    ref_raw = raw.replace(b"clightpycl_amd.geo_optical_elements\n", b"cgeo_optical_elements\n")
+    assert ref_raw != raw
+    p2 = tmp_path / "ref.txt"
+    p2.write_bytes(ref_raw)
+    tr3 = CL_Tracer.__new__(CL_Tracer)
+    tr3.load_pickle_results(str(p2))
+    assert type(tr3.meshes[0]).__name__ == "GeoObject"
+    with pytest.raises(Exception):
+        pickle.loads(ref_raw)                   # a plain loader cannot resolve the reference's module

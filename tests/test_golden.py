@@ -1,8 +1,11 @@
 """Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py from
-the pinned oracle).  CPU: the seeded scene builders and the oracle still
-reproduce them.  GPU: liblpc reproduces the first bounce bit-exactly (powers of
-rays leaving a dissipative medium within 2 ulp: exp() differs between libm and
-the device library) and the trace's ray counts / measured power."""
+the REFERENCE's own kernels compiled for gfx950 and its host loop, on the GPU
+box).  CPU: the seeded scene builders reproduce the inputs bit for bit and the
+CPU oracle reproduces the outputs -- decisions, hit indices and destinations bit
+for bit, children directions / powers within the few ulp that the hardware's
+rsqrt and the device library's exp differ from the C library, the trace's counts
+within SURVEY.md section 8c's tolerance.  GPU: liblpc reproduces every output
+bit for bit and the trace's counts and measured power."""
 import glob
 import os
 
@@ -22,14 +25,20 @@ def load(name):
     return dict(np.load(os.path.join(HERE, "golden", name + ".npz")))
 
 
-def _compare(got, g, name):
+def _compare(got, g, name, exact=True):
+    """exact: bit for bit.  Otherwise (the CPU oracle): decisions, indices and
+    destinations bit for bit; children directions (|d| ~ 1) within 4e-6, powers
+    within 4e-6 of the ray's own power (hardware rsqrt / device exp vs libm)."""
+    parent = np.abs(np.asarray(g["b_pow"], np.float64)).reshape(-1)
     for k in KEYS:
         a = got[k][:, :3] if got[k].ndim == 2 and got[k].shape[1] == 4 else got[k]
         b = g["b_" + k]
-        if name == "cube" and k in ("pow", "r_pow", "t_pow"):
-            np.testing.assert_allclose(a, b, rtol=4e-7, atol=0, err_msg=k)
-        else:
+        if exact or k not in ("r_dir", "t_dir", "pow", "r_pow", "t_pow"):
             np.testing.assert_array_equal(a, b, err_msg=f"{name}:{k}")
+            continue
+        d = np.abs(np.asarray(a, np.float64) - b)
+        tol = 4e-6 if k.endswith("dir") else 4e-6 * np.maximum(parent, np.abs(np.asarray(b, np.float64)))
+        assert np.all(d <= tol), (name, k, float(d.max()))
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -43,7 +52,13 @@ def test_builders_and_oracle_reproduce_fixture(oracle_mod, name):
     assert S.tri_count == int(g["tri_count"])
     b = oracle_mod.bounce(S, g["origin"], g["dir"], g["pow_in"], np.zeros(n, np.int32), np.full(n, -2, np.int32),
                           g["max_ray_len"], g["ior_env"])
-    _compare(b, g, "oracle")
+    _compare(b, g, "oracle", exact=False)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                               keep_results=False)
+    want = list(g["counts"])
+    assert len(info["counts"]) == len(want)
+    assert all(abs(a - b) <= 1e-3 * b for a, b in zip(info["counts"], want)), (info["counts"], want)
+    np.testing.assert_allclose(info["mesh_power"], g["mesh_power"], rtol=1e-4, atol=1e-12)
 
 
 @pytest.mark.gpu
@@ -60,4 +75,4 @@ def test_gpu_reproduces_fixture(engine, name):
     from lightpycl_amd.distributed import ShardedTrace
     r = ShardedTrace(engine).run(sc.iterations, sc.tau, float(np.sum(g["pow_in"], dtype=np.float64)))
     assert r["global_counts"] == list(g["counts"])
-    np.testing.assert_allclose(r["mesh_power"], g["mesh_power"], rtol=1e-6 if name == "cube" else 1e-12)
+    np.testing.assert_allclose(r["mesh_power"], g["mesh_power"], rtol=1e-12)

@@ -6,7 +6,8 @@ iterative_tracer.py:383-391) and the trace-end angular histogram all-reduced.
 
 The parent spawns fresh child processes (torch.multiprocessing, spawn) and never
 replaces itself.  The global per-iteration counts, per-mesh measured power and
-histogram must equal the oracle's single-process trace of all rays.
+histogram must equal the single-process trace of all rays by the reference's own
+kernels (the `checker` fixture; the CPU oracle without oracle/_ref).
 """
 import json
 import os
@@ -73,14 +74,15 @@ def _child(rank, world, port, name, n, hook, out_path):
 
 @pytest.mark.parametrize("name,n,hook", [("synthetic", 20000, "shm"), ("lens", 20000, "shm"),
                                          ("lens", 9000, "gloo")])
-def test_sharded_trace_two_processes(oracle_mod, tmp_path, name, n, hook):
+def test_sharded_trace_two_processes(oracle_mod, checker, tmp_path, name, n, hook):
     import torch.multiprocessing as mp
     from lightpycl_amd import scenes
     out = str(tmp_path / "r.json")
     mp.spawn(_child, args=(2, _free_port(), name, n, hook, out), nprocs=2, join=True)
     got = json.load(open(out))
     sc = scenes.BUILDERS[name](n=n, seed=2)
-    res, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env)
+    res, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                                 bounce_fn=checker[0])
     assert got["counts"] == info["counts"]
     np.testing.assert_allclose(got["mesh_power"], info["mesh_power"], rtol=1e-12, atol=1e-12)
     for counts, mpow, _ in got["runs"]:
