@@ -10,6 +10,7 @@ MI355X_MICROARCH.md section HBM (FETCH_SIZE reads half of a wide streaming read)
 """
 import collections
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -37,6 +38,8 @@ if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
     rec = {"source": f"profiles/{tag}_pmc.json", "kernel": kname,
            "fetch_size_kb_mean": fetch, "write_size_kb_mean": write,
            "hbm_bytes_per_launch": (2.0 * fetch + write) * 1024.0,
+           "kernels_sha16": hashlib.sha256(open(os.path.join(root, "lightpycl_amd", "csrc", "lpc_kernels.hip"),
+                                                "rb").read()).hexdigest()[:16],
            "note": f"mean over the {kname} launches of one bench step (all iterations)"}
     for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
         if c in ki:
