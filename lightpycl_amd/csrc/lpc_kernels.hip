@@ -186,8 +186,12 @@ static __device__ __forceinline__ void unit_dir(const f3 &D, float &nx, float &n
     nx = D.x * u; ny = D.y * u; nz = D.z * u;
 }
 
-// Stack depth per wave (node refs); the host checks every hierarchy fits.
-#define LPC_STACK 64
+// Stack depth per wave (node refs); the host checks every hierarchy fits (one
+// node per step: (W - 1) levels + 1; NB nodes per step: NB W levels).
+#define LPC_STACK 256
+#define LPC_STACK1 64
+// Nodes per step of the batched walk (trav_packet NB > 1)
+#define LPC_NB 4
 
 // k-th set bit (0-based) of m.
 static __device__ __forceinline__ int select_bit(uint64_t m, int k)
@@ -204,6 +208,7 @@ static __device__ __forceinline__ int select_bit(uint64_t m, int k)
 // LDS of one wave's traversal.
 struct WaveLds {
     int32_t stack[LPC_STACK];
+    uint32_t nbuf[LPC_NB][48];         // batched walk: the step's node records (cx cy cz negB negA ref, W = 8)
     int32_t qidx[64], qscan[64];
     uint64_t qmask[64];
     float ray[6][64];                  // the packet's rays (O, D) for the drain
@@ -219,7 +224,12 @@ struct WaveLds {
 // triangle's (index, lane mask) is queued for the exact test.
 // PROF: the profiling counters / records and the LPC_DBG timing switches
 // (compiled out of the default launches: fewer live registers in the hot loop).
-template <int W, bool PROF = true, class RL = RayPair, bool HALF = false>
+// NB > 1 (W = 8): the walk takes up to NB nodes off the stack per step, the
+// wave fetches their records at once (16 lanes x 12 bytes per node, vector loads
+// into LDS) and tests them one after the other: NB node fetches in flight
+// instead of one scalar-load round trip per node (the walk's critical path).  The
+// visit order changes, the results do not (order-independent flushes).
+template <int W, bool PROF = true, class RL = RayPair, bool HALF = false, int NB = 1>
 static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                                                    int64_t n, const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
@@ -306,18 +316,71 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(SP.ctr, (uint32_t)top);
             base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0);
+            // one node per step: top <= 64 (the host's depth check, LPC_STACK1)
+            constexpr int kSpan = NB > 1 ? LPC_STACK : 64;
             if (base + (uint32_t)top <= SP.cap) {
-                if (lane < top) {
-                    SpillItem it;
-                    it.w = (int32_t)w; it.node = L.stack[lane]; it.slot = P.slot; it.piece = piece_id;
-                    SP.items[base + lane] = it;
+#pragma unroll
+                for (int j0 = 0; j0 < kSpan; j0 += 64) {
+                    const int j = j0 + lane;
+                    if (j < top) {
+                        SpillItem it;
+                        it.w = (int32_t)w; it.node = L.stack[j]; it.slot = P.slot; it.piece = piece_id;
+                        SP.items[base + j] = it;
+                    }
                 }
                 top = 0;
                 break;
             }
             // queue full: void the part of the range inside it, carry on here
-            if (lane < top && base + (uint32_t)lane < SP.cap) SP.items[base + lane].node = -1;
+#pragma unroll
+            for (int j0 = 0; j0 < kSpan; j0 += 64) {
+                const int j = j0 + lane;
+                if (j < top && base + (uint32_t)j < SP.cap) SP.items[base + j].node = -1;
+            }
             budget = 0;
+        }
+        if constexpr (NB > 1) {
+            static_assert(W == 8, "batched walk: 8-wide nodes");
+            const int k = min(top, NB);
+            {   // lanes 16 i + j fetch dwords 3 j .. 3 j + 2 of the i-th node from the top
+                const int i = lane >> 4, j = lane & 15;
+                if (i < k) {
+                    const uint32_t *src = (const uint32_t *)(nodes + L.stack[top - 1 - i]) + 3 * j;
+                    const uint32_t a = src[0], b = src[1], c = src[2];
+                    L.nbuf[i][3 * j] = a; L.nbuf[i][3 * j + 1] = b; L.nbuf[i][3 * j + 2] = c;
+                }
+            }
+            top -= k;
+            for (int b = 0; b < k; ++b) {
+                const float *nf = (const float *)L.nbuf[b];
+                const int32_t *nr = (const int32_t *)L.nbuf[b] + 5 * W;
+                ++n_nodes;
+                float d[W];
+#pragma unroll
+                for (int q = 0; q < W; q += 2) {
+                    const lpc_f2 cx = {nf[q], nf[q + 1]}, cy = {nf[W + q], nf[W + q + 1]};
+                    const lpc_f2 cz = {nf[2 * W + q], nf[2 * W + q + 1]}, nB = {nf[3 * W + q], nf[3 * W + q + 1]};
+                    const lpc_f2 nA = {nf[4 * W + q], nf[4 * W + q + 1]};
+                    const lpc_f2 r = HALF ? filter_test2h(cx, cy, cz, nB, nA, O.x, O.y, O.z, nx, ny, nz)
+                                          : filter_test2(cx, cy, cz, nB, nA, O.x, O.y, O.z, nx, ny, nz);
+                    d[q] = r.x;
+                    d[q + 1] = r.y;
+                }
+                if (__builtin_amdgcn_readfirstlane(nr[0]) >= 0) {     // internal node: children are nodes
+#pragma unroll
+                    for (int q = 0; q < W; ++q)
+                        if (any_lane(d[q] <= 0.0f)) L.stack[top++] = __builtin_amdgcn_readfirstlane(nr[q]);
+                } else {                                                 // leaf: triangles -> exact-test queue
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(d[q] <= 0.0f);
+                        if (!m) continue;
+                        if (lane == 0) { L.qidx[nq] = ~nr[q]; L.qmask[nq] = m; }
+                        if (++nq == 64) drain();
+                    }
+                }
+            }
+            continue;
         }
         const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
         const NodeW<W> N = nodes[node];
@@ -434,7 +497,7 @@ __global__ __launch_bounds__(256, 6) void k_intersect(RaysIn R, const float *__r
 // item that again exceeds the budget hands its remaining subtrees to the next
 // level's queue (`out`; budget 0 on the last level).  One wave per block (a
 // wave's slot frees when its items end, see k_rootwalk).
-template <int W, bool PROF = false, bool HALF = false>
+template <int W, bool PROF = false, bool HALF = false, int NB = 1>
 __global__ __launch_bounds__(64, 6) void k_spill(RayBase ray, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -451,8 +514,8 @@ __global__ __launch_bounds__(64, 6) void k_spill(RayBase ray, int64_t n,
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = I.node; P.slot = I.slot;
-        trav_packet<W, PROF, RayBase, HALF>(lds, ray, n, perm, nodes, xrec, P, I.w, I.piece, eps,
-                                            max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
+        trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, I.w, I.piece, eps,
+                                                max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
     }
 }
 
@@ -560,22 +623,42 @@ __global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restri
     }
 }
 
-// k_roots_s: k_roots_r's tests (lanes = a packet's rays, one ballot per piece)
-// as tasks: a block takes pb packets, task t = (packet t / S, piece class t % S)
-// tests the pieces p = class + S k (npieces <= 64 S), the block's 4 waves take
-// the tasks in turn, and the block reserves all its items with one atomic.
-// Small populations (few packets) get S = 2..4 waves per packet instead of one
-// wave looping over every piece; large ones several packets per atomic.
-// Same tests, same items as k_roots / k_roots_r (their order in the queue may
-// differ; the walk's results do not depend on it).
+// k_roots_s: k_roots_r's tests (lanes = a packet's rays) as tasks: a block takes
+// pb packets, task t = (packet t / S, piece class t % S) tests the pieces
+// p = class + S k (npieces <= 64 S), the block's 4 waves take the tasks in turn,
+// and the block reserves all its items with one atomic.  Small populations (few
+// packets) get S = 2..4 waves per packet instead of one wave looping over every
+// piece; large ones several packets per atomic.
+// Gated form (ngroups > 0: pieces cut below the run roots): a task first tests
+// the runs' root records (`groups`, s_lo/s_hi = the run's range of pieces) and
+// then only the pieces of runs some ray of the packet passes.  Exact: a ray whose
+// line Moller-Trumbore accepts against a triangle passes every test above it
+// (node_record of all triangles below), the run root's included, so a piece of a
+// run no ray passes holds no accepted pair for the packet.
+// Piece records are wave-uniform (scalar loads); a lane accumulates its own
+// pass bits and the wave ORs them once per task (no ballot per test).
 #define LPC_ROOTS_TASKS 16
+static __device__ __forceinline__ uint64_t wave_or64(uint64_t v)
+{
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    for (int o = 32; o >= 1; o >>= 1) {
+        lo |= (uint32_t)__shfl_xor((int)lo, o, 64);
+        hi |= (uint32_t)__shfl_xor((int)hi, o, 64);
+    }
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)hi) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
+}
+
+template <bool HALF>
 __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                 const Piece *__restrict__ pieces, int npieces, QueueArgs Q,
-                                                 int half, int S, int pb)
+                                                 const Piece *__restrict__ pieces, int npieces,
+                                                 const Piece *__restrict__ groups, int ngroups, QueueArgs Q,
+                                                 int S, int pb)
 {
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int c = q_shard(blockIdx.x);
     const int ntask = S * pb;
     for (int t = wv; t < ntask; t += 4) {
@@ -588,16 +671,31 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
             load_ray(R, rs, n, s < n ? s : n - 1, O, D);
             float nx, ny, nz;
             unit_dir(D, nx, ny, nz);
-            const int np = (npieces - cls + S - 1) / S;                       // this class's pieces
-            const Piece Pl = pieces[min(cls + S * lane, npieces - 1)];
-            for (int k = 0; k < np; ++k) {
-                if (bcasti(Pl.root, k) < 0) continue;
-                const float cx = bcast(Pl.cx, k), cy = bcast(Pl.cy, k), cz = bcast(Pl.cz, k);
-                const float nb = bcast(Pl.negB, k), na = bcast(Pl.negA, k);
-                const float d = half ? filter_testh(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz)
-                                     : filter_test(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz);
-                if (any_lane(d <= 0.0f)) m |= 1ull << k;
+            uint64_t ml = 0;                    // this lane's ray: bit k = piece cls + S k passes
+            auto test = [&](int lo, int hi) {   // the class's pieces in [lo, hi)
+                const int p0 = lo + ((cls - lo % S) % S + S) % S;
+                for (int p = p0, k = p0 / S; p < hi; p += S, ++k) {
+                    const Piece &P = pieces[p];
+                    const float d = HALF ? filter_testh(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz)
+                                         : filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz);
+                    ml |= (uint64_t)(d <= 0.0f) << k;
+                }
+            };
+            if (ngroups > 0) {
+                uint64_t gl = 0;
+                for (int g = 0; g < ngroups; ++g) {
+                    const Piece &G = groups[g];
+                    const float d = filter_test(G.cx, G.cy, G.cz, G.negB, G.negA, O.x, O.y, O.z, nx, ny, nz);
+                    gl |= (uint64_t)(d <= 0.0f) << g;
+                }
+                for (uint64_t gm = wave_or64(gl); gm; gm &= gm - 1) {
+                    const int g = __builtin_ctzll(gm);
+                    test(groups[g].s_lo, groups[g].s_hi);
+                }
+            } else {
+                test(0, npieces);
             }
+            m = wave_or64(ml);
         }
         if (lane == 0) s_m[t] = m;
     }
@@ -629,7 +727,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
 // One wave per block: a block's slots free as soon as its item ends, where a
 // 4-wave block holds its LDS until its slowest item ends (round 2 per-item
 // records: ~2 800 of 6 144 wave slots walking on average with 4).
-template <int W, bool PROF = false, bool HALF = false>
+template <int W, bool PROF = false, bool HALF = false, int NB = 1>
 __global__ __launch_bounds__(64, 6) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
@@ -652,8 +750,8 @@ __global__ __launch_bounds__(64, 6) void k_rootwalk(RayBase ray, int64_t n,
         memset(&P, 0, sizeof(P));
         P.root = (int32_t)q_node(it);
         P.slot = (int32_t)q_slot(it);
-        trav_packet<W, PROF, RayBase, HALF>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot, eps,
-                                            max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
+        trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot, eps,
+                                                max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
     }
 }
 

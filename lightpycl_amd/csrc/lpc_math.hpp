@@ -423,8 +423,8 @@ LPC_HD float filter_testh(float cx, float cy, float cz, float negB, float negA, 
     const float ww = wx * wx + wy * wy + wz * wz;
     const float q = negA + negB * ww;
     const float wn = wx * nx + wy * ny + wz * nz;
-    if (wn < 0.0f && wn * wn + (q + q) - LPC_HALF_MU2 * ww > 0.0f) return 1.0f;
-    return pp + q;
+    const float d = pp + q;
+    return ((wn < 0.0f) & (wn * wn + (q + q) - LPC_HALF_MU2 * ww > 0.0f)) ? 1.0f : d;   // a select, no branch
 }
 
 // Float-evaluation slack of filter_test, both ways (factor on A and B, and an

@@ -59,6 +59,8 @@ struct Pop {
 struct PieceTable {
     DBuf pieces, spieces;              // hierarchy pieces (k_rootwalk / k_intersect), sliver pieces (k_slivers)
     int32_t npieces = 0, nspieces = 0;
+    DBuf groups;                       // k_roots_s gate: the runs' root records, s_lo/s_hi = their pieces
+    int32_t ngroups = 0;               // 0: no gate (pieces are the run roots, or > 64 runs)
     std::vector<float> sdmin;          // per sliver piece (ascending): min dmin of its slivers
 };
 
@@ -100,6 +102,9 @@ struct lpc_handle {
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
+    bool roots_gate = true;                         // LPC_ROOTS_GATE: k_roots_s tests the run roots first
+    int walk_nb = 1;                                // LPC_WALK_NB: nodes per walk step (1 or LPC_NB, 8-wide only)
+    int max_levels = 0;                             // deepest run hierarchy (stack bound of the batched walk)
     int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
     bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
@@ -322,7 +327,7 @@ static FiltRec test_rec(float cx, float cy, float cz, float negB, float negA)
 
 static void drop_piece_tables(lpc_handle *h)
 {
-    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
+    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); dfree(kv.second.groups); }
     h->ptabs.clear();
 }
 
@@ -335,6 +340,7 @@ static int build_records(lpc_handle *h)
     int32_t n_nodes = 0;
     std::vector<SliverRec> slivers;
     h->run_levels.clear();
+    h->max_levels = 0;
     h->node_self.clear();
     h->run_slo.clear(); h->run_shi.clear();
     h->sliver_dmin_host.clear();
@@ -453,7 +459,8 @@ static int build_records(lpc_handle *h)
             ent.swap(up);
         } while (ent.size() > 1);
         // W-wide: at most W - 1 siblings wait per level on a wave's stack
-        if ((W - 1) * (int)levels.size() + 1 > LPC_STACK) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
+        if ((W - 1) * (int)levels.size() + 1 > LPC_STACK1) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
+        h->max_levels = std::max(h->max_levels, (int)levels.size());
         for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
             h->run_levels.back().push_back(it->first);
             h->run_levels.back().push_back(it->second);
@@ -509,13 +516,22 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
     }
     auto it = h->ptabs.find(cut);
     if (it != h->ptabs.end()) { *out = &it->second; return 0; }
-    std::vector<Piece> pcs, spc;
+    std::vector<Piece> pcs, spc, grp;
     std::vector<float> sdm;
     for (size_t r = 0; r < nr; ++r) {
         if (run_slot[r] < 0) continue;
         const std::vector<int32_t> &L = h->run_levels[r];
         if (!L.empty()) {
             const size_t lv = (size_t)cut[r];
+            Piece gp;                   // the run root's own test over the run's pieces
+            memset(&gp, 0, sizeof(gp));
+            gp.root = L[0];
+            const FiltRec &gt = h->node_self[(size_t)gp.root];
+            gp.cx = gt.cx; gp.cy = gt.cy; gp.cz = gt.cz; gp.negB = gt.negB; gp.negA = gt.negA;
+            gp.slot = run_slot[r];
+            gp.s_lo = (int32_t)pcs.size();
+            gp.s_hi = gp.s_lo + L[2 * lv + 1];
+            grp.push_back(gp);
             for (int32_t i = 0; i < L[2 * lv + 1]; ++i) {
                 Piece p;
                 memset(&p, 0, sizeof(p));
@@ -557,6 +573,13 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
     if (!spc.empty()) {
         RETIF(dalloc(h, t.spieces, spc.size() * sizeof(Piece)));
         HIPCHK(h, hipMemcpy(t.spieces.p, spc.data(), spc.size() * sizeof(Piece), hipMemcpyHostToDevice));
+    }
+    // the gate pays when the runs are cut below their roots (<= 64 runs: one mask)
+    t.ngroups = 0;
+    if (h->roots_gate && grp.size() <= 64 && grp.size() < pcs.size()) {
+        RETIF(dalloc(h, t.groups, grp.size() * sizeof(Piece)));
+        HIPCHK(h, hipMemcpy(t.groups.p, grp.data(), grp.size() * sizeof(Piece), hipMemcpyHostToDevice));
+        t.ngroups = (int32_t)grp.size();
     }
     *out = &t;
     return 0;
@@ -730,6 +753,13 @@ static void spill_level_args(lpc_handle *h, const SpillArgs &SP, int l, int leve
     O->budget = l + 1 < levels ? SP.budget : 0;
 }
 
+// The batched walk (LPC_WALK_NB > 1): 8-wide hierarchies whose stack bound
+// (NB W per level) fits LPC_STACK.
+static bool walk_batched(const lpc_handle *h)
+{
+    return h->walk_nb > 1 && h->built_w == 8 && LPC_NB * 8 * h->max_levels <= LPC_STACK;
+}
+
 // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
 // what exceeds the budget for level l + 1; the last level finishes
 static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
@@ -747,18 +777,21 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
         // 4-wave units, launched as single-wave blocks
         const unsigned g =
             (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l)) * 4u;
-#define LPC_LAUNCH_SPILL(WW, NT, PF, HF)                                                                         \
-    hipLaunchKernelGGL((k_spill<WW, PF, HF>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,                        \
+#define LPC_LAUNCH_SPILL(WW, NT, PF, HF, B)                                                                      \
+    hipLaunchKernelGGL((k_spill<WW, PF, HF, B>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,                     \
                        (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
                        I, O)
         // profiling counters only in the PROF instantiation (fewer live registers without)
         if (h->built_w == 8) {
-            if (stats) LPC_LAUNCH_SPILL(8, Node8, true, false);
-            else if (h->half_now) LPC_LAUNCH_SPILL(8, Node8, false, true);   // the half-line cull (LPC_HALF 1/2)
-            else LPC_LAUNCH_SPILL(8, Node8, false, false);
+            if (stats) LPC_LAUNCH_SPILL(8, Node8, true, false, 1);
+            else if (walk_batched(h)) {
+                if (h->half_now) LPC_LAUNCH_SPILL(8, Node8, false, true, LPC_NB);
+                else LPC_LAUNCH_SPILL(8, Node8, false, false, LPC_NB);
+            } else if (h->half_now) LPC_LAUNCH_SPILL(8, Node8, false, true, 1);   // the half-line cull (LPC_HALF 1/2)
+            else LPC_LAUNCH_SPILL(8, Node8, false, false, 1);
         } else {
-            if (stats) LPC_LAUNCH_SPILL(4, Node4, true, false);
-            else LPC_LAUNCH_SPILL(4, Node4, false, false);
+            if (stats) LPC_LAUNCH_SPILL(4, Node4, true, false, 1);
+            else LPC_LAUNCH_SPILL(4, Node4, false, false, 1);
         }
 #undef LPC_LAUNCH_SPILL
     }
@@ -824,11 +857,19 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     Q.err = (uint32_t *)((char *)h->d_acc.p + offsetof(DevAcc, qerr));
     Q.rcap = (uint32_t)rcap;
     if (h->host_prof)
-        fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d S %d pb %d blocks %lld rcap %lld\n",
-                (long long)n, (long long)npk, (int)pt->npieces, rs_S, rs_pb, (long long)rs_blocks, (long long)rcap);
-    if (roots_s)
-        hipLaunchKernelGGL(k_roots_s, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
-                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0, rs_S, rs_pb);
+        fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d groups %d S %d pb %d blocks %lld rcap %lld\n",
+                (long long)n, (long long)npk, (int)pt->npieces, (int)pt->ngroups, rs_S, rs_pb, (long long)rs_blocks,
+                (long long)rcap);
+    if (roots_s) {
+        if (h->half_roots)
+            hipLaunchKernelGGL(k_roots_s<true>, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
+                               (const Piece *)pt->pieces.p, (int)pt->npieces, (const Piece *)pt->groups.p,
+                               (int)pt->ngroups, Q, rs_S, rs_pb);
+        else
+            hipLaunchKernelGGL(k_roots_s<false>, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
+                               (const Piece *)pt->pieces.p, (int)pt->npieces, (const Piece *)pt->groups.p,
+                               (int)pt->ngroups, Q, rs_S, rs_pb);
+    }
     else if (pt->npieces <= 64)
         hipLaunchKernelGGL(k_roots_r, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
@@ -845,17 +886,20 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
-#define LPC_LAUNCH_WALK(WW, NT, PF, HF)                                                                          \
-    hipExtLaunchKernelGGL((k_rootwalk<WW, PF, HF>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,    \
+#define LPC_LAUNCH_WALK(WW, NT, PF, HF, B)                                                                       \
+    hipExtLaunchKernelGGL((k_rootwalk<WW, PF, HF, B>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm, \
                           (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,   \
                           stats, Q, SP)
     if (h->built_w == 8) {
-        if (stats) LPC_LAUNCH_WALK(8, Node8, true, false);
-        else if (h->half_now) LPC_LAUNCH_WALK(8, Node8, false, true);        // the half-line cull (LPC_HALF 1/2)
-        else LPC_LAUNCH_WALK(8, Node8, false, false);
+        if (stats) LPC_LAUNCH_WALK(8, Node8, true, false, 1);
+        else if (walk_batched(h)) {
+            if (h->half_now) LPC_LAUNCH_WALK(8, Node8, false, true, LPC_NB);
+            else LPC_LAUNCH_WALK(8, Node8, false, false, LPC_NB);
+        } else if (h->half_now) LPC_LAUNCH_WALK(8, Node8, false, true, 1);   // the half-line cull (LPC_HALF 1/2)
+        else LPC_LAUNCH_WALK(8, Node8, false, false, 1);
     } else {
-        if (stats) LPC_LAUNCH_WALK(4, Node4, true, false);
-        else LPC_LAUNCH_WALK(4, Node4, false, false);
+        if (stats) LPC_LAUNCH_WALK(4, Node4, true, false, 1);
+        else LPC_LAUNCH_WALK(4, Node4, false, false, 1);
     }
 #undef LPC_LAUNCH_WALK
     if (h->prof) h->ev_kern.push_back({k0, k1});
@@ -1169,6 +1213,8 @@ int lpc_open(int device, lpc_handle **out)
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
+    h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
+    h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
     h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
@@ -1237,7 +1283,7 @@ int lpc_close(lpc_handle *h)
     h->acc_host = nullptr;
     if (h->acc_map) (void)hipHostFree(h->acc_map);
     h->acc_map = h->acc_map_dev = nullptr;
-    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); }
+    for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); dfree(kv.second.groups); }
     prof_resolve(h);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->stream2) { (void)hipStreamSynchronize(h->stream2); (void)hipStreamDestroy(h->stream2); }

@@ -96,6 +96,10 @@ _POLICIES = [
     dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"), dict(LPC_SLIVER_LATE="0"),
     dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_SHADE_KU="0"),
     dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
+    dict(LPC_ROOTS_GATE="0"), dict(LPC_ROOTS_GATE="0", LPC_Q_TARGET="10000000"), dict(LPC_Q_TARGET="3000000"),
+    # the batched walk (LPC_NB nodes per step), with hand-over queues that overflow
+    dict(LPC_WALK_NB="4"), dict(LPC_WALK_NB="4", LPC_BUDGET="2", LPC_SPILL_CAP="100"),
+    dict(LPC_WALK_NB="4", LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
     # work hand-over: budgets, a queue that overflows
     dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_BUDGET="0"),
     dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
