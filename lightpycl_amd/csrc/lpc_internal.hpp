@@ -166,8 +166,22 @@ struct CompactArgs {
 // k_stage_move, see lpc_kernels.hip).  Tile counts are packed in one word:
 // reflected | refracted << 9 | measured << 18 (each <= LPC_ST_TILE).
 #define LPC_ST_TILE 256                   // rays per staging tile (k_shade_stage / k_stage_move block)
+// Device-sized iterations (trace_run's speculative enqueue):
+// what the iteration of sequence parity p reads -- its population size, the
+// measured record's length before it, its rays' max |D|^2 -- written by the
+// previous iteration's k_stage_move (n 0: the trace ended, or a kept direction
+// exceeded Dcap: dcap_hit, the host rebuilds the records and re-runs).
+struct IterCtl {
+    long long n[2];
+    unsigned long long m[2];
+    unsigned int dm2[2];
+    unsigned int dcap_hit;
+    unsigned int pad;
+};
+
 struct StageArgs {
     ShadeArgs S;                      // shading inputs (S.o unused)
+    const long long *nd;              // device-sized launch: S.n read here (NULL: S.n)
     float *stR, *stT;                 // staged kept children: 8 arrays each (ox..pw | pmid), stride cst
     float *stM;                       // staged measured rays: x y z pw | mesh, stride cst
     int64_t cst;
@@ -209,6 +223,11 @@ struct MoveArgs {
     int64_t ngroups;
     unsigned long long *gsum_next;    // the next launch's group counts: its first gdirty_next (left by the
     int64_t gdirty_next;              //   launch before this one) zeroed here
+    IterCtl *ctl;                     // NULL, or the next iteration's size is written here
+    int par;                          // this iteration's parity in ctl (k_stage_move<true>: ntiles,
+                                      //   ngroups and m_base from ctl[par] as well)
+    double thr;                       // trace_run's power threshold (-inf: none)
+    double dcap2;                     // Dcap^2 (1 - 1e-6), check_dcap's bound
 };
 
 struct PostprocAosArgs {

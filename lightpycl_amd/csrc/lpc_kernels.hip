@@ -82,12 +82,9 @@ static __device__ __forceinline__ T wave_red(T v, int op)   // 0 min, 1 max, 2 s
 // w*64*RPL + r*64 + lane on lane `lane`, the map of k_intersect (RPL 1) and
 // k_slivers (RPL 2)).
 template <int RPL>
-__global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                PacketRec *__restrict__ pk)
+static __device__ __forceinline__ void packet_bound(const RaysIn &R, const float *__restrict__ rs, int64_t n,
+                                                    PacketRec *__restrict__ pk, int64_t w, int lane)
 {
-    const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w * 64 * RPL >= n) return;
     int64_t q[RPL];
     for (int r = 0; r < RPL; ++r) {
         const int64_t s = w * 64 * RPL + r * 64 + lane;
@@ -135,6 +132,18 @@ __global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restric
     packet_angle_finish(ang, fin != 0, Q);
     for (int k = 0; k < 5; ++k) Q.pad[k] = 0;
     if (lane == 0) pk[w] = Q;
+}
+
+// nd != NULL: a device-sized launch (the population size read on the device,
+// grid-stride over the packets; trace_run's speculative iterations).
+template <int RPL>
+__global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restrict__ rs, int64_t n,
+                                                PacketRec *__restrict__ pk, const long long *__restrict__ nd)
+{
+    if (nd) n = *nd;
+    const int lane = threadIdx.x & 63;
+    for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w * 64 * RPL < n; w += (int64_t)gridDim.x * 4)
+        packet_bound<RPL>(R, rs, n, pk, w, lane);
 }
 
 // Per-ray nearest-hit state and its flush into the run's slot (original ray
@@ -503,9 +512,10 @@ __global__ __launch_bounds__(64, 6) void k_spill(RayBase ray, int64_t n,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                unsigned long long *__restrict__ stats, SpillArgs SP,
-                                               SpillArgs out)
+                                               SpillArgs out, const long long *__restrict__ nd)
 {
     __shared__ WaveLds lds;
+    if (nd) n = *nd;
     const uint32_t total = min(*SP.ctr, SP.cap);
     const uint32_t stride = gridDim.x;
     for (uint32_t it = blockIdx.x; it < total; it += stride) {
@@ -649,20 +659,44 @@ static __device__ __forceinline__ uint64_t wave_or64(uint64_t v)
            (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
 }
 
+// Grid-stride over the virtual blocks (pb packets each; device-sized launches
+// read n on the device, nd != NULL).
+template <bool HALF>
+static __device__ __forceinline__ void roots_block(const RaysIn &R, const float *__restrict__ rs, int64_t n,
+                                                   const Piece *__restrict__ pieces, int npieces,
+                                                   const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
+                                                   int S, int pb, int64_t vb, unsigned long long *s_m,
+                                                   uint32_t *s_off);
+
 template <bool HALF>
 __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                  const Piece *__restrict__ pieces, int npieces,
                                                  const Piece *__restrict__ groups, int ngroups, QueueArgs Q,
-                                                 int S, int pb)
+                                                 int S, int pb, const long long *__restrict__ nd)
 {
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
+    if (nd) n = *nd;
+    const int64_t nvb = ((n + 63) / 64 + pb - 1) / pb;
+    for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off);
+        __syncthreads();                          // s_m / s_off reused by the next virtual block
+    }
+}
+
+template <bool HALF>
+static __device__ __forceinline__ void roots_block(const RaysIn &R, const float *__restrict__ rs, int64_t n,
+                                                   const Piece *__restrict__ pieces, int npieces,
+                                                   const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
+                                                   int S, int pb, int64_t vb, unsigned long long *s_m,
+                                                   uint32_t *s_off)
+{
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int c = q_shard(blockIdx.x);
+    const int c = q_shard((uint32_t)vb);
     const int ntask = S * pb;
     for (int t = wv; t < ntask; t += 4) {
-        const int64_t w = (int64_t)blockIdx.x * pb + t / S;
+        const int64_t w = vb * pb + t / S;
         const int cls = t % S;
         uint64_t m = 0;
         if (w * 64 < n) {
@@ -710,7 +744,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
     for (int t = wv; t < ntask; t += 4) {
         const uint64_t m = s_m[t];
         if (!((m >> lane) & 1ull)) continue;
-        const int64_t w = (int64_t)blockIdx.x * pb + t / S;
+        const int64_t w = vb * pb + t / S;
         const int p = t % S + S * lane;
         const uint32_t pos = base + s_off[t] + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
         if (pos < Q.rcap)
@@ -734,9 +768,10 @@ __global__ __launch_bounds__(64, 6) void k_rootwalk(RayBase ray, int64_t n,
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                      unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                      unsigned long long *__restrict__ stats, QueueArgs Q,
-                                                     SpillArgs out)
+                                                     SpillArgs out, const long long *__restrict__ nd)
 {
     __shared__ WaveLds lds;
+    if (nd) n = *nd;
     uint32_t pre[LPC_Q_CSHARDS + 1];
     pre[0] = 0;
 #pragma unroll
@@ -762,6 +797,9 @@ __global__ __launch_bounds__(64, 6) void k_rootwalk(RayBase ray, int64_t n,
 // loads), then, for the slivers that pass, the per-ray line filter and the exact
 // test.  Most (packet, piece) pairs fail the packet test, so a wave's fixed cost
 // (sliver records, loop setup) is spread over ppw packets.
+// Device-sized launch (nd != NULL): the population size and its max |D|^2 (dm2d,
+// float bits) read on the device, ppw = the packets over the grid's waves, and
+// every sliver piece in grid.y (a piece whose slivers no ray can pass exits).
 __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restrict__ rs, int64_t n,
                                                  const int32_t *__restrict__ perm,
                                                  const PacketRec *__restrict__ pk,
@@ -770,9 +808,16 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
                                                  unsigned long long *__restrict__ skey,
                                                  int32_t *__restrict__ scnt,
                                                  unsigned long long *__restrict__ stats, int ppw,
-                                                 float dmax)
+                                                 float dmax, const long long *__restrict__ nd,
+                                                 const unsigned *__restrict__ dm2d)
 {
     const int lane = threadIdx.x & 63;
+    if (nd) {
+        n = *nd;
+        const double d2 = (double)__uint_as_float(*dm2d);
+        dmax = d2 >= 0.0 ? (float)fmin(sqrt(d2 * (1.0 + 1e-5)), (double)INFINITY) : INFINITY;   // as run_intersect
+        ppw = (int)max((int64_t)1, ((n + 127) / 128 + (int64_t)gridDim.x * 4 - 1) / ((int64_t)gridDim.x * 4));
+    }
     const int64_t npk = (n + 127) / 128;
     const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
     if (w0 >= npk) return;
@@ -783,6 +828,7 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
     if (j < P.s_hi) S = srec[j];
     else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
     if (!(S.dmin <= dmax)) S.a = NAN;             // no ray of the launch can pass its DEN test
+    if (!any_lane(S.a == S.a)) return;            // the whole piece culled
     const int64_t o = (int64_t)P.slot * n;
     uint32_t n_tests = 0, n_exact = 0;
     for (int64_t w = w0; w < w1; ++w) {
@@ -1271,7 +1317,7 @@ __global__ __launch_bounds__(256) void k_scatter(CompactArgs A)
 //                  sum) and publishes them to the host.
 // Children and measured rays land at the same positions as with the four
 // kernels ([reflected ; refracted], each in parent order).
-template <int KU>
+template <int KU, bool DS>
 __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
 {
     __shared__ double s_mp[LPC_MP_MAX][LPC_ST_TILE / 64];
@@ -1279,9 +1325,13 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     __shared__ double s_pow[LPC_ST_TILE / 64];
     __shared__ float s_dm[LPC_ST_TILE / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t tile = blockIdx.x;
+    // the shading inputs as a local (a device-sized launch sets its n; writing the
+    // kernel argument itself would put the whole argument block in scratch)
+    ShadeArgs S = A.S;
+    if constexpr (DS) S.n = *A.nd;
+    auto tile_body = [&](const int64_t tile) {
     const int64_t r = tile * LPC_ST_TILE + threadIdx.x;
-    const bool in = r < A.S.n;
+    const bool in = r < S.n;
     PostOut po;
     po.hit_mesh = -1;
     f3 dest = mk3(0.0f, 0.0f, 0.0f);
@@ -1290,19 +1340,19 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     s.r_meas = -1; s.t_meas = -1;
     if (in) {
         uint64_t touched = 0;
-        s = shade_eval<KU>(A.S, r, po, dest, &touched);
+        s = shade_eval<KU>(S, r, po, dest, &touched);
         // the slots just read back to the clean state: those a flush wrote (noted
         // while postproc read them; slots 64 and up are read again)
-        const unsigned long long k0 = slot_key(A.S.max_ray_len, -1);
+        const unsigned long long k0 = slot_key(S.max_ray_len, -1);
         while (touched) {
             const int j = __builtin_ctzll(touched);
             touched &= touched - 1;
-            const int64_t a = (int64_t)j * A.S.n + r;
+            const int64_t a = (int64_t)j * S.n + r;
             A.skey[a] = k0;
             A.scnt[a] = 0;
         }
-        for (int32_t j = 64; j < A.S.K; ++j) {
-            const int64_t a = (int64_t)j * A.S.n + r;
+        for (int32_t j = 64; j < S.K; ++j) {
+            const int64_t a = (int64_t)j * S.n + r;
             if (A.skey[a] != k0) A.skey[a] = k0;
             if (A.scnt[a] != 0) A.scnt[a] = 0;
         }
@@ -1367,8 +1417,19 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
         A.tdm[tile] = __float_as_uint(td);
         if (cR | cT | cM) atomicAdd(&A.gsum[tile / LPC_ST_GROUP], gsum_pack(cR, cT, cM));
     }
+    };
+    if constexpr (!DS) {
+        tile_body(blockIdx.x);                    // one tile per block
+    } else {                                      // device-sized: grid-stride over the tiles
+        const int64_t ntiles = (S.n + LPC_ST_TILE - 1) / LPC_ST_TILE;
+        for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+            tile_body(tile);
+            __syncthreads();                      // the shared sums are reused by the next tile
+        }
+    }
 }
 
+template <bool DS>
 __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
 {
     __shared__ long long s_red[LPC_ST_TILE / 64][6];
@@ -1377,13 +1438,24 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     __shared__ float s_d[LPC_ST_TILE];
     __shared__ double s_m[LPC_MP_MAX][LPC_ST_TILE];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int64_t tile = blockIdx.x;
+    // device-sized launch (DS): the population size and measured-record length
+    // the previous iteration left in A.ctl; grid-stride over the tiles (tile 0's
+    // block also publishes an empty iteration's counters)
+    int64_t ntiles = A.ntiles, ngroups = A.ngroups;
+    unsigned long long m_base = A.m_base;
+    if constexpr (DS) {
+        const long long n = A.ctl->n[A.par];
+        ntiles = (n + LPC_ST_TILE - 1) / LPC_ST_TILE;
+        ngroups = (ntiles + LPC_ST_GROUP - 1) / LPC_ST_GROUP;
+        m_base = A.ctl->m[A.par];
+    }
+    auto tile_body = [&](const int64_t tile) {
     // this tile's prefix and the totals: the group counts (the groups before this
     // tile's, all groups), then this group's tiles before it
     long long pre[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
     const int64_t g = tile / LPC_ST_GROUP;
     const unsigned long long m21 = (1ull << 21) - 1ull;
-    for (int64_t k = t; k < A.ngroups; k += LPC_ST_TILE) {
+    for (int64_t k = t; k < ngroups; k += LPC_ST_TILE) {
         const unsigned long long v = A.gsum[k];
         const long long c[3] = {(long long)(v & m21), (long long)((v >> 21) & m21), (long long)((v >> 42) & m21)};
         for (int f = 0; f < 3; ++f) {
@@ -1413,7 +1485,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         // iteration counters: fixed-order power sum, max |dir|^2
         double lp = 0.0, lm[LPC_MP_MAX] = {0.0, 0.0, 0.0, 0.0};
         float ld = 0.0f;
-        for (int64_t j = t; j < A.ntiles; j += LPC_ST_TILE) {
+        for (int64_t j = t; j < ntiles; j += LPC_ST_TILE) {
             lp += A.tpow[j];
             ld = fmaxf(ld, __uint_as_float(A.tdm[j]));
             for (int m = 0; m < A.nmp; ++m) lm[m] += A.tmp[j * LPC_MP_MAX + m];
@@ -1434,16 +1506,28 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
             DevAcc a;
             memset(&a, 0, sizeof(a));
             for (int m = 0; m < A.nmp; ++m) {         // the trace's running sums, in iteration order
-                A.mrun[m] = (A.m_base == 0 ? 0.0 : A.mrun[m]) + s_m[m][0];
+                A.mrun[m] = (m_base == 0 ? 0.0 : A.mrun[m]) + s_m[m][0];
                 a.mpow[m] = A.mrun[m];
             }
             a.nR = (unsigned long long)s_tot[0]; a.nT = (unsigned long long)s_tot[1];
-            a.m_total = A.m_base + (unsigned long long)s_tot[2];
+            a.m_total = m_base + (unsigned long long)s_tot[2];
             a.nM_iter = (unsigned long long)s_tot[2];
             a.pow_next = s_p[0];
             a.dmax2_bits = __float_as_uint(s_d[0]);
             a.qerr = A.acc->qerr;
             *A.acc = a;
+            if (A.ctl) {
+                // the next iteration's size for device-sized launches: 0 once the
+                // trace ends (trace_run's rules, iterative_tracer.py:383-391) or a
+                // kept direction exceeds the filter records' Dcap (the host rebuilds)
+                const unsigned long long kept = a.nR + a.nT;
+                const bool dc = !((double)s_d[0] <= A.dcap2);
+                const bool stop = a.pow_next < A.thr || kept == 0 || dc;
+                A.ctl->n[A.par ^ 1] = stop ? 0 : (long long)kept;
+                A.ctl->m[A.par ^ 1] = a.m_total;
+                A.ctl->dm2[A.par ^ 1] = a.dmax2_bits;
+                if (dc && kept) A.ctl->dcap_hit = 1u;
+            }
             if (A.host_acc) {
                 // publish to the mapped host copy, the sequence number last: the
                 // host launches the next iteration while the rows still move
@@ -1470,7 +1554,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     }
     // this tile's staged rows into place: kept children (two per thread at most,
     // loads of both issued before the stores), then measured rays
-    const uint32_t v = A.tcnt[tile];
+    const uint32_t v = tile < ntiles ? A.tcnt[tile] : 0u;
     const int cR = (int)(v & 511u), cT = (int)((v >> 9) & 511u), cM = (int)((v >> 18) & 511u);
     const int64_t c = A.cst, cb = A.capR, cm = A.capM, s0 = tile * LPC_ST_TILE;
     float row[2][8];
@@ -1499,9 +1583,18 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         for (int a = 0; a < 8; ++a) A.popR[a * cb + dst[h]] = row[h][a];
     }
     if (hasM) {
-        const int64_t d = (int64_t)A.m_base + s_pre[2] + t;
+        const int64_t d = (int64_t)m_base + s_pre[2] + t;
 #pragma unroll
         for (int a = 0; a < 5; ++a) A.mrec[a * cm + d] = mrow[a];
+    }
+    };
+    if constexpr (!DS) {
+        tile_body(blockIdx.x);                    // one tile per block
+    } else {
+        for (int64_t tile = blockIdx.x; tile < max(ntiles, (int64_t)1); tile += gridDim.x) {
+            tile_body(tile);
+            __syncthreads();                      // s_red / s_pre / s_tot reused by the next tile
+        }
     }
 }
 

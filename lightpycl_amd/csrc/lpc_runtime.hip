@@ -66,6 +66,7 @@ struct PieceTable {
 
 const int kShadeF = 12;   // float arrays of the shade outputs
 const int kShadeI = 8;    // int arrays
+const int kAccRing = 8;   // mapped counter slots (iterations in flight: at most 2)
 
 }  // namespace
 
@@ -91,6 +92,7 @@ struct lpc_handle {
     std::vector<int32_t> meas_meshes;
     DBuf d_nodes, d_srec, d_xrec, d_verts, d_mat, d_ior, d_refl, d_diss;
     double dcap = 16.0;
+    double dcap_init = 16.0;                        // LPC_DCAP_MILLI / 1000 (tests: a rebuild inside a trace)
     std::map<std::vector<int32_t>, PieceTable> ptabs;   // by the hierarchy level each live run is cut at
     // workspace
     int64_t chunk = 0;                              // rays per chunk (0 -> default)
@@ -101,6 +103,7 @@ struct lpc_handle {
     int64_t onesweep_min = 500000;                  // onesweep radix sort from this many rays (merge sort below)
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
+    int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     bool roots_gate = true;                         // LPC_ROOTS_GATE: k_roots_s tests the run roots first
     int walk_nb = 1;                                // LPC_WALK_NB: nodes per walk step (1 or LPC_NB, 8-wide only)
@@ -156,13 +159,23 @@ struct lpc_handle {
     int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
     DBuf w_qroots;                                  // root items
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
-    DevAcc *acc_map = nullptr, *acc_map_dev = nullptr;   // mapped pinned copy k_scan publishes (+ device address)
+    DevAcc *acc_map = nullptr, *acc_map_dev = nullptr;   // mapped pinned ring k_scan / k_stage_move publish into
+                                                    // (slot seq % kAccRing; + device address)
+    // speculative iterations (trace_run, LPC_SPEC): iteration i + 1 is enqueued
+    // device-sized (IterCtl) before iteration i's counters are read
+    bool spec = true;
+    DBuf d_ctl;                                     // IterCtl
+    int ctl_par = 0;                                // the parity the next enqueued iteration reads
+    double ds_thr = -INFINITY;                      // trace_run's power threshold (k_stage_move's stop rule)
+    std::vector<double> hist_r;                     // the last trace_run's populations / its first (the
+    int32_t hist_iter = -1;                         //   speculation's prediction) and its iteration limit
+    bool dcap_rebuilt = false;                      // check_dcap rebuilt the records (a speculative iteration is void)
     unsigned int acc_seq = 0;
     bool early_acc = true;                          // LPC_EARLY_ACC: read the counters before k_scatter ends
     bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
     hipEvent_t ev_side[2] = {nullptr, nullptr};     // rays ready (main -> side), slivers done (side -> main)
-    double host_last = 0.0, t_first = 0.0;
+    double host_last = 0.0;
     bool pop_init = false;                          // the population is I (the emitted rays, set_rays)
     bool mp_valid = false;                          // mp_last = the trace's measured power per measure mesh
     DBuf d_mrun;                                    // its running sums on the device (k_stage_move)
@@ -227,6 +240,16 @@ static int set_err(lpc_handle *h, int code, const std::string &msg)
         else if (K_ <= 12) hipLaunchKernelGGL(KERN<12>, grid, block, 0, stream, __VA_ARGS__);    \
         else if (K_ <= 16) hipLaunchKernelGGL(KERN<16>, grid, block, 0, stream, __VA_ARGS__);    \
         else hipLaunchKernelGGL(KERN<0>, grid, block, 0, stream, __VA_ARGS__);                   \
+    } while (0)
+
+#define LPC_KU_LAUNCH2(h, KERN, B, grid, block, stream, ...)                                      \
+    do {                                                                                         \
+        const int K_ = (h)->shade_ku ? (h)->K : 1 << 30;                                         \
+        if (K_ <= 4) hipLaunchKernelGGL((KERN<4, B>), grid, block, 0, stream, __VA_ARGS__);      \
+        else if (K_ <= 8) hipLaunchKernelGGL((KERN<8, B>), grid, block, 0, stream, __VA_ARGS__); \
+        else if (K_ <= 12) hipLaunchKernelGGL((KERN<12, B>), grid, block, 0, stream, __VA_ARGS__); \
+        else if (K_ <= 16) hipLaunchKernelGGL((KERN<16, B>), grid, block, 0, stream, __VA_ARGS__); \
+        else hipLaunchKernelGGL((KERN<0, B>), grid, block, 0, stream, __VA_ARGS__);              \
     } while (0)
 
 // Wait for a trace's kernels still queued on the stream: lpc_trace_iterate and
@@ -593,6 +616,7 @@ using RaySortCfg = rocprim::default_config;
 using RaySortOnesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                    rocprim::default_config, 0>;
 
+
 // Rays per chunk.  Default: as many as ~32 GB of per-chunk workspace holds (slots
 // 12 B per mesh + ~200 B of coherence copies, shade outputs and sort buffers per
 // ray), at most 128 Mi: a chunk is also the unit of the coherence sort, and large
@@ -683,28 +707,32 @@ static hipEvent_t ev_get(lpc_handle *h)
 // Resolve recorded event pairs (after a stream sync).
 static void prof_resolve(lpc_handle *h)
 {
-    for (auto &pr : h->ev_isect) {
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_isect_ms += ms;
-        h->ev_pool.push_back(pr.first);
-        h->ev_pool.push_back(pr.second);
-    }
-    h->ev_isect.clear();
-    for (auto &pr : h->ev_kern) {
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_kern_ms += ms;
-        h->ev_pool.push_back(pr.first);
-        h->ev_pool.push_back(pr.second);
-    }
-    h->ev_kern.clear();
-    for (auto &pr : h->ev_rest) {
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) h->prof_rest_ms += ms;
-        h->ev_pool.push_back(pr.first);
-        h->ev_pool.push_back(pr.second);
-    }
-    h->ev_rest.clear();
+    // pairs whose end has not happened yet (a speculative iteration still queued)
+    // stay for a later call
+    auto drain = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, double &acc) {
+        size_t keep = 0;
+        for (auto &pr : v) {
+            if (hipEventQuery(pr.second) == hipErrorNotReady) { v[keep++] = pr; continue; }
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) acc += ms;
+            h->ev_pool.push_back(pr.first);
+            h->ev_pool.push_back(pr.second);
+        }
+        v.resize(keep);
+    };
+    drain(h->ev_isect, h->prof_isect_ms);
+    drain(h->ev_kern, h->prof_kern_ms);
+    drain(h->ev_rest, h->prof_rest_ms);
 }
+
+// Device-sized launch of a population whose size the previous iteration left in
+// IterCtl (run_intersect / run_queue / run_spill_levels; NULL: host-sized).
+struct DevSize {
+    const long long *nd;        // population size (device)
+    const unsigned *dm2;        // its max |D|^2 (float bits, device)
+    int64_t pred;               // expected size: piece level, budgets, grids
+    int64_t bound;              // capacity bound: workspaces, root-item shards
+};
 
 // Work hand-over (k_spill levels): queue, budget by population size.
 static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
@@ -764,7 +792,7 @@ static bool walk_batched(const lpc_handle *h)
 // what exceeds the budget for level l + 1; the last level finishes
 static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
                             float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
-                            unsigned long long *stats, const SpillArgs &SP)
+                            unsigned long long *stats, const SpillArgs &SP, const long long *nd = nullptr)
 {
     uint32_t *misc = (uint32_t *)h->d_misc.p;
     RayBase ray;
@@ -780,7 +808,7 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
 #define LPC_LAUNCH_SPILL(WW, NT, PF, HF, B)                                                                      \
     hipLaunchKernelGGL((k_spill<WW, PF, HF, B>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,                     \
                        (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
-                       I, O)
+                       I, O, nd)
         // profiling counters only in the PROF instantiation (fewer live registers without)
         if (h->built_w == 8) {
             if (stats) LPC_LAUNCH_SPILL(8, Node8, true, false, 1);
@@ -836,19 +864,22 @@ static int check_qerr(lpc_handle *h)
 // and hands heavy subtrees to the k_spill levels.
 static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
                      const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
-                     unsigned long long *stats)
+                     unsigned long long *stats, const DevSize *ds = nullptr)
 {
+    // device-sized (ds): n is the expected size (grids), the bound sizes the shards
     const int64_t npk = (n + 63) / 64;
     const int64_t rblocks = (npk + 3) / 4;
-    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 4), pb packets per block
+    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 4; device-sized S <= 16), pb packets per block
     const int rs_S = (int)((pt->npieces + 63) / 64);
-    const bool roots_s = h->roots_s > 0 && rs_S <= 4;
+    const bool roots_s = h->roots_s > 0 && (rs_S <= 4 || (ds && rs_S <= LPC_ROOTS_TASKS));
+    if (ds && !roots_s) return set_err(h, LPC_E_STATE, "internal: device-sized root tests need k_roots_s");
     const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? 1 : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
     const int64_t rs_blocks = roots_s ? (npk + rs_pb - 1) / rs_pb : 0;
+    const int64_t rs_vblocks = !ds ? rs_blocks : (((ds->bound + 63) / 64) + rs_pb - 1) / rs_pb;
     // per shard: at most its blocks' packets x pieces items (k_roots* flag an
     // overflow through Q.err instead of dropping items silently)
     const int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
-                                  ((rs_blocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+                                  ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
     if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "root items: too many per shard");
     RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
     QueueArgs Q;
@@ -862,13 +893,13 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
                 (long long)rcap);
     if (roots_s) {
         if (h->half_roots)
-            hipLaunchKernelGGL(k_roots_s<true>, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
-                               (const Piece *)pt->pieces.p, (int)pt->npieces, (const Piece *)pt->groups.p,
-                               (int)pt->ngroups, Q, rs_S, rs_pb);
+            hipLaunchKernelGGL(k_roots_s<true>, dim3((unsigned)std::max<int64_t>(rs_blocks, 1)), dim3(256), 0,
+                               h->stream, in, rs, n, (const Piece *)pt->pieces.p, (int)pt->npieces,
+                               (const Piece *)pt->groups.p, (int)pt->ngroups, Q, rs_S, rs_pb, ds ? ds->nd : nullptr);
         else
-            hipLaunchKernelGGL(k_roots_s<false>, dim3((unsigned)rs_blocks), dim3(256), 0, h->stream, in, rs, n,
-                               (const Piece *)pt->pieces.p, (int)pt->npieces, (const Piece *)pt->groups.p,
-                               (int)pt->ngroups, Q, rs_S, rs_pb);
+            hipLaunchKernelGGL(k_roots_s<false>, dim3((unsigned)std::max<int64_t>(rs_blocks, 1)), dim3(256), 0,
+                               h->stream, in, rs, n, (const Piece *)pt->pieces.p, (int)pt->npieces,
+                               (const Piece *)pt->groups.p, (int)pt->ngroups, Q, rs_S, rs_pb, ds ? ds->nd : nullptr);
     }
     else if (pt->npieces <= 64)
         hipLaunchKernelGGL(k_roots_r, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
@@ -889,7 +920,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
 #define LPC_LAUNCH_WALK(WW, NT, PF, HF, B)                                                                       \
     hipExtLaunchKernelGGL((k_rootwalk<WW, PF, HF, B>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm, \
                           (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,   \
-                          stats, Q, SP)
+                          stats, Q, SP, ds ? ds->nd : nullptr)
     if (h->built_w == 8) {
         if (stats) LPC_LAUNCH_WALK(8, Node8, true, false, 1);
         else if (walk_batched(h)) {
@@ -903,18 +934,23 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     }
 #undef LPC_LAUNCH_WALK
     if (h->prof) h->ev_kern.push_back({k0, k1});
-    return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP);
+    return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP, ds ? ds->nd : nullptr);
 }
 
 // intersect for n rays of `in` into the slot arrays, and optionally into a
 // caller's [ray][mesh] buffers (st_user != NULL, the reference's scratch layout).
 // traced != NULL (trace iterations without per-ray exports): the launch works in
 // its coherence order and *traced receives the rays in that order.
+// ds != NULL (a speculative trace iteration, chained traced population): n is
+// the bound, the kernels read the population size on the device and the
+// launch shapes follow ds->pred.
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
                          float *st_user, int32_t *si_user, int32_t *sc_user,
-                         double dmax2 = INFINITY, RaysIn *traced = nullptr)
+                         double dmax2 = INFINITY, RaysIn *traced = nullptr, const DevSize *ds = nullptr)
 {
     RETIF(ensure_ws(h, n));
+    const int64_t nb = n;                          // capacity
+    if (ds) n = std::max<int64_t>(1, std::min(ds->pred, nb));   // launch shapes
     PieceTable *pt;
     RETIF(piece_table(h, n, &pt));
     const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
@@ -970,7 +1006,6 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(n, LPC_MISC_WORDS))), dim3(256), 0, h->stream,
                            n, SI);
     }
-    if (h->host_prof && h->t_first == 0.0) h->t_first = host_us();
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
     if (sorted) {
@@ -991,8 +1026,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
                                                                  (size_t)n, b0, b1, h->stream));
         else
-            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n, b0,
-                                                            b1, h->stream));
+            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
+                                                            b0, b1, h->stream));
         perm = vout;
         hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
                            perm, (float *)h->w_rs.p, traced ? 1 : 0);
@@ -1016,8 +1051,12 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (!(dmax2 >= 0.0)) dmax2 = INFINITY;          // NaN bound (a NaN direction): no culling
     const float dmax = (float)std::min<double>(sqrt(dmax2 * (1.0 + 1e-5)), (double)INFINITY);
     int32_t nsp = 0;
-    while (nsp < pt->nspieces && (h->sliver_cull == 0 || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
+    while (nsp < pt->nspieces && (ds || h->sliver_cull == 0 || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
     const float dmax_k = h->sliver_cull ? dmax : INFINITY;
+    // device-sized: the population's max |D| read on the device (every sliver piece
+    // in the grid, culled there)
+    const unsigned *dm2_dev = ds && h->sliver_cull ? ds->dm2 : nullptr;
+    const long long *nd_dev = ds ? ds->nd : nullptr;
     // the slivers run beside the hierarchy stage on a second stream (both only
     // add to the slots with order-independent atomics); joined at the end
     hipStream_t ss = h->stream;
@@ -1038,10 +1077,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                                   : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
             const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
             hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
-                               (PacketRec *)h->w_pk.p);
+                               (PacketRec *)h->w_pk.p, nd_dev);
             hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
                                (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw, dmax_k);
+                               scnt, stats, (int)ppw, dmax_k, nd_dev, dm2_dev);
             HIPCHK(h, hipGetLastError());
         }
         if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
@@ -1056,13 +1095,16 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (h->queue == 2 && !h->prof_waves) {
         PieceTable *ptq;
         RETIF(piece_table(h, n, &ptq, q_level(h, n)));
-        qpath = (n + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS && (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES &&
+        // device-sized: at most 16 root-test classes (k_roots_s), else the run roots
+        if (ds && ptq->npieces > 64 * LPC_ROOTS_TASKS) RETIF(piece_table(h, n, &ptq, 1));
+        qpath = (nb + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS && (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES &&
                 h->K <= LPC_Q_MAX_SLOTS;
         if (qpath) {
             pt = ptq;                   // same sliver pieces at every level
-            if (pt->npieces > 0) RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats));
+            if (pt->npieces > 0) RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds));
         }
     }
+    if (ds && !qpath) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the root-item path");
     if (pt->npieces > 0 && !qpath) {
         // k_intersect: one wave per (packet, piece) (LPC_QUEUE=0, per-wave records)
         uint32_t *wrec = nullptr;
@@ -1149,6 +1191,7 @@ static int check_dcap(lpc_handle *h, double dmax2)
 {
     if (dmax2 <= h->dcap * h->dcap * (1.0 - 1e-6)) return 0;
     h->dcap = INFINITY;
+    h->dcap_rebuilt = true;
     return build_records(h);
 }
 
@@ -1192,7 +1235,10 @@ int lpc_open(int device, lpc_handle **out)
     if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
     rc = dalloc(h, h->d_mrun, LPC_MP_MAX * sizeof(double));
     if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
-    if (hipMemset(h->d_acc.p, 0, sizeof(DevAcc)) != hipSuccess) {    // counters start empty (qerr 0)
+    rc = dalloc(h, h->d_ctl, sizeof(IterCtl));
+    if (rc) { g_open_err = h->err; lpc_close(h); return rc; }
+    if (hipMemset(h->d_acc.p, 0, sizeof(DevAcc)) != hipSuccess ||   // counters start empty (qerr 0)
+        hipMemset(h->d_ctl.p, 0, sizeof(IterCtl)) != hipSuccess) {
         g_open_err = "counter init";
         lpc_close(h);
         return LPC_E_HIP;
@@ -1215,6 +1261,8 @@ int lpc_open(int device, lpc_handle **out)
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
     h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
     h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);
+    h->spec = env_int("LPC_SPEC", h->spec) != 0;
+    h->dcap_init = (double)env_int("LPC_DCAP_MILLI", 16000) / 1000.0;
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
     h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
@@ -1249,13 +1297,13 @@ int lpc_open(int device, lpc_handle **out)
             h->ev_side[0] = h->ev_side[1] = nullptr;
         }
     }
-    if (hipHostMalloc((void **)&h->acc_map, sizeof(DevAcc), hipHostMallocMapped | hipHostMallocCoherent) !=
+    if (hipHostMalloc((void **)&h->acc_map, kAccRing * sizeof(DevAcc), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
         hipHostGetDevicePointer((void **)&h->acc_map_dev, h->acc_map, 0) != hipSuccess) {
         h->acc_map = h->acc_map_dev = nullptr;       // counters then come by copy + stream sync
         h->early_acc = false;
     } else {
-        memset(h->acc_map, 0, sizeof(DevAcc));
+        memset(h->acc_map, 0, kAccRing * sizeof(DevAcc));
     }
     if (hipHostMalloc((void **)&h->acc_host, sizeof(DevAcc), hipHostMallocDefault) != hipSuccess) {
         g_open_err = "pinned host buffer";
@@ -1277,7 +1325,7 @@ int lpc_close(lpc_handle *h)
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->d_misc, &h->d_wrec, &h->w_spill, &h->w_qroots,
-                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum};
+                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1377,7 +1425,7 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
         }
         h->scene_scale = diag2 > 0.0 ? 0.5 * sqrt(diag2) : 1.0;
     }
-    h->dcap = 16.0;
+    h->dcap = h->dcap_init;
     RETIF(build_records(h));
     RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
     RETIF(dalloc(h, h->d_verts, vv.size() * 4));
@@ -1672,6 +1720,7 @@ int lpc_trace_reset(lpc_handle *h)
     h->pop_emitted = true;
     h->pop_dmax2 = h->init_dmax2;
     h->m_total = 0;                             // measured record emptied (the first iteration resets the counters)
+    h->m_inflight = 0;
     return 0;
 }
 
@@ -1690,42 +1739,7 @@ static int xchg_stats(lpc_handle *h, const lpc_iter_stats &S, lpc_iter_stats *G)
 }
 
 static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait)
-{
-    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
-    if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
-    *n_iter = 0;
-    h->gstats.clear();
-    for (int32_t i = 0; i < max_iter; ++i) {
-        lpc_iter_stats S;
-        RETIF(lpc_trace_iterate(h, nullptr, nullptr, nullptr, nullptr, nullptr, &S));
-        per_iter[i] = S;
-        *n_iter = i + 1;
-        // sharded trace: every rank decides on the sums over all ranks (the
-        // identical bits everywhere), so all stop at the iteration a single
-        // device would (iterative_tracer.py:383-391)
-        lpc_iter_stats G = S;
-        if (h->xchg) RETIF(xchg_stats(h, S, &G));
-        h->gstats.push_back(G);
-        if (G.power_next < power_threshold) break;          // :383
-        if (G.n_reflect + G.n_refract == 0) break;          // :389
-    }
-    if (measured_count || mesh_power) {                     // the trace's aggregates, same call
-        int64_t c = 0;
-        std::vector<double> mp((size_t)h->K + 1, 0.0);
-        RETIF(lpc_trace_measured(h, &c, mp.data()));
-        if (h->xchg) {                                      // trace-end sums over the ranks
-            mp[(size_t)h->K] = (double)c;
-            if (h->xchg(h->xchg_ctx, mp.data(), h->K + 1) != 0)
-                return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
-            c = (int64_t)mp[(size_t)h->K];
-        }
-        if (measured_count) *measured_count = c;
-        if (mesh_power) memcpy(mesh_power, mp.data(), (size_t)h->K * 8);
-    }
-    if (wait) RETIF(settle(h));                             // the trace's last kernels too
-    return 0;
-}
+                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait);
 
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                   int32_t *n_iter, int64_t *measured_count, double *mesh_power)
@@ -1807,11 +1821,11 @@ static int ensure_measured(lpc_handle *h, int64_t need)
     int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * h->m_cap, 1 << 16));
     DBuf nb;
     RETIF(dalloc(h, nb, (size_t)cap * 5 * 4));
-    if (h->m_total > 0) {
+    if (h->m_cap > 0) {         // all old rows: an iteration still in flight may append past m_total
         for (int k = 0; k < 5; ++k)
             HIPCHK(h, hipMemcpyAsync((char *)nb.p + (size_t)k * cap * 4,
                                      (char *)h->m_buf.p + (size_t)k * h->m_cap * 4,
-                                     (size_t)h->m_total * 4, hipMemcpyDeviceToDevice, h->stream));
+                                     (size_t)h->m_cap * 4, hipMemcpyDeviceToDevice, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     dfree(h->m_buf);
@@ -1820,18 +1834,19 @@ static int ensure_measured(lpc_handle *h, int64_t need)
     return 0;
 }
 
-// Wait (spinning) until k_scan has published this iteration's counters
-// (sequence number h->acc_seq) in the mapped host copy; the stream keeps running.
-// A stream that fails or finishes without publishing is reported.
-static int wait_mapped_acc(lpc_handle *h, DevAcc *out)
+// Wait (spinning) until k_scan / k_stage_move has published the counters of the
+// iteration with sequence number `seq` in its mapped ring slot; the stream keeps
+// running.  A stream that fails or finishes without publishing is reported.
+static int wait_mapped_acc(lpc_handle *h, unsigned seq, DevAcc *out)
 {
-    volatile DevAcc *m = h->acc_map;
+    DevAcc *slot = h->acc_map + seq % kAccRing;
+    volatile DevAcc *m = slot;
     for (uint64_t i = 1;; ++i) {
-        if (__atomic_load_n(&h->acc_map->seq, __ATOMIC_ACQUIRE) == h->acc_seq) break;
+        if (__atomic_load_n(&slot->seq, __ATOMIC_ACQUIRE) == seq) break;
         if ((i & 255u) == 0u) {
             const hipError_t e = hipStreamQuery(h->stream);
             if (e == hipSuccess) {
-                if (__atomic_load_n(&h->acc_map->seq, __ATOMIC_ACQUIRE) == h->acc_seq) break;
+                if (__atomic_load_n(&slot->seq, __ATOMIC_ACQUIRE) == seq) break;
                 return set_err(h, LPC_E_HIP, "iteration counters were not published");
             }
             if (e != hipErrorNotReady) return set_err(h, LPC_E_HIP, std::string("trace: ") + hipGetErrorString(e));
@@ -1845,24 +1860,45 @@ static int wait_mapped_acc(lpc_handle *h, DevAcc *out)
     return 0;
 }
 
-int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
-                      int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st)
+// An enqueued iteration whose counters have not been read yet.
+struct Pending {
+    int64_t n_in = 0;           // its population (-1: device-sized, known once the iteration before is read)
+    unsigned seq = 0;           // mapped ring slot / sequence number (early)
+    bool early = false;         // counters through the mapped ring (else copy + sync)
+    bool traced = false;        // its children come out in traced order
+    bool fused = false;         // k_shade_stage + k_stage_move: it wrote the next IterCtl entry
+    bool mp_fused = false;      // it summed the measured power per measure mesh
+    bool ds = false;            // device-sized (speculative)
+    bool empty = false;         // nothing to do (n_in 0, host-sized)
+    int64_t n_bound = 0;        // device-sized: population bound
+    // host state before its enqueue (undo of a discarded speculative iteration)
+    bool was_init = false, was_traced = false, was_emitted = false;
+};
+
+// Enqueue one iteration over the current population (host-sized: h->n_cur rays;
+// ds != NULL: device-sized, traced single-chunk only).  Host bookkeeping that
+// needs no counters (population roles) happens here; iter_collect the rest.
+static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow, int32_t *out_meas,
+                        float *out_next_pow, const DevSize *ds, Pending *P)
 {
-    const double t_enter = h && h->host_prof ? host_us() : 0.0;
-    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
-    if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_iterate before trace_set_rays");
-    HIPCHK(h, hipSetDevice(h->device));
-    lpc_iter_stats S;
-    memset(&S, 0, sizeof(S));
-    const int64_t N = h->n_cur;
-    S.n_in = N;
-    if (N == 0) { if (st) *st = S; return 0; }
+    *P = Pending();
+    P->was_init = h->pop_init; P->was_traced = h->pop_traced; P->was_emitted = h->pop_emitted;
+    const int64_t N = ds ? ds->bound : h->n_cur;
+    P->n_in = ds ? -1 : N;
+    P->ds = ds != nullptr;
+    P->n_bound = N;
+    if (N == 0) { P->empty = true; return 0; }
     const int64_t C = std::min(N, chunk_rays(h));
+    if (ds && C < N) return set_err(h, LPC_E_STATE, "internal: device-sized iteration over one chunk only");
     RETIF(ensure_ws(h, C));
     RETIF(pop_reserve(h, h->B, 2 * N));
-    RETIF(pop_reserve(h, h->T, N));
-    RETIF(ensure_measured(h, h->m_total + N));
-    if (C >= N) {                       // one chunk: the counters reset rides on the slot reset
+    if (!ds) RETIF(pop_reserve(h, h->T, N));
+    // measured rows: the iterations still in flight may append up to their populations
+    RETIF(ensure_measured(h, h->m_total + h->m_inflight + N));
+    h->m_inflight += N;
+    if (ds) {
+        h->acc_pending = false;         // k_stage_move writes every counter
+    } else if (C >= N) {                // one chunk: the counters reset rides on the slot reset
         h->acc_pending = true;
         h->acc_pending_total = h->m_total;
     } else {
@@ -1875,21 +1911,29 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     // its parents' coherence order; measured rays per iteration likewise)
     const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow;
     const bool traced = h->traced && C >= N && !exports;
-    // the counters come back through the mapped host copy k_scan writes, so the
-    // host decides and launches the next iteration while k_scatter still runs
-    // (profiling: only the light level, whose events end before k_scan)
+    // the counters come back through the mapped host ring k_scan / k_stage_move
+    // write, so the host decides and launches the next iteration while the rows
+    // still move (profiling: only the light level, whose events end before)
     const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && (!h->prof || h->prof_light);
-    if (early) ++h->acc_seq;
+    ++h->acc_seq;
+    P->seq = h->acc_seq;
+    P->early = early;
+    P->traced = traced;
     // traced single chunk: k_shade_stage + k_stage_move
     const bool fused = traced && h->fuse_compact && C >= N;
-    bool mp_fused = false;                  // this iteration summed the measured power per mesh
+    if (ds && !(fused && early)) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the fused path");
+    P->fused = fused;
+    const size_t Cs = (size_t)h->ws_rays;
+    const int64_t ntc = (int64_t)((Cs + LPC_ST_TILE - 1) / LPC_ST_TILE);   // staging tile arrays' stride
+    IterCtl *ctl = (IterCtl *)h->d_ctl.p;
+    const int par = h->ctl_par;
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         RaysIn in = (h->pop_init ? h->I : h->A).in(base);
         RaysIn tin;
         h->in_trace = true;
         const int rc_i = run_intersect(h, in, nc, h->max_ray_len, nullptr, nullptr, nullptr, h->pop_dmax2,
-                                       traced ? &tin : nullptr);
+                                       traced ? &tin : nullptr, ds);
         h->in_trace = false;
         RETIF(rc_i);
         if (traced) in = tin;
@@ -1905,33 +1949,37 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
         if (A.direct_t) A.nT = A.nR;
         A.mx = mf; A.my = mf + mc; A.mz = mf + 2 * mc; A.mp = mf + 3 * mc;
         A.mm = (int32_t *)(mf + 4 * mc);
-        A.host_acc = early ? h->acc_map_dev : nullptr;
-        A.seq = h->acc_seq;
+        A.host_acc = early ? h->acc_map_dev + P->seq % kAccRing : nullptr;
+        A.seq = P->seq;
         if (fused) {                  // shade + staged compaction, two kernels (k_shade_stage, k_stage_move)
-            const int64_t nt = (nc + LPC_ST_TILE - 1) / LPC_ST_TILE;
-            const size_t Cs = (size_t)h->ws_rays;
+            // device-sized: grid from the expected size (grid-stride over the actual tiles)
+            const int64_t ng_rays = ds ? std::max<int64_t>(1, std::min(ds->pred, nc)) : nc;
+            const int64_t nt = (ng_rays + LPC_ST_TILE - 1) / LPC_ST_TILE;
+            const int64_t nt_max = (nc + LPC_ST_TILE - 1) / LPC_ST_TILE;     // tiles the launch may touch
             StageArgs G;
             G.S = shade_args(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false);
+            G.nd = ds ? ds->nd : nullptr;
             G.stR = (float *)h->w_shf.p;                // the 20 shade-output arrays hold the staging rows
             G.stT = (float *)h->w_shi.p;
             G.stM = (float *)h->w_soa.p;
             G.cst = (int64_t)Cs;
             G.tpow = (double *)h->w_fc.p;
-            G.tcnt = (uint32_t *)(G.tpow + nt);
-            G.tdm = G.tcnt + nt;
+            G.tcnt = (uint32_t *)(G.tpow + ntc);
+            G.tdm = G.tcnt + ntc;
             G.skey = (unsigned long long *)h->w_key.p;
             G.scnt = (int32_t *)h->w_sc.p;
             // measured power per measure mesh summed on the way (no k_mesh_sum at the trace end)
             G.nmp = h->meas_meshes.size() <= (size_t)LPC_MP_MAX ? (int)h->meas_meshes.size() : 0;
             for (int m = 0; m < LPC_MP_MAX; ++m) G.mpm[m] = m < G.nmp ? h->meas_meshes[(size_t)m] : -1;
-            G.tmp = (double *)(G.tdm + nt);             // 16 nt bytes in: 8-aligned
-            const int64_t ng = (nt + LPC_ST_GROUP - 1) / LPC_ST_GROUP;
+            G.tmp = (double *)(G.tdm + ntc);            // 16 ntc bytes in: 8-aligned
+            const int64_t ng = (nt_max + LPC_ST_GROUP - 1) / LPC_ST_GROUP;
             unsigned long long *gs = (unsigned long long *)h->w_gsum.p;
             G.gsum = gs + (size_t)h->gpar * (size_t)h->gcap;
 
-            LPC_KU_LAUNCH(h, k_shade_stage, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
+            if (ds) LPC_KU_LAUNCH2(h, k_shade_stage, true, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
+            else LPC_KU_LAUNCH2(h, k_shade_stage, false, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
             MoveArgs M;
-            M.ntiles = nt;
+            M.ntiles = nt_max;
             M.stR = G.stR; M.stT = G.stT; M.stM = G.stM; M.cst = G.cst;
             M.tcnt = G.tcnt; M.tpow = G.tpow; M.tdm = G.tdm;
             M.popR = h->B.f(0); M.capR = h->B.cap;
@@ -1948,11 +1996,16 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
             M.ngroups = ng;
             M.gsum_next = gs + (size_t)(1 - h->gpar) * (size_t)h->gcap;
             M.gdirty_next = h->gdirty[1 - h->gpar];
+            M.ctl = ctl;
+            M.par = par;
+            M.thr = h->ds_thr;
+            M.dcap2 = h->dcap * h->dcap * (1.0 - 1e-6);
             h->gdirty[1 - h->gpar] = 0;
             h->gdirty[h->gpar] = ng;            // this launch's k_shade_stage adds into its first ng groups
             h->gpar = 1 - h->gpar;
-            mp_fused = G.nmp > 0 || h->meas_meshes.empty();
-            hipLaunchKernelGGL(k_stage_move, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
+            P->mp_fused = G.nmp > 0 || h->meas_meshes.empty();
+            if (ds) hipLaunchKernelGGL(k_stage_move<true>, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
+            else hipLaunchKernelGGL(k_stage_move<false>, dim3((unsigned)nt), dim3(LPC_ST_TILE), 0, h->stream, M);
             h->slots_clean = true;              // k_shade_stage restored what it read
             h->slots_mrl = h->max_ray_len;
             h->misc_clean = true;               // k_stage_move reset the next launch's words
@@ -1989,38 +2042,51 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
                            h->B.out(), h->T.in(), (const DevAcc *)h->d_acc.p, h->B.cap, h->T.cap);
         HIPCHK(h, hipGetLastError());
     }
+    h->ctl_par ^= 1;                    // the next iteration reads the entry this one's k_stage_move writes
+    // the children are the next population (their counts come with iter_collect)
+    std::swap(h->A, h->B);
+    h->pop_init = false;
+    h->pop_traced = traced;
+    h->pop_emitted = false;
+    h->inflight = true;                 // k_stage_move / k_scatter may still run
+    return 0;
+}
+
+// Read an enqueued iteration's counters (in enqueue order) and finish its host
+// bookkeeping.  out_next_pow: the kept children's power (the population after it).
+static int iter_collect(lpc_handle *h, const Pending &P, float *out_next_pow, lpc_iter_stats *st)
+{
+    lpc_iter_stats S;
+    memset(&S, 0, sizeof(S));
+    S.n_in = P.n_in;
+    if (P.empty) { if (st) *st = S; return 0; }
     DevAcc acc;
     const double t_wait = h->host_prof ? host_us() : 0.0;
-    if (early) {
-        RETIF(wait_mapped_acc(h, &acc));
+    if (P.early) {
+        RETIF(wait_mapped_acc(h, P.seq, &acc));
     } else {
         HIPCHK(h, hipMemcpyAsync(h->acc_host, h->d_acc.p, sizeof(DevAcc), hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         acc = *h->acc_host;
     }
+    h->m_inflight -= P.n_bound;
     if (acc.qerr) return q_failed(h);
     if (h->host_prof) {
         const double t_got = host_us();
-        fprintf(stderr, "[lpc host] n %lld  since last %.1f us  first launch %.1f us  launch %.1f us  wait %.1f us\n",
-                (long long)N, t_enter - h->host_last, h->t_first > 0.0 ? h->t_first - t_enter : -1.0,
-                t_wait - t_enter, t_got - t_wait);
-        h->t_first = 0.0;
+        fprintf(stderr, "[lpc host] n %lld%s  since last %.1f us  wait %.1f us\n", (long long)P.n_in,
+                P.ds ? " (device-sized)" : "", t_wait - h->host_last, t_got - t_wait);
         h->host_last = t_got;
     }
     const int64_t nR = (int64_t)acc.nR, nT = (int64_t)acc.nT;
-    if (out_next_pow && nR + nT > 0) {
-        HIPCHK(h, hipMemcpyAsync(out_next_pow, h->B.f(6), (size_t)(nR + nT) * 4, hipMemcpyDeviceToHost, h->stream));
+    if (out_next_pow && nR + nT > 0) {   // the population after the swap (iter_enqueue)
+        HIPCHK(h, hipMemcpyAsync(out_next_pow, h->A.f(6), (size_t)(nR + nT) * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     if (h->prof) prof_resolve(h);
-    std::swap(h->A, h->B);
-    h->pop_init = false;
-    h->pop_traced = traced;
-    h->pop_emitted = false;
     h->n_cur = nR + nT;
     h->m_total = (int64_t)acc.m_total;
     // the running per-mesh measured power stays valid while every iteration sums it
-    h->mp_valid = h->mp_valid && mp_fused;
+    h->mp_valid = h->mp_valid && P.mp_fused;
     if (h->mp_valid) memcpy(h->mp_last, acc.mpow, sizeof(h->mp_last));
     S.n_reflect = nR; S.n_refract = nT; S.n_measured = (int64_t)acc.nM_iter;
     S.power_next = acc.pow_next;
@@ -2028,8 +2094,152 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     memcpy(&dm2, &acc.dmax2_bits, 4);
     RETIF(check_dcap(h, (double)dm2));
     h->pop_dmax2 = (double)dm2;                 // the next population's max |D|^2 (float, see run_intersect)
-    h->inflight = true;                         // k_stage_move / k_scatter may still run
     if (st) *st = S;
+    return 0;
+}
+
+// A speculative iteration the trace did not need (it ran empty on the device:
+// IterCtl said 0): the population roles go back to before its enqueue.
+static void iter_discard(lpc_handle *h, const Pending &P)
+{
+    h->m_inflight -= P.n_bound;
+    if (P.empty) return;
+    std::swap(h->A, h->B);
+    h->pop_init = P.was_init;
+    h->pop_traced = P.was_traced;
+    h->pop_emitted = P.was_emitted;
+}
+
+int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
+                      int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st)
+{
+    const double t_enter = h && h->host_prof ? host_us() : 0.0;
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_iterate before trace_set_rays");
+    HIPCHK(h, hipSetDevice(h->device));
+    Pending P;
+    RETIF(iter_enqueue(h, out_origin4, out_dest4, out_pow, out_meas, out_next_pow, nullptr, &P));
+    if (h->host_prof && !P.empty)
+        fprintf(stderr, "[lpc host] n %lld  launch %.1f us\n", (long long)P.n_in, host_us() - t_enter);
+    return iter_collect(h, P, out_next_pow, st);
+}
+
+// May the iteration after the one in flight (population <= bound rays, chained
+// traced) be enqueued device-sized?  Single chunk, fused compaction, mapped
+// counters, root-item path, no all-reduce hook (a sharded trace decides on the
+// sums over all ranks, which the device does not see), no per-kernel profiling.
+static bool ds_ok(const lpc_handle *h, int64_t bound)
+{
+    return h->spec && !h->xchg && h->traced && h->fuse_compact && h->early_acc && h->acc_map_dev &&
+           (!h->prof || h->prof_light) && h->queue == 2 && !h->prof_waves && h->roots_s > 0 && bound > 0 &&
+           bound <= chunk_rays(h) && (bound + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
+           (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES && h->K <= LPC_Q_MAX_SLOTS;
+}
+
+// The trace loop (iterative_tracer.py:383-391).  With speculation (LPC_SPEC, and
+// a previous trace of the same first population, limit and threshold that
+// reached the next iteration), iteration i + 1 is enqueued device-sized
+// (IterCtl: its size and the stop rule evaluated by iteration i's k_stage_move)
+// before iteration i's counters are read, so the GPU never waits for the host
+// between iterations.  The results are the same bits: the device applies the
+// host's rules; an iteration the trace turns out not to need runs empty and is
+// dropped (iter_discard); a Dcap overflow (records rebuilt) re-runs it host-sized.
+static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
+    if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_run before trace_set_rays");
+    HIPCHK(h, hipSetDevice(h->device));
+    *n_iter = 0;
+    h->gstats.clear();
+    // the prediction: the last trace from emitted rays with this iteration limit
+    // (which iterations it reached, populations relative to the first)
+    const int64_t n0 = h->pop_emitted ? h->n_cur : -1;
+    const bool hist_ok = n0 > 0 && h->hist_iter == max_iter && !h->hist_r.empty();
+    h->dcap_rebuilt = false;
+    std::vector<int64_t> seen;
+    h->ds_thr = power_threshold;
+    int rc = 0;
+    Pending cur, nxt;
+    bool have_cur = false, have_nxt = false;
+    for (int32_t i = 0; i < max_iter; ++i) {
+        if (!have_cur) {
+            if ((rc = iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &cur))) break;
+            have_cur = true;
+        }
+        // iteration i + 1, device-sized, while iteration i runs (its population is
+        // known: host-sized, or the kept children of iteration i - 1)
+        if (hist_ok && i + 1 < max_iter && (int64_t)h->hist_r.size() > i + 1 && cur.fused && !cur.empty &&
+            cur.n_in > 0) {
+            const int64_t bound = 2 * cur.n_in;
+            if (ds_ok(h, bound)) {
+                IterCtl *ctl = (IterCtl *)h->d_ctl.p;
+                DevSize D;
+                D.nd = &ctl->n[h->ctl_par];
+                D.dm2 = &ctl->dm2[h->ctl_par];
+                D.pred = std::max<int64_t>(1, std::min((int64_t)llround(h->hist_r[(size_t)i + 1] * (double)n0), bound));
+                D.bound = bound;
+                if ((rc = iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, &D, &nxt))) break;
+                have_nxt = true;
+            }
+        }
+        lpc_iter_stats S;
+        rc = iter_collect(h, cur, nullptr, &S);
+        have_cur = false;
+        if (rc) break;
+        per_iter[i] = S;
+        *n_iter = i + 1;
+        seen.push_back(S.n_in);
+        // sharded trace: every rank decides on the sums over all ranks (the
+        // identical bits everywhere), so all stop at the iteration a single
+        // device would (iterative_tracer.py:383-391)
+        lpc_iter_stats G = S;
+        if (h->xchg && (rc = xchg_stats(h, S, &G))) break;
+        h->gstats.push_back(G);
+        const bool stop = G.power_next < power_threshold || G.n_reflect + G.n_refract == 0;   // :383, :389
+        if (have_nxt) {
+            const bool rebuilt = h->dcap_rebuilt;
+            h->dcap_rebuilt = false;
+            if (stop || rebuilt || i + 1 >= max_iter) {
+                // ran empty on the device (its IterCtl size was 0): not part of the trace
+                iter_discard(h, nxt);
+                have_nxt = false;
+            } else {
+                nxt.n_in = G.n_reflect + G.n_refract;
+                cur = nxt;
+                have_cur = true;
+                have_nxt = false;
+            }
+        }
+        if (stop) break;
+    }
+    if (have_nxt) iter_discard(h, nxt);
+    if (have_cur) {                                         // an error with one still queued
+        (void)hipStreamSynchronize(h->stream);
+        iter_discard(h, cur);
+    }
+    RETIF(rc);
+    // this trace's populations (relative to the first) predict the next trace's
+    if (n0 > 0) {
+        h->hist_r.clear();
+        for (int64_t v : seen) h->hist_r.push_back((double)v / (double)n0);
+        h->hist_iter = max_iter;
+    }
+    if (measured_count || mesh_power) {                     // the trace's aggregates, same call
+        int64_t c = 0;
+        std::vector<double> mp((size_t)h->K + 1, 0.0);
+        RETIF(lpc_trace_measured(h, &c, mp.data()));
+        if (h->xchg) {                                      // trace-end sums over the ranks
+            mp[(size_t)h->K] = (double)c;
+            if (h->xchg(h->xchg_ctx, mp.data(), h->K + 1) != 0)
+                return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
+            c = (int64_t)mp[(size_t)h->K];
+        }
+        if (measured_count) *measured_count = c;
+        if (mesh_power) memcpy(mesh_power, mp.data(), (size_t)h->K * 8);
+    }
+    if (wait) RETIF(settle(h));                             // the trace's last kernels too
     return 0;
 }
 

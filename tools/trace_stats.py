@@ -18,6 +18,7 @@ o = np.asarray(sc.sources[0].rays_origin, np.float32)
 d = np.asarray(sc.sources[0].rays_dir, np.float32)
 p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
 e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+thr = (1.0 - sc.tau) * float(np.sum(p, dtype=np.float64))
 for counters in (False, True):
     e.reset()
     e.prof_enable(True, counters=counters)
@@ -44,6 +45,6 @@ for counters in (False, True):
             print(f"    tail waves {pr['tail_waves']}: nodes/wave {pr['tail_nodes']/tw:.0f} "
                   f"spread {pr['tail_spread_urad']/tw/1e6:.4f} rad exact/wave {pr['tail_exact']/tw:.0f}; "
                   f"all waves: nodes/wave {pr['node_visits']/max(pr['wave_traversals'],1):.1f}", flush=True)
-        if st.n_reflect + st.n_refract == 0:
+        if st.n_reflect + st.n_refract == 0 or st.power_next < thr:   # iterative_tracer.py:383-391
             break
     print("counters" if counters else "timing only")
