@@ -44,10 +44,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector peak
-# MI355X_MICROARCH.md ("v_fma_f32 (wave64): 2 cyc (SIMD-32)"; "4 SIMD-32 vector units"
-# per CU): 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction =
-# chip-wide VALU issue peak in wave-instructions per second (= 157.3 TF / 64 lanes / 2 flops)
-VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
+# VALU issue peak: each CU has 4 SIMDs of 16 lanes, so a wave64 VALU instruction
+# occupies its SIMD for 4 cycles; 256 CUs x 4 SIMDs x 2.4 GHz / 4 = 614.4 G
+# wave-instructions per second (x 64 lanes x 2 flops = the 78.6 TF FP32 FMA peak
+# without packing; packed FP32 doubles the flops, not the instruction rate)
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4
 RAY_BYTES = 156                # algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # per triangle per bounce-iteration
 MT_FLOPS = 46                  # Moller-Trumbore flops per ray-triangle test
@@ -59,8 +60,8 @@ CONFIGS = [("parabolic", 1_000_000, 4), ("lens", 10_000_000, 8), ("eye", 10_000_
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     ap.add_argument("--cpu-rays", type=int, default=1 << 20, help="CPU baseline sample (rays, one bounce)")
@@ -87,6 +88,9 @@ def load_pmc():
     except Exception:
         return {}
     pmc["stale"] = pmc.get("kernels_sha16") != src_sha16() or pmc.get("kernel") not in (None, WALK_KERNEL)
+    if pmc["stale"]:
+        print(f"bench: {p} was collected on other kernel sources or another kernel; PMC figures not used",
+              file=sys.stderr)
     return pmc
 
 
@@ -143,6 +147,34 @@ def cpu_leg(sc, eng, o, d, p, nrays, first_stats, timed):
               "checked_against": "oracle/lpc_oracle.c (C restatement of kernel_reflect_refract_intersect.cl; "
                                  "rsqrt/sqrt/exp correctly rounded / libm); liblpc vs the reference's own gfx950 "
                                  "kernels: bit-exact, tests/test_ref_parity.py"}
+    # the reference's own kernels (the unmodified .cl compiled for gfx950 by ROCm's
+    # OpenCL front end, IEEE division/sqrt, no contraction: oracle/_ref, DESIGN.md
+    # section 3) on the same rays, every output field bit for bit
+    co = os.path.join(ROOT, "oracle", "_ref", "lpc_ref_ieee.co")
+    if os.path.exists(co):
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import ref_gpu
+        rk = ref_gpu.RefKernels("ieee")
+        try:
+            rr = rk.bounce(S, o, d, p, z, pm, sc.max_ray_len, sc.ior_env)
+        finally:
+            rk.close()
+        bad = np.zeros(n, bool)
+        per = {}
+        names = ("dest", "pow", "meas", "isect_mid", "isect_idx", "n1", "n2", "entering", "r_dir", "r_pow",
+                 "r_meas", "t_dir", "t_pow", "t_meas")
+        for k in names:
+            a = np.asarray(g[k]).reshape(n, -1)[:, :3]
+            b = np.asarray(rr[k]).reshape(n, -1)[:, :3]
+            diff = np.any((a != b) & ~(np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else a != b, axis=1)
+            per[k] = int(diff.sum())
+            bad |= diff
+        parity["vs_reference_kernels"] = {
+            "rays": int(n), "mismatched_rays": int(bad.sum()),
+            "per_field": {k: v for k, v in per.items() if v},
+            "fields": ", ".join(names) + " (values equal; NaN = NaN)",
+            "build": "oracle/_ref/lpc_ref_ieee.co: /root/reference/kernel_reflect_refract_intersect.cl unmodified, "
+                     "ROCm OpenCL C for gfx950, IEEE div/sqrt, -ffp-contract=off"}
     if n == len(first_stats["population"]):
         kr = int(np.sum(ref["r_meas"] == 0))
         kt = int(np.sum(ref["t_meas"] == 0))
@@ -258,6 +290,10 @@ def main():
         step()
     if not a.no_prof:
         eng.prof_enable(True, light=True)    # HIP events around the walk kernel's launches only
+        # untimed: the same number of steps once with events, so the timed region
+        # takes its events from the pool instead of creating them
+        for _ in range(a.steps):
+            step()
     eng.prof_read(reset=True)
     sync()
     t0 = time.perf_counter()
@@ -341,7 +377,7 @@ def main():
                           "valu_insts_per_launch": valu_per_launch, "pmc_stale": stale,
                           "note": f"executed VALU wave-instructions per {WALK_KERNEL} launch (PMC SQ_INSTS_VALU, "
                                   "profiles/pmc_intersect.json) / its live average launch time / chip issue "
-                                  "peak (256 CU x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction)"},
+                                  "peak (256 CU x 4 SIMD x 2.4 GHz / 4 cycles per wave64 instruction on a 16-lane SIMD)"},
         # brute-force equivalent: what the reference's O(N*M) loop would have to sustain
         "ri_equivalent": {"ri_per_s": pairs_per_s, "mt_tflops_equiv": mt_tflops,
                           "fp32_peak_tflops": FP32_PEAK_TFLOPS,

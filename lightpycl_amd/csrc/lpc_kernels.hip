@@ -661,12 +661,21 @@ static __device__ __forceinline__ uint64_t wave_or64(uint64_t v)
 
 // Grid-stride over the virtual blocks (pb packets each; device-sized launches
 // read n on the device, nd != NULL).
+// The root tests' records in LDS (cx cy cz negB | negA): the piece loop reads
+// them with broadcast LDS loads instead of one scalar-load round trip per piece.
+struct RootsLds {
+    float4 pc[LPC_ROOTS_TASKS * 64];
+    float pa[LPC_ROOTS_TASKS * 64];
+    float4 gc[64];
+    float ga[64];
+};
+
 template <bool HALF>
 static __device__ __forceinline__ void roots_block(const RaysIn &R, const float *__restrict__ rs, int64_t n,
                                                    const Piece *__restrict__ pieces, int npieces,
                                                    const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
                                                    int S, int pb, int64_t vb, unsigned long long *s_m,
-                                                   uint32_t *s_off);
+                                                   uint32_t *s_off, const RootsLds &L);
 
 template <bool HALF>
 __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restrict__ rs, int64_t n,
@@ -676,10 +685,22 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
 {
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
+    __shared__ RootsLds L;
     if (nd) n = *nd;
+    for (int i = threadIdx.x; i < npieces; i += 256) {
+        const Piece &P = pieces[i];
+        L.pc[i] = make_float4(P.cx, P.cy, P.cz, P.negB);
+        L.pa[i] = P.negA;
+    }
+    for (int i = threadIdx.x; i < ngroups; i += 256) {
+        const Piece &G = groups[i];
+        L.gc[i] = make_float4(G.cx, G.cy, G.cz, G.negB);
+        L.ga[i] = G.negA;
+    }
+    __syncthreads();
     const int64_t nvb = ((n + 63) / 64 + pb - 1) / pb;
     for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off);
+        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off, L);
         __syncthreads();                          // s_m / s_off reused by the next virtual block
     }
 }
@@ -689,7 +710,7 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
                                                    const Piece *__restrict__ pieces, int npieces,
                                                    const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
                                                    int S, int pb, int64_t vb, unsigned long long *s_m,
-                                                   uint32_t *s_off)
+                                                   uint32_t *s_off, const RootsLds &L)
 {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -708,18 +729,21 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
             uint64_t ml = 0;                    // this lane's ray: bit k = piece cls + S k passes
             auto test = [&](int lo, int hi) {   // the class's pieces in [lo, hi)
                 const int p0 = lo + ((cls - lo % S) % S + S) % S;
+#pragma unroll 4
                 for (int p = p0, k = p0 / S; p < hi; p += S, ++k) {
-                    const Piece &P = pieces[p];
-                    const float d = HALF ? filter_testh(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz)
-                                         : filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz);
+                    const float4 c = L.pc[p];
+                    const float a = L.pa[p];
+                    const float d = HALF ? filter_testh(c.x, c.y, c.z, c.w, a, O.x, O.y, O.z, nx, ny, nz)
+                                         : filter_test(c.x, c.y, c.z, c.w, a, O.x, O.y, O.z, nx, ny, nz);
                     ml |= (uint64_t)(d <= 0.0f) << k;
                 }
             };
             if (ngroups > 0) {
                 uint64_t gl = 0;
+#pragma unroll 4
                 for (int g = 0; g < ngroups; ++g) {
-                    const Piece &G = groups[g];
-                    const float d = filter_test(G.cx, G.cy, G.cz, G.negB, G.negA, O.x, O.y, O.z, nx, ny, nz);
+                    const float4 c = L.gc[g];
+                    const float d = filter_test(c.x, c.y, c.z, c.w, L.ga[g], O.x, O.y, O.z, nx, ny, nz);
                     gl |= (uint64_t)(d <= 0.0f) << g;
                 }
                 for (uint64_t gm = wave_or64(gl); gm; gm &= gm - 1) {
@@ -998,6 +1022,276 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     if (i >= n) return;
     keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
     vals[i] = (int32_t)i;
+}
+
+// ---------------------------------------------------------------------------
+// Counting sort of the coherence keys when the key bits that vary span <= 16
+// (the emitted rays of a traced trace from a point source or a collimated beam,
+// set_rays): MSD with two 8-bit digits, every rank taken in index order (wave
+// match ballots, waves and rounds in order), so the permutation is the stable
+// sort's and identical from run to run.
+//   k_bkey      key (+ 32-byte row, + slot reset), the block's hi-digit counts
+//   k_bprefix   per hi digit: exclusive prefix of the block counts, digit total
+//   k_bscatter  stable scatter by hi digit: (lo digit, ray) into bucket order;
+//               block 0 writes the bucket starts.  One level (lb = 0): perm
+//   k_bsort2    one block per hi bucket: stable order by lo digit in LDS, perm
+//               written in order
+// then k_gather_aos as after rocPRIM.  Replaces key + rocPRIM onesweep (4 fills,
+// 2 histogram and 2 look-back pass kernels for 1 M rays).  set_rays takes this
+// path only when a host estimate puts at most LPC_BS_MAXB rays into a hi bucket.
+#define LPC_BS_T 1024                      // threads per block
+#define LPC_BS_RPB 4096                    // rays per k_bkey / k_bscatter block
+#define LPC_BS_HB 8                        // hi digit bits (at most); lo digit <= 8 bits
+#define LPC_BS_ND (1 << LPC_BS_HB)
+#define LPC_BS_MAXB 16384                  // largest hi bucket k_bsort2 orders in LDS
+
+// Rank of each lane's digit among the lower lanes with the same digit, and the
+// number of valid lanes with it (`valid` lanes only).
+static __device__ __forceinline__ void wave_match(uint32_t d, bool valid, int nbits, int &rank, int &cnt, bool &last)
+{
+    uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (k >= nbits) break;
+        const bool b = (d >> k) & 1u;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(b);
+        peers &= b ? m : ~m;
+    }
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    rank = __builtin_popcountll(peers & lt);
+    cnt = __builtin_popcountll(peers);
+    last = valid && (peers >> lane) == 1ull;           // highest lane of its digit
+}
+
+struct BSortLds {
+    uint16_t wc[LPC_BS_T / 64][LPC_BS_ND];   // per wave, per digit: the round's count (zero between rounds)
+    uint32_t off[LPC_BS_T / 64][LPC_BS_ND];  // per wave, per digit: the wave's first position
+    uint32_t run[LPC_BS_ND + 1];             // running position per digit
+};
+
+// One round of LPC_BS_T items (item j of the round on thread j): stable
+// positions from the running per-digit positions; `run` advances by the round's
+// counts.  The per-digit prefix over the 16 waves: 4 threads per digit (4 waves
+// each), combined with two shuffles.
+static __device__ __forceinline__ uint32_t bs_round(BSortLds &S, uint32_t d, bool valid, int nbits, int nd)
+{
+    const int t = threadIdx.x, w = t >> 6;
+    int rank, cnt;
+    bool last;
+    wave_match(d, valid, nbits, rank, cnt, last);
+    if (last) S.wc[w][d] = (uint16_t)cnt;
+    __syncthreads();
+    {
+        const int e = t >> 2, g = t & 3;                // digit e, waves 4 g .. 4 g + 3
+        uint32_t c[4], p = 0;
+        if (e < nd) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                c[v] = S.wc[4 * g + v][e];
+                S.wc[4 * g + v][e] = 0;
+                p += c[v];
+            }
+        }
+        uint32_t incl = p;                              // inclusive scan over the 4 threads of the digit
+        const uint32_t u1 = __shfl_up(incl, 1, 64);
+        if (g >= 1) incl += u1;
+        const uint32_t u2 = __shfl_up(incl, 2, 64);
+        if (g >= 2) incl += u2;
+        if (e < nd) {
+            uint32_t o = S.run[e] + incl - p;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                S.off[4 * g + v][e] = o;
+                o += c[v];
+            }
+        }
+        // the digit's 4 threads are lanes of one wave: their reads of run[e] above
+        // are done before this write
+        if (e < nd && g == 3) S.run[e] += incl;
+    }
+    __syncthreads();
+    return valid ? S.off[w][d] + (uint32_t)rank : 0u;
+}
+
+// dst[d] = base + sum of src[0 .. d) for d <= nd (nd < LPC_BS_T), block-wide; the
+// caller synchronises before reading dst.
+static __device__ __forceinline__ void bs_excl_scan(const uint32_t *src, int nd, uint32_t base, uint32_t *dst,
+                                                    uint32_t *ws)
+{
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t v = t < nd ? src[t] : 0u;
+    uint32_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t e = base + incl - v;
+    for (int k = 0; k < w; ++k) e += ws[k];
+    if (t <= nd) dst[t] = e;
+}
+
+// Keys of rays [b * RPB, (b + 1) * RPB) and their 32-byte rows (k_raykey), the
+// window's hi digit counted per block into hist[digit * nblk + b].
+__global__ __launch_bounds__(LPC_BS_T) void k_bkey(RaysIn R, int64_t n, float bx0, float by0, float bz0, float sx,
+                                                   float sy, float sz, uint32_t *__restrict__ keys,
+                                                   float4 *__restrict__ aos, SlotInit SI, int b0, int lb, int hb,
+                                                   uint32_t *__restrict__ hist, int64_t nblk)
+{
+    __shared__ uint32_t hcnt[LPC_BS_ND];
+    const int nd = 1 << hb;
+    if ((int)threadIdx.x < nd) hcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * LPC_BS_RPB;
+#pragma unroll
+    for (int j = 0; j < LPC_BS_RPB / LPC_BS_T; ++j) {
+        const int64_t i = base + j * LPC_BS_T + threadIdx.x;
+        if (SI.skey || SI.misc || SI.acc) slot_init_ray(SI, n, i);
+        if (i < n) {
+            const uint32_t k = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
+            keys[i] = k;
+            atomicAdd(&hcnt[(k >> (b0 + lb)) & (uint32_t)(nd - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nd) hist[(int64_t)threadIdx.x * nblk + blockIdx.x] = hcnt[threadIdx.x];
+}
+
+// One block per hi digit: exclusive prefix of its per-block counts (in place),
+// the digit's total into tot[digit].
+__global__ __launch_bounds__(256) void k_bprefix(uint32_t *__restrict__ hist, int64_t nblk, uint32_t *__restrict__ tot)
+{
+    __shared__ uint32_t ws[4];
+    uint32_t *row = hist + (int64_t)blockIdx.x * nblk;
+    uint32_t carry = 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t c0 = 0; c0 < nblk; c0 += 256) {
+        const int64_t c = c0 + threadIdx.x;
+        const uint32_t v = c < nblk ? row[c] : 0u;
+        uint32_t incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) ws[w] = incl;
+        __syncthreads();
+        uint32_t wbase = 0, all = 0;
+        for (int v2 = 0; v2 < 4; ++v2) {
+            if (v2 < w) wbase += ws[v2];
+            all += ws[v2];
+        }
+        if (c < nblk) row[c] = carry + wbase + incl - v;
+        carry += all;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+// Stable scatter by hi digit: (lo digit, ray) pairs into bucket order, or for
+// one level (lb == 0) the final permutation.  Block 0 writes the bucket starts
+// (bst[0 .. nd]).
+__global__ __launch_bounds__(LPC_BS_T) void k_bscatter(const uint32_t *__restrict__ keys, int64_t n, int b0, int lb,
+                                                       int hb, const uint32_t *__restrict__ hist, int64_t nblk,
+                                                       const uint32_t *__restrict__ tot, uint32_t *__restrict__ bst,
+                                                       uint8_t *__restrict__ mlo, int32_t *__restrict__ midx,
+                                                       int32_t *__restrict__ perm)
+{
+    __shared__ BSortLds S;
+    __shared__ uint32_t st[LPC_BS_ND + 1];
+    __shared__ uint32_t ws[LPC_BS_T / 64];
+    const int nd = 1 << hb;
+    const int t = threadIdx.x;
+    bs_excl_scan(tot, nd, 0u, st, ws);
+    for (int i = t; i < (LPC_BS_T / 64) * LPC_BS_ND; i += LPC_BS_T) (&S.wc[0][0])[i] = 0;
+    __syncthreads();
+    if (t < nd) S.run[t] = st[t] + hist[(int64_t)t * nblk + blockIdx.x];
+    if (blockIdx.x == 0 && t <= nd) bst[t] = st[t];
+    const int64_t base = (int64_t)blockIdx.x * LPC_BS_RPB;
+    constexpr int NR = LPC_BS_RPB / LPC_BS_T;
+    uint32_t k[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+        const int64_t i = base + j * LPC_BS_T + t;
+        k[j] = i < n ? keys[i] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+        const int64_t i = base + j * LPC_BS_T + t;
+        const bool valid = i < n;
+        const uint32_t d = (k[j] >> (b0 + lb)) & (uint32_t)(nd - 1);
+        const uint32_t pos = bs_round(S, d, valid, hb, nd);
+        if (valid) {
+            if (lb == 0) {
+                perm[pos] = (int32_t)i;
+            } else {
+                mlo[pos] = (uint8_t)((k[j] >> b0) & ((1u << lb) - 1u));
+                midx[pos] = (int32_t)i;
+            }
+        }
+    }
+}
+
+// One block per hi bucket: stable order of its (lo digit, ray) pairs by the lo
+// digit.  Buckets of <= LPC_BS_MAXB rays are ordered in LDS and perm written in
+// order (coalesced); a larger one (the host's estimate missed) writes each entry
+// where it goes.
+__global__ __launch_bounds__(LPC_BS_T) void k_bsort2(const uint8_t *__restrict__ mlo,
+                                                     const int32_t *__restrict__ midx, int lb,
+                                                     const uint32_t *__restrict__ bst, int32_t *__restrict__ perm)
+{
+    __shared__ BSortLds S;
+    __shared__ uint32_t hl[LPC_BS_ND], lst[LPC_BS_ND + 1];
+    __shared__ uint32_t ws[LPC_BS_T / 64];
+    __shared__ uint16_t order[LPC_BS_MAXB];            // bucket-local entry of each output position
+    const int nl = 1 << lb;
+    const int t = threadIdx.x;
+    const int64_t s0 = bst[blockIdx.x], s1 = bst[blockIdx.x + 1];
+    if (s1 <= s0) return;                               // block-uniform
+    const bool staged = s1 - s0 <= LPC_BS_MAXB;
+    if (t < nl) hl[t] = 0;
+    for (int i = t; i < (LPC_BS_T / 64) * LPC_BS_ND; i += LPC_BS_T) (&S.wc[0][0])[i] = 0;
+    __syncthreads();
+    constexpr int IPT = 4;
+    constexpr int CH = LPC_BS_T * IPT;
+    for (int64_t c0 = s0; c0 < s1; c0 += CH) {          // lo-digit counts of the bucket
+        uint32_t d[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const int64_t i = c0 + j * LPC_BS_T + t;
+            d[j] = i < s1 ? mlo[i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (d[j] != 0xffffffffu) atomicAdd(&hl[d[j]], 1u);
+    }
+    __syncthreads();
+    bs_excl_scan(hl, nl, staged ? 0u : (uint32_t)s0, lst, ws);
+    __syncthreads();
+    if (t < nl) S.run[t] = lst[t];
+    for (int64_t c0 = s0; c0 < s1; c0 += CH) {
+        uint32_t d[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const int64_t i = c0 + j * LPC_BS_T + t;
+            d[j] = i < s1 ? mlo[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const int64_t i = c0 + j * LPC_BS_T + t;
+            const bool valid = i < s1;
+            const uint32_t lp = bs_round(S, d[j], valid, lb, nl);
+            if (valid) {
+                if (staged) order[lp] = (uint16_t)(i - s0);
+                else perm[lp] = midx[i];
+            }
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    for (int64_t p = s0 + t; p < s1; p += LPC_BS_T) perm[p] = midx[s0 + order[p - s0]];
 }
 
 // Test entry (lpc_filter_eval, tests/test_gpu_filter.py): the device's own

@@ -101,6 +101,8 @@ struct lpc_handle {
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf w_aos;                                     // rays as 32-byte rows for the coherence gather
     int64_t onesweep_min = 500000;                  // onesweep radix sort from this many rays (merge sort below)
+    bool bsort = true;                              // counting sort (k_bkey..k_bsort2) for key windows <= 16 bits
+    DBuf w_bhist;                                   // its per-block hi-digit counts + digit totals
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
@@ -130,6 +132,7 @@ struct lpc_handle {
     bool sort_rays = true;
     int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
+    int64_t resort_min = INT64_MAX;                 // chained traced populations from this size are sorted again
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 24;                          // node visits before a wave hands over (0 off)
@@ -154,6 +157,7 @@ struct lpc_handle {
     bool pop_traced = false;                        // the population is in its parents' traced order
     bool pop_emitted = false;                       // the population is the emitted rays (set_rays)
     int init_key_lo = 0, init_key_hi = 32;          // key bits that vary over the emitted rays (set_rays)
+    bool init_bsort = false;                        // their sort may be the counting sort (bsort_fits)
     int queue = 2;                                  // LPC_QUEUE: 2 root items + k_rootwalk (default), 0 k_intersect
     int64_t q_walk_blocks = 16384;                  // k_rootwalk grid in 4-wave units (grid-stride)
     int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
@@ -651,6 +655,7 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
         RETIF(dalloc(h, h->w_aos, (size_t)C * 32));
         RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
+        RETIF(dalloc(h, h->w_bhist, ((size_t)LPC_BS_ND * ((C + LPC_BS_RPB - 1) / LPC_BS_RPB) + 2 * LPC_BS_ND + 8) * 4));
         size_t tb = 0;
         HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                                         (const int32_t *)nullptr, (int32_t *)nullptr, (size_t)C, 0,
@@ -967,7 +972,9 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // traced mode: the children come out in their parents' traced order and need
     // no sort of their own
     const bool chained_pop = traced && h->pop_traced;
-    const bool sorted = h->sort_rays && n >= h->sort_min && !chained_pop;
+    // a chained population keeps its parents' order, except a large one
+    // (LPC_RESORT_MIN): after many generations that order has lost its coherence
+    const bool sorted = h->sort_rays && n >= h->sort_min && (!chained_pop || (!ds && n >= h->resort_min));
     // the slot reset rides on k_raykey when it runs before everything that reads misc
     const bool fold_init = sorted && n >= LPC_MISC_WORDS;
     // Traced single-chunk iterations (k_shade_stage) leave every slot they read in
@@ -1018,16 +1025,35 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         // the emitted rays' varying key bits (set_rays)
         int b0 = 0, b1 = 32;
         if (traced && h->pop_emitted) { b0 = h->init_key_lo; b1 = h->init_key_hi; }
-        hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
-                           h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
-                           (float4 *)h->w_aos.p, SIk);
-        size_t tb = h->sort_tmp_bytes;
-        if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
-            HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
-                                                                 (size_t)n, b0, b1, h->stream));
-        else
-            HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
-                                                            b0, b1, h->stream));
+        const int nbits = b1 - b0;
+        if (traced && h->pop_emitted && h->init_bsort && nbits >= 1 && nbits <= 16 && n >= LPC_MISC_WORDS) {
+            // counting sort (MSD, two 8-bit digits, stable), then the gather
+            const int hb = std::min(nbits, LPC_BS_HB), lb = nbits - hb;
+            const int64_t nblk = (n + LPC_BS_RPB - 1) / LPC_BS_RPB;
+            uint32_t *hist = (uint32_t *)h->w_bhist.p, *tot = hist + (size_t)LPC_BS_ND * nblk;
+            uint32_t *bst = tot + LPC_BS_ND;
+            hipLaunchKernelGGL(k_bkey, dim3((unsigned)nblk), dim3(LPC_BS_T), 0, h->stream, in, n, h->box_lo[0],
+                               h->box_lo[1], h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin,
+                               (float4 *)h->w_aos.p, SIk, b0, lb, hb, hist, nblk);
+            hipLaunchKernelGGL(k_bprefix, dim3(1u << hb), dim3(256), 0, h->stream, hist, nblk, tot);
+            hipLaunchKernelGGL(k_bscatter, dim3((unsigned)nblk), dim3(LPC_BS_T), 0, h->stream, (const uint32_t *)kin,
+                               n, b0, lb, hb, (const uint32_t *)hist, nblk, (const uint32_t *)tot, bst,
+                               (uint8_t *)kout, vin, vout);
+            if (lb > 0)
+                hipLaunchKernelGGL(k_bsort2, dim3(1u << hb), dim3(LPC_BS_T), 0, h->stream, (const uint8_t *)kout,
+                                   (const int32_t *)vin, lb, (const uint32_t *)bst, vout);
+        } else {
+            hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
+                               h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
+                               (float4 *)h->w_aos.p, SIk);
+            size_t tb = h->sort_tmp_bytes;
+            if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
+                HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
+                                                                     (size_t)n, b0, b1, h->stream));
+            else
+                HIPCHK(h, rocprim::radix_sort_pairs<RaySortCfg>(h->w_sort_tmp.p, tb, kin, kout, vin, vout, (size_t)n,
+                                                                b0, b1, h->stream));
+        }
         perm = vout;
         hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
                            perm, (float *)h->w_rs.p, traced ? 1 : 0);
@@ -1251,11 +1277,13 @@ int lpc_open(int device, lpc_handle **out)
     h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
     h->sort_rays = env_int("LPC_SORT", 1) != 0;
     h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
+    h->bsort = env_int("LPC_BSORT", h->bsort) != 0;
     h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
     h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
     h->half = (int)env_int("LPC_HALF", h->half);
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
+    h->resort_min = std::max<int64_t>(1, env_int("LPC_RESORT_MIN", h->resort_min));
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
@@ -1323,7 +1351,7 @@ int lpc_close(lpc_handle *h)
     DBuf *bufs[] = {&h->d_nodes, &h->w_pk, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
-                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
+                    &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->w_bhist, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->d_misc, &h->d_wrec, &h->w_spill, &h->w_qroots,
                     &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl};
     for (DBuf *b : bufs) dfree(*b);
@@ -1670,6 +1698,44 @@ static int reset_measured(lpc_handle *h)
     return 0;
 }
 
+// May the emitted rays' coherence sort be the counting sort (k_bkey..k_bsort2)?
+// Its second level runs one block per hi bucket, so it pays only when no bucket
+// is large: a host estimate of the hi-digit counts (k_raykey's key, host float
+// arithmetic: a heuristic, the sort itself is exact either way).  A collimated
+// beam's few origin cells, or a narrow cone's few direction cells, go to rocPRIM.
+static bool bsort_fits(const lpc_handle *h, int64_t n, const float *o4, const float *d4)
+{
+    const int nbits = h->init_key_hi - h->init_key_lo;
+    if (!h->bsort || nbits < 1 || nbits > 16 || n < LPC_MISC_WORDS) return false;
+    const int hb = std::min(nbits, LPC_BS_HB), lb = nbits - hb;
+    if (lb == 0) return true;                              // one level: no per-bucket pass
+    std::vector<uint32_t> c((size_t)1 << hb, 0u);
+    auto spread2 = [](uint32_t x) { x &= 0xff; x = (x | (x << 4)) & 0x0f0f; x = (x | (x << 2)) & 0x3333;
+                                    return (x | (x << 1)) & 0x5555; };
+    auto spread3 = [](uint32_t x) { x &= 0x1f; x = (x | (x << 8)) & 0x100f; x = (x | (x << 4)) & 0x10c3;
+                                    return (x | (x << 2)) & 0x1249; };
+    uint32_t mx = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const float dx = d4[4 * i], dy = d4[4 * i + 1], dz = d4[4 * i + 2];
+        const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+        float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
+        if (dz < 0.0f) {
+            const float tx = (1.0f - fabsf(py)) * (px >= 0.0f ? 1.0f : -1.0f);
+            const float ty = (1.0f - fabsf(px)) * (py >= 0.0f ? 1.0f : -1.0f);
+            px = tx; py = ty;
+        }
+        const uint32_t du = (uint32_t)fminf(fmaxf((px * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
+        const uint32_t dv = (uint32_t)fminf(fmaxf((py * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
+        uint32_t oc[3];
+        for (int k = 0; k < 3; ++k)
+            oc[k] = (uint32_t)fminf(fmaxf((o4[4 * i + k] - h->box_lo[k]) * h->box_scale[k], 0.0f), 31.0f);
+        const uint32_t key = ((spread3(oc[0]) | (spread3(oc[1]) << 1) | (spread3(oc[2]) << 2)) << 16) |
+                             spread2(du) | (spread2(dv) << 1);
+        mx = std::max(mx, ++c[(key >> (h->init_key_lo + lb)) & ((1u << hb) - 1u)]);
+    }
+    return mx <= (uint32_t)LPC_BS_MAXB;
+}
+
 int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const float *dir4,
                        const float *pow, float max_ray_len, float ior_env)
 {
@@ -1695,6 +1761,7 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
         if (same_o) h->init_key_hi = 16;
         if (same_d) h->init_key_lo = 16;
         if (same_o && same_d) { h->init_key_lo = 0; h->init_key_hi = 8; }   // one digit pass
+        h->init_bsort = bsort_fits(h, n, origin4, dir4);
     }
     RETIF(check_dcap(h, h->init_dmax2));
     RETIF(pop_reserve(h, h->I, std::max<int64_t>(n, 1)));
@@ -2132,7 +2199,7 @@ static bool ds_ok(const lpc_handle *h, int64_t bound)
 {
     return h->spec && !h->xchg && h->traced && h->fuse_compact && h->early_acc && h->acc_map_dev &&
            (!h->prof || h->prof_light) && h->queue == 2 && !h->prof_waves && h->roots_s > 0 && bound > 0 &&
-           bound <= chunk_rays(h) && (bound + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
+           bound <= chunk_rays(h) && bound < h->resort_min && (bound + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
            (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES && h->K <= LPC_Q_MAX_SLOTS;
 }
 

@@ -15,6 +15,12 @@ Mirrors ``/root/reference/iterative_tracer.py``:
 Extra keyword ``keep_results=False`` selects the aggregate mode: no per-ray results
 cross PCIe; measured rays and per-mesh measured power stay on the device
 (``get_measured_rays`` / ``measured_power`` / the binning calls read them there).
+In that mode the measured rays of an iteration come in the device's coherence
+(traced) order, not the reference's ray order: the same rays bit for bit as a
+set, so order-dependent reductions over them (a float32 ``np.sum``, the stable
+sort behind ``get_beam_width_half_power``'s tie-breaking) can differ from the
+reference in the last bits.  ``keep_results=True`` (the default) keeps the
+reference's order (iteration, then ray).
 """
 from __future__ import annotations
 
@@ -138,7 +144,9 @@ class CL_Tracer:
         return self.engine.measured()[1]
 
     def get_measured_rays(self):
-        """End points and powers of every ray that hit a measure surface (:395-411)."""
+        """End points and powers of every ray that hit a measure surface (:395-411),
+        in the reference's order; in aggregate mode (``keep_results=False``) per
+        iteration in the device's traced order (see the module docstring)."""
         if self._aggregate:
             pos, pw, _ = self.engine.fetch_measured()
             return pos, pw

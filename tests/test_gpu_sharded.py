@@ -54,17 +54,20 @@ def _child(rank, world, port, name, n, hook, out_path):
     tr = ShardedTrace(eng, comm, iter_comm=iter_comm)
     in_pow = float(np.sum(p[lo:hi], dtype=np.float64))
     runs = []
+    eng.prof_read(reset=True)
     for rep in range(3):                        # back-to-back asynchronous traces (the bench's step)
         eng.reset()
         r = tr.run(sc.iterations, sc.tau, in_pow, wait=False)
         runs.append((r["global_counts"], list(map(float, r["mesh_power"])), r["bounces"]))
     eng.sync()
+    pr = eng.prof_read(reset=True)              # host time inside the per-iteration all-reduce hook
     eng.reset()
     r = tr.run(sc.iterations, sc.tau, in_pow, hist=(LIMITS, POINTS))
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump(dict(counts=r["global_counts"], mesh_power=list(map(float, r["mesh_power"])),
-                           hist=r["hist"][0].tolist(), runs=runs), f)
+                           hist=r["hist"][0].tolist(), runs=runs, xchg_us=pr["xchg_us"],
+                           xchg_calls=pr["xchg_calls"]), f)
     if hook == "shm":
         iter_comm.close()
     eng.close()
@@ -80,6 +83,11 @@ def test_sharded_trace_two_processes(oracle_mod, checker, tmp_path, name, n, hoo
     out = str(tmp_path / "r.json")
     mp.spawn(_child, args=(2, _free_port(), name, n, hook, out), nprocs=2, join=True)
     got = json.load(open(out))
+    # the exchange cost per iteration, kept with the GPU run's outputs
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "sharded.jsonl"), "a") as f:
+        f.write(json.dumps(dict(scene=name, n=n, hook=hook, calls=got["xchg_calls"],
+                                us_per_exchange=got["xchg_us"] / max(got["xchg_calls"], 1))) + "\n")
     sc = scenes.BUILDERS[name](n=n, seed=2)
     res, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
                                  bounce_fn=checker[0])
