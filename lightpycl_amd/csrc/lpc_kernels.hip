@@ -44,6 +44,11 @@ namespace lpck {
 // per-ray result flush, bit 1 = cull children behind the ray origin, bit 2 =
 // skip the exact tests (drains).
 __constant__ int lpc_dbg = 0;
+// Drain entries whose ray mask has at least this many rays are tested
+// triangle-uniform (the record by scalar loads, each lane its own ray, results
+// in registers); sparser ones are expanded into packed (triangle, ray) pairs.
+// 65 = packed only (LPC_DRAIN_U, read at lpc_open).
+__constant__ int lpc_drain_u = 8;
 
 // ---------------------------------------------------------------------------
 // Intersection.  Rays are processed in the coherence order (k_raykey + radix
@@ -281,6 +286,59 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
     auto drain = [&]() {
         if (nq == 0) return;
         if (PROF && (lpc_dbg & 4)) { nq = 0; return; }   // TIMING EXPERIMENT ONLY (results wrong): no exact tests
+        {   // dense entries: one triangle for all its rays at once (its record by
+            // scalar loads); the sparse entries move to the front of the queue for
+            // the packed pairs below
+            const bool ve = lane < nq;
+            const int32_t my_idx = ve ? L.qidx[lane] : 0;
+            const uint64_t my_mask = ve ? L.qmask[lane] : 0ull;
+            const uint64_t dense = __builtin_amdgcn_ballot_w64(ve && __builtin_popcountll(my_mask) >= lpc_drain_u);
+            if (dense) {
+                const bool keep = ve && !((dense >> lane) & 1ull);
+                const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+                if (keep) {
+                    const int pos = __builtin_popcountll(km & ((1ull << lane) - 1ull));
+                    L.qidx[pos] = my_idx;
+                    L.qmask[pos] = my_mask;
+                }
+                auto rl64 = [](uint64_t v, int l) -> uint64_t {
+                    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+                };
+                // this lane's own ray against each dense triangle, accumulated in
+                // registers with the same rule, then into its LDS accumulators
+                // (only this lane writes them here; the packed pairs' LDS atomics
+                // come later in this wave's program order)
+                unsigned long long ukey = key0;
+                int32_t ucnt = 0;
+                for (uint64_t dm = dense; dm; dm &= dm - 1) {
+                    const int e = __builtin_ctzll(dm);
+                    const int32_t idx = __builtin_amdgcn_readlane(my_idx, e);
+                    const uint64_t m = rl64(my_mask, e);
+                    const ExactRec x = xrec[idx];
+                    if ((m >> lane) & 1ull) {
+                        float t;
+                        if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
+                                     mk3(x.e2x, x.e2y, x.e2z), &t) && t > eps) {
+                            ++ucnt;
+                            if (t < max_ray_len) {
+                                const unsigned long long k = slot_key(t, idx);
+                                ukey = k < ukey ? k : ukey;
+                            }
+                        }
+                        if (PROF) ++n_exact;
+                    }
+                    n_pairs += (uint32_t)__builtin_popcountll(m);
+                }
+                if (ucnt) {
+                    L.lcnt[lane] += ucnt;
+                    const unsigned long long kl = L.lkey[lane];
+                    L.lkey[lane] = ukey < kl ? ukey : kl;
+                }
+                nq = __builtin_popcountll(km);
+                if (nq == 0) return;
+            }
+        }
         const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
         int incl = pc;
         for (int o = 1; o < 64; o <<= 1) {
@@ -1043,7 +1101,7 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
 #define LPC_BS_RPB 4096                    // rays per k_bkey / k_bscatter block
 #define LPC_BS_HB 8                        // hi digit bits (at most); lo digit <= 8 bits
 #define LPC_BS_ND (1 << LPC_BS_HB)
-#define LPC_BS_MAXB 16384                  // largest hi bucket k_bsort2 orders in LDS
+#define LPC_BS_MAXB 16384                  // largest hi bucket the host estimate admits (k_bsort2 chunks)
 
 // Rank of each lane's digit among the lower lanes with the same digit, and the
 // number of valid lanes with it (`valid` lanes only).
@@ -1234,64 +1292,65 @@ __global__ __launch_bounds__(LPC_BS_T) void k_bscatter(const uint32_t *__restric
     }
 }
 
-// One block per hi bucket: stable order of its (lo digit, ray) pairs by the lo
-// digit.  Buckets of <= LPC_BS_MAXB rays are ordered in LDS and perm written in
-// order (coalesced); a larger one (the host's estimate missed) writes each entry
-// where it goes.
+// Second level: block (bucket b = blockIdx.x, chunk c = blockIdx.y) orders the
+// c-th LPC_BS_RPB entries of hi bucket b by the lo digit, stably: an entry's
+// place is the bucket start + the bucket's entries of smaller lo digits (counted
+// over the whole bucket) + the entries of its digit in earlier chunks (counted
+// over those chunks) + its rank inside the chunk.  Chunks past the bucket's end
+// exit; a bucket needs at most LPC_BS_MAXB / LPC_BS_RPB chunks (the host's estimate),
+// a larger one is ordered by its last block, serially over its remaining chunks.
 __global__ __launch_bounds__(LPC_BS_T) void k_bsort2(const uint8_t *__restrict__ mlo,
                                                      const int32_t *__restrict__ midx, int lb,
                                                      const uint32_t *__restrict__ bst, int32_t *__restrict__ perm)
 {
     __shared__ BSortLds S;
-    __shared__ uint32_t hl[LPC_BS_ND], lst[LPC_BS_ND + 1];
+    __shared__ uint32_t hl[LPC_BS_ND], hb4[LPC_BS_ND], lst[LPC_BS_ND + 1];
     __shared__ uint32_t ws[LPC_BS_T / 64];
-    __shared__ uint16_t order[LPC_BS_MAXB];            // bucket-local entry of each output position
     const int nl = 1 << lb;
     const int t = threadIdx.x;
     const int64_t s0 = bst[blockIdx.x], s1 = bst[blockIdx.x + 1];
-    if (s1 <= s0) return;                               // block-uniform
-    const bool staged = s1 - s0 <= LPC_BS_MAXB;
-    if (t < nl) hl[t] = 0;
+    const int64_t c0 = s0 + (int64_t)blockIdx.y * LPC_BS_RPB;
+    if (c0 >= s1) return;                               // block-uniform
+    // the last chunk block takes every chunk from its own to the bucket's end
+    const bool last = blockIdx.y + 1 == gridDim.y;
+    const int64_t c1 = last ? s1 : min(s1, c0 + LPC_BS_RPB);
+    if (t < nl) { hl[t] = 0; hb4[t] = 0; }
     for (int i = t; i < (LPC_BS_T / 64) * LPC_BS_ND; i += LPC_BS_T) (&S.wc[0][0])[i] = 0;
     __syncthreads();
-    constexpr int IPT = 4;
-    constexpr int CH = LPC_BS_T * IPT;
-    for (int64_t c0 = s0; c0 < s1; c0 += CH) {          // lo-digit counts of the bucket
+    constexpr int IPT = LPC_BS_RPB / LPC_BS_T;
+    for (int64_t e0 = s0; e0 < s1; e0 += LPC_BS_RPB) {  // lo-digit counts: the bucket, and before c0
         uint32_t d[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
-            const int64_t i = c0 + j * LPC_BS_T + t;
+            const int64_t i = e0 + j * LPC_BS_T + t;
             d[j] = i < s1 ? mlo[i] : 0xffffffffu;
         }
 #pragma unroll
-        for (int j = 0; j < IPT; ++j)
-            if (d[j] != 0xffffffffu) atomicAdd(&hl[d[j]], 1u);
+        for (int j = 0; j < IPT; ++j) {
+            if (d[j] == 0xffffffffu) continue;
+            atomicAdd(&hl[d[j]], 1u);
+            if (e0 + j * LPC_BS_T + t < c0) atomicAdd(&hb4[d[j]], 1u);
+        }
     }
     __syncthreads();
-    bs_excl_scan(hl, nl, staged ? 0u : (uint32_t)s0, lst, ws);
+    bs_excl_scan(hl, nl, (uint32_t)s0, lst, ws);
     __syncthreads();
-    if (t < nl) S.run[t] = lst[t];
-    for (int64_t c0 = s0; c0 < s1; c0 += CH) {
+    if (t < nl) S.run[t] = lst[t] + hb4[t];
+    for (int64_t e0 = c0; e0 < c1; e0 += LPC_BS_RPB) {
         uint32_t d[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
-            const int64_t i = c0 + j * LPC_BS_T + t;
-            d[j] = i < s1 ? mlo[i] : 0u;
+            const int64_t i = e0 + j * LPC_BS_T + t;
+            d[j] = i < c1 ? mlo[i] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
-            const int64_t i = c0 + j * LPC_BS_T + t;
-            const bool valid = i < s1;
-            const uint32_t lp = bs_round(S, d[j], valid, lb, nl);
-            if (valid) {
-                if (staged) order[lp] = (uint16_t)(i - s0);
-                else perm[lp] = midx[i];
-            }
+            const int64_t i = e0 + j * LPC_BS_T + t;
+            const bool valid = i < c1;
+            const uint32_t pos = bs_round(S, d[j], valid, lb, nl);
+            if (valid) perm[pos] = midx[i];
         }
     }
-    if (!staged) return;
-    __syncthreads();
-    for (int64_t p = s0 + t; p < s1; p += LPC_BS_T) perm[p] = midx[s0 + order[p - s0]];
 }
 
 // Test entry (lpc_filter_eval, tests/test_gpu_filter.py): the device's own
@@ -1396,7 +1455,8 @@ static __device__ __forceinline__ ShadeOut shade_ray(const ShadeArgs &A, int64_t
     A.o.tdx[r] = s.t_dir.x; A.o.tdy[r] = s.t_dir.y; A.o.tdz[r] = s.t_dir.z;
     A.o.tpw[r] = s.t_pow; A.o.tms[r] = s.t_meas;
     if (A.o.iidx) {
-        A.o.iidx[r] = po.hit_idx; A.o.n1[r] = po.n1; A.o.n2[r] = po.n2; A.o.ent[r] = po.entering;
+        A.o.iidx[r] = po.hit_idx; A.o.n1[r] = po.n1; A.o.n2[r] = po.n2;
+        A.o.ent[r] = po.hit_mesh >= 0 ? po.entering : 0;   // no hit: the reference's zeroed buffer (iterative_tracer.py:230)
     }
     return s;
 }

@@ -132,7 +132,7 @@ struct lpc_handle {
     bool sort_rays = true;
     int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
-    int64_t resort_min = INT64_MAX;                 // chained traced populations from this size are sorted again
+    int64_t resort_min = 2000000;                   // chained traced populations from this size are sorted again
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 24;                          // node visits before a wave hands over (0 off)
@@ -1040,7 +1040,8 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                n, b0, lb, hb, (const uint32_t *)hist, nblk, (const uint32_t *)tot, bst,
                                (uint8_t *)kout, vin, vout);
             if (lb > 0)
-                hipLaunchKernelGGL(k_bsort2, dim3(1u << hb), dim3(LPC_BS_T), 0, h->stream, (const uint8_t *)kout,
+                hipLaunchKernelGGL(k_bsort2, dim3(1u << hb, LPC_BS_MAXB / LPC_BS_RPB), dim3(LPC_BS_T), 0, h->stream,
+                                   (const uint8_t *)kout,
                                    (const int32_t *)vin, lb, (const uint32_t *)bst, vout);
         } else {
             hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
@@ -1312,6 +1313,8 @@ int lpc_open(int device, lpc_handle **out)
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
+        const int du = (int)std::min<int64_t>(65, std::max<int64_t>(1, env_int("LPC_DRAIN_U", 8)));
+        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_drain_u), &du, sizeof(du)));
     }
     h->q_target = std::max<int64_t>(1, env_int("LPC_Q_TARGET", h->q_target));
     h->early_acc = env_int("LPC_EARLY_ACC", h->early_acc) != 0;

@@ -24,7 +24,7 @@ def bounce_stats(a, b, max_ray_len):
     rays whose discrete outputs agree."""
     n = len(a["isect_mid"])
     disc = np.zeros(n, bool)
-    for k in ("isect_mid", "isect_idx", "meas", "r_meas", "t_meas", "n1", "n2"):
+    for k in ("isect_mid", "isect_idx", "meas", "r_meas", "t_meas", "n1", "n2", "entering"):
         disc |= np.asarray(a[k]).reshape(-1) != np.asarray(b[k]).reshape(-1)
     same = ~disc
     out = dict(n=n, id_mismatch=int(disc.sum()))

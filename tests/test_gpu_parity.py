@@ -45,11 +45,11 @@ def _cmp_bounce(g, o, exact=True):
     """exact: bit for bit (the reference kernels).  Otherwise (the CPU oracle):
     decisions and destinations bit for bit, children within the hardware
     rsqrt's ulp as it propagates through the Fresnel formulas."""
-    hit = o["isect_mid"] >= 0
     for k in ("isect_mid", "n1", "n2", "r_meas", "t_meas", "meas"):
         np.testing.assert_array_equal(g[k], o[k], err_msg=k)
     np.testing.assert_array_equal(g["isect_idx"], o["isect_idx"], err_msg="isect_idx")
-    np.testing.assert_array_equal(g["entering"][hit], o["entering"][hit], err_msg="entering")
+    # no hit: the reference leaves its zeroed buffer (iterative_tracer.py:230), liblpc writes 0
+    np.testing.assert_array_equal(g["entering"], o["entering"], err_msg="entering")
     np.testing.assert_array_equal(g["dest"][:, :3], o["dest"][:, :3], err_msg="dest")
     for k in ("r_dir", "t_dir", "pow", "r_pow", "t_pow"):
         a = g[k][:, :3] if g[k].ndim == 2 else g[k]
@@ -529,3 +529,39 @@ def test_counting_sort_equals_radix_sort(monkeypatch, name, n):
     assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
     for x, y in zip(a[3:], b[3:]):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n", [("lens", 30000), ("eye", 3000)])
+def test_resort_equals_chained(monkeypatch, name, n):
+    """Large chained populations sorted again (LPC_RESORT_MIN; default 2 M rays,
+    here forced from 1000) against the children kept in their parents' traced
+    order: the same per-ray results in another order, so identical per-iteration
+    counts and the identical measured rays as a set, per-mesh power to float64
+    summation order."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.BUILDERS[name](n=n, seed=31)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+    out = []
+    for rmin in ("1000", "1000000000000"):
+        monkeypatch.setenv("LPC_RESORT_MIN", rmin)
+        e = Engine(0)
+        try:
+            e.upload_meshes(sc.meshes)
+            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+            for rep in range(2):
+                e.reset()
+                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+            pos, p, mm = e.fetch_measured()
+            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm))
+        finally:
+            e.close()
+    a, b = out
+    assert a[0] == b[0] and a[1] == b[1]
+    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)
+
+    def rows(pos, p, mm):
+        r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
+        return r[np.lexsort(r.T[::-1])]
+    np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
