@@ -111,10 +111,13 @@ def _preload_hip_runtime():
 
 
 def load(path: str = LIB_PATH):
-    """Load liblpc.so and declare every entry point of include/lpc.h."""
+    """Load liblpc.so and declare every entry point of include/lpc.h.
+    LPC_LIB_PATH names another in-tree build of the same sources (A/B of
+    compile-time variants, tools/ab.py); the default is lightpycl_amd/liblpc.so."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("LPC_LIB_PATH") or path
     _preload_hip_runtime()
     if not os.path.exists(path):
         raise LpcError(f"liblpc.so not built ({path}); run lightpycl_amd.build.build() "

@@ -48,7 +48,16 @@ __constant__ int lpc_dbg = 0;
 // triangle-uniform (the record by scalar loads, each lane its own ray, results
 // in registers); sparser ones are expanded into packed (triangle, ray) pairs.
 // 65 = packed only (LPC_DRAIN_U, read at lpc_open).
-__constant__ int lpc_drain_u = 8;
+__constant__ int lpc_drain_u = 24;
+// Compile-time variants (A/B builds, tools/build_variant.sh): the packed drain
+// with the next step's records requested ahead (LPC_DRAIN_PIPE), and the
+// hierarchy kernels' launch bounds in waves per SIMD (LPC_WALK_MINB).
+#ifndef LPC_DRAIN_PIPE
+#define LPC_DRAIN_PIPE 0
+#endif
+#ifndef LPC_WALK_MINB
+#define LPC_WALK_MINB 6
+#endif
 
 // ---------------------------------------------------------------------------
 // Intersection.  Rays are processed in the coherence order (k_raykey + radix
@@ -311,11 +320,15 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                 // come later in this wave's program order)
                 unsigned long long ukey = key0;
                 int32_t ucnt = 0;
-                for (uint64_t dm = dense; dm; dm &= dm - 1) {
-                    const int e = __builtin_ctzll(dm);
-                    const int32_t idx = __builtin_amdgcn_readlane(my_idx, e);
-                    const uint64_t m = rl64(my_mask, e);
-                    const ExactRec x = xrec[idx];
+                uint64_t dm = dense;
+                int32_t idx = __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dm));
+                ExactRec x = xrec[idx];
+                for (; dm; dm &= dm - 1) {
+                    const uint64_t m = rl64(my_mask, __builtin_ctzll(dm));
+                    // the next dense entry's record, loaded while this one is tested
+                    const uint64_t dn = dm & (dm - 1);
+                    const int32_t nidx = dn ? __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dn)) : idx;
+                    const ExactRec nx = xrec[nidx];
                     if ((m >> lane) & 1ull) {
                         float t;
                         if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
@@ -329,6 +342,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                         if (PROF) ++n_exact;
                     }
                     n_pairs += (uint32_t)__builtin_popcountll(m);
+                    idx = nidx;
+                    x = nx;
                 }
                 if (ucnt) {
                     L.lcnt[lane] += ucnt;
@@ -348,6 +363,44 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
         L.qscan[lane] = incl;
         const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
         n_pairs += (uint32_t)total;
+#if LPC_DRAIN_PIPE
+        // 64 pairs per step, one per lane; the next step's pair is located and its
+        // record requested before this step's tests (two gathers in flight)
+        auto locate = [&](int q, int &r, int32_t &idx) {
+            int e = 0;                             // first entry with qscan[e] > q
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
+            const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
+            r = select_bit(L.qmask[e], k);
+            idx = L.qidx[e];
+        };
+        int r0 = 0;
+        int32_t i0 = ~0;
+        if (lane < total) locate(lane, r0, i0);
+        ExactRec x0 = xrec[i0 >= 0 ? i0 : 0];
+        for (int base = 0; base < total; base += 64) {
+            const int q1 = base + 64 + lane;
+            int r1 = 0;
+            int32_t i1 = ~0;
+            if (q1 < total) locate(q1, r1, i1);
+            const ExactRec x1 = xrec[i1 >= 0 ? i1 : 0];
+            if (i0 >= 0) {
+                const f3 Or = mk3(L.ray[0][r0], L.ray[1][r0], L.ray[2][r0]);
+                const f3 Dr = mk3(L.ray[3][r0], L.ray[4][r0], L.ray[5][r0]);
+                float t;
+                if (mt_exact(Or, Dr, mk3(x0.v0x, x0.v0y, x0.v0z), mk3(x0.e1x, x0.e1y, x0.e1z),
+                             mk3(x0.e2x, x0.e2y, x0.e2z), &t) && t > eps) {
+                    atomicAdd(&L.lcnt[r0], 1);
+                    if (t < max_ray_len) atomicMin(&L.lkey[r0], slot_key(t, i0));
+                }
+                if (PROF) ++n_exact;
+            }
+            r0 = r1;
+            i0 = i1;
+            x0 = x1;
+        }
+#else
         for (int base = 0; base < total; base += 64) {
             const int q = base + lane;
             if (q < total) {
@@ -370,6 +423,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                 if (PROF) ++n_exact;
             }
         }
+#endif
         nq = 0;
     };
     int budget = SP.budget;
@@ -438,12 +492,13 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
                     for (int q = 0; q < W; ++q)
                         if (any_lane(d[q] <= 0.0f)) L.stack[top++] = __builtin_amdgcn_readfirstlane(nr[q]);
                 } else {                                                 // leaf: triangles -> exact-test queue
+                    if (nq > 64 - W) drain();                            // room for the leaf's W entries
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
                         const uint64_t m = __builtin_amdgcn_ballot_w64(d[q] <= 0.0f);
                         if (!m) continue;
                         if (lane == 0) { L.qidx[nq] = ~nr[q]; L.qmask[nq] = m; }
-                        if (++nq == 64) drain();
+                        ++nq;
                     }
                 }
             }
@@ -479,12 +534,13 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
             for (int k = 0; k < W; ++k)
                 if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
         } else {                                   // leaf: triangles ~ref -> exact-test queue
+            if (nq > 64 - W) drain();              // room for the leaf's W entries (one drain site per node)
 #pragma unroll
             for (int k = 0; k < W; ++k) {
                 const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
                 if (!m) continue;
                 if (lane == 0) { L.qidx[nq] = ~N.ref[k]; L.qmask[nq] = m; }
-                if (++nq == 64) drain();
+                ++nq;
             }
         }
     }
@@ -565,7 +621,7 @@ __global__ __launch_bounds__(256, 6) void k_intersect(RaysIn R, const float *__r
 // level's queue (`out`; budget 0 on the last level).  One wave per block (a
 // wave's slot frees when its items end, see k_rootwalk).
 template <int W, bool PROF = false, bool HALF = false, int NB = 1>
-__global__ __launch_bounds__(64, 6) void k_spill(RayBase ray, int64_t n,
+__global__ __launch_bounds__(64, LPC_WALK_MINB) void k_spill(RayBase ray, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
@@ -844,7 +900,7 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
 // 4-wave block holds its LDS until its slowest item ends (round 2 per-item
 // records: ~2 800 of 6 144 wave slots walking on average with 4).
 template <int W, bool PROF = false, bool HALF = false, int NB = 1>
-__global__ __launch_bounds__(64, 6) void k_rootwalk(RayBase ray, int64_t n,
+__global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,

@@ -1313,7 +1313,7 @@ int lpc_open(int device, lpc_handle **out)
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
-        const int du = (int)std::min<int64_t>(65, std::max<int64_t>(1, env_int("LPC_DRAIN_U", 8)));
+        const int du = (int)std::min<int64_t>(65, std::max<int64_t>(1, env_int("LPC_DRAIN_U", 24)));
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_drain_u), &du, sizeof(du)));
     }
     h->q_target = std::max<int64_t>(1, env_int("LPC_Q_TARGET", h->q_target));
