@@ -20,3 +20,5 @@ grep scene gpurun_out/r3s_eye.log | python -c "
 import sys,json
 for l in sys.stdin:
     tag,js=l.split(' ',1); d=json.loads(js); print(tag,d['scene'],round(d['ms_per_trace'],3),round(d['ray_bounces_per_s']/1e9,3))"
+bash tools/pmc_probe.sh "k_shade_stage|k_roots_s|k_stage_move|k_slivers|k_bsort2|k_bscatter|k_rootwalk|k_spill" > gpurun_out/r3s_pmc.txt 2>&1 || { tail -20 gpurun_out/r3s_pmc.txt; exit 1; }
+cut -c1-260 gpurun_out/r3s_pmc.txt | head -60
