@@ -843,8 +843,19 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
             uint64_t ml = 0;                    // this lane's ray: bit k = piece cls + S k passes
             auto test = [&](int lo, int hi) {   // the class's pieces in [lo, hi)
                 const int p0 = lo + ((cls - lo % S) % S + S) % S;
-#pragma unroll 4
-                for (int p = p0, k = p0 / S; p < hi; p += S, ++k) {
+                int p = p0, k = p0 / S;
+                // two pieces per packed-FP32 test (each half one evaluation of the
+                // scalar test's formula: the same conservative filter)
+#pragma unroll 2
+                for (; p + S < hi; p += 2 * S, k += 2) {
+                    const float4 c0 = L.pc[p], c1 = L.pc[p + S];
+                    const lpc_f2 cx = {c0.x, c1.x}, cy = {c0.y, c1.y}, cz = {c0.z, c1.z}, nb = {c0.w, c1.w};
+                    const lpc_f2 na = {L.pa[p], L.pa[p + S]};
+                    const lpc_f2 d = HALF ? filter_test2h(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz)
+                                          : filter_test2(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz);
+                    ml |= ((uint64_t)(d.x <= 0.0f) << k) | ((uint64_t)(d.y <= 0.0f) << (k + 1));
+                }
+                if (p < hi) {
                     const float4 c = L.pc[p];
                     const float a = L.pa[p];
                     const float d = HALF ? filter_testh(c.x, c.y, c.z, c.w, a, O.x, O.y, O.z, nx, ny, nz)
