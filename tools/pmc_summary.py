@@ -41,8 +41,21 @@ if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
            "kernels_sha16": hashlib.sha256(open(os.path.join(root, "lightpycl_amd", "csrc", "lpc_kernels.hip"),
                                                 "rb").read()).hexdigest()[:16],
            "note": f"mean over the {kname} launches of one bench step (all iterations)"}
-    for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES",
+              "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
         if c in ki:
             rec[c.lower() + "_mean"] = ki[c]["mean"]
+    # the primary (1 M-ray) launches alone: bench.py --steps 1 --warmup 0 runs the
+    # first iteration by itself (launch 0), then traces of three iterations each
+    # (pre-warm, timed, histogram): launches 1, 4, 7, ... are primaries
+    prim = {}
+    for c, v in ki.items():
+        idx = [0] + [i for i in range(1, len(v["values"])) if (i - 1) % 3 == 0]
+        vals = [v["values"][i] for i in idx if i < len(v["values"])]
+        if vals:
+            prim[c] = sum(vals) / len(vals)
+    if "FETCH_SIZE" in prim and "WRITE_SIZE" in prim:
+        prim["hbm_bytes"] = (2.0 * prim["FETCH_SIZE"] + prim["WRITE_SIZE"]) * 1024.0
+    rec["primary_launch"] = prim
     json.dump(rec, open(os.path.join(out, "pmc_intersect.json"), "w"), indent=1)
     print(json.dumps(rec, indent=1))
