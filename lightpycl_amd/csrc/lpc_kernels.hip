@@ -239,6 +239,153 @@ struct WaveLds {
     int32_t lcnt[64];                  // per-ray hit count
 };
 
+// Drain a wave's queue of deferred exact tests: entries (triangle ~idx, mask of
+// the wave's rays) in L.qidx / L.qmask [0, nq), results folded into the per-ray
+// accumulators L.lkey / L.lcnt (minimal slot_key(t, idx) for t < max_ray_len, a
+// count for every accepted t > eps: mt_accumulate's rule).  Dense entries
+// (>= lpc_drain_u rays) are tested triangle-uniform, the rest as packed
+// (triangle, ray) pairs, 64 per step (ray r = lane r's ray: O, D in that lane,
+// L.ray for the packed pairs).
+template <bool PROF>
+static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, const int lane,
+                                                   const ExactRec *__restrict__ xrec, const float eps,
+                                                   const float max_ray_len, const unsigned long long key0,
+                                                   const f3 &O, const f3 &D, uint32_t &n_pairs, uint32_t &n_exact)
+{
+    if (nq == 0) return;
+    if (PROF && (lpc_dbg & 4)) { nq = 0; return; }   // TIMING EXPERIMENT ONLY (results wrong): no exact tests
+    {   // dense entries: one triangle for all its rays at once (its record by
+        // scalar loads); the sparse entries move to the front of the queue for
+        // the packed pairs below
+        const bool ve = lane < nq;
+        const int32_t my_idx = ve ? L.qidx[lane] : 0;
+        const uint64_t my_mask = ve ? L.qmask[lane] : 0ull;
+        const uint64_t dense = __builtin_amdgcn_ballot_w64(ve && __builtin_popcountll(my_mask) >= lpc_drain_u);
+        if (dense) {
+            const bool keep = ve && !((dense >> lane) & 1ull);
+            const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+            if (keep) {
+                const int pos = __builtin_popcountll(km & ((1ull << lane) - 1ull));
+                L.qidx[pos] = my_idx;
+                L.qmask[pos] = my_mask;
+            }
+            auto rl64 = [](uint64_t v, int l) -> uint64_t {
+                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+            };
+            // this lane's own ray against each dense triangle, accumulated in
+            // registers with the same rule, then into its LDS accumulators
+            // (only this lane writes them here; the packed pairs' LDS atomics
+            // come later in this wave's program order)
+            unsigned long long ukey = key0;
+            int32_t ucnt = 0;
+            uint64_t dm = dense;
+            int32_t idx = __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dm));
+            ExactRec x = xrec[idx];
+            for (; dm; dm &= dm - 1) {
+                const uint64_t m = rl64(my_mask, __builtin_ctzll(dm));
+                // the next dense entry's record, loaded while this one is tested
+                const uint64_t dn = dm & (dm - 1);
+                const int32_t nidx = dn ? __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dn)) : idx;
+                const ExactRec nx = xrec[nidx];
+                if ((m >> lane) & 1ull) {
+                    float t;
+                    if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
+                                 mk3(x.e2x, x.e2y, x.e2z), &t) && t > eps) {
+                        ++ucnt;
+                        if (t < max_ray_len) {
+                            const unsigned long long k = slot_key(t, idx);
+                            ukey = k < ukey ? k : ukey;
+                        }
+                    }
+                    if (PROF) ++n_exact;
+                }
+                n_pairs += (uint32_t)__builtin_popcountll(m);
+                idx = nidx;
+                x = nx;
+            }
+            if (ucnt) {
+                L.lcnt[lane] += ucnt;
+                const unsigned long long kl = L.lkey[lane];
+                L.lkey[lane] = ukey < kl ? ukey : kl;
+            }
+            nq = __builtin_popcountll(km);
+            if (nq == 0) return;
+        }
+    }
+    const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
+    int incl = pc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    L.qscan[lane] = incl;
+    const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+    n_pairs += (uint32_t)total;
+#if LPC_DRAIN_PIPE
+    // 64 pairs per step, one per lane; the next step's pair is located and its
+    // record requested before this step's tests (two gathers in flight)
+    auto locate = [&](int q, int &r, int32_t &idx) {
+        int e = 0;                             // first entry with qscan[e] > q
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
+        const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
+        r = select_bit(L.qmask[e], k);
+        idx = L.qidx[e];
+    };
+    int r0 = 0;
+    int32_t i0 = ~0;
+    if (lane < total) locate(lane, r0, i0);
+    ExactRec x0 = xrec[i0 >= 0 ? i0 : 0];
+    for (int base = 0; base < total; base += 64) {
+        const int q1 = base + 64 + lane;
+        int r1 = 0;
+        int32_t i1 = ~0;
+        if (q1 < total) locate(q1, r1, i1);
+        const ExactRec x1 = xrec[i1 >= 0 ? i1 : 0];
+        if (i0 >= 0) {
+            const f3 Or = mk3(L.ray[0][r0], L.ray[1][r0], L.ray[2][r0]);
+            const f3 Dr = mk3(L.ray[3][r0], L.ray[4][r0], L.ray[5][r0]);
+            float t;
+            if (mt_exact(Or, Dr, mk3(x0.v0x, x0.v0y, x0.v0z), mk3(x0.e1x, x0.e1y, x0.e1z),
+                         mk3(x0.e2x, x0.e2y, x0.e2z), &t) && t > eps) {
+                atomicAdd(&L.lcnt[r0], 1);
+                if (t < max_ray_len) atomicMin(&L.lkey[r0], slot_key(t, i0));
+            }
+            if (PROF) ++n_exact;
+        }
+        r0 = r1;
+        i0 = i1;
+        x0 = x1;
+    }
+#else
+    for (int base = 0; base < total; base += 64) {
+        const int q = base + lane;
+        if (q < total) {
+            int e = 0;                         // first entry with qscan[e] > q
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
+            const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
+            const int r = select_bit(L.qmask[e], k);
+            const int32_t idx = L.qidx[e];
+            const ExactRec x = xrec[idx];
+            const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
+            const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
+            float t;
+            if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
+                t > eps) {
+                atomicAdd(&L.lcnt[r], 1);
+                if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
+            }
+            if (PROF) ++n_exact;
+        }
+    }
+#endif
+    nq = 0;
+}
+
 // One packet (64 rays of the coherence order from w*64, one per lane) against
 // one piece (a subtree of one mesh run).  The wave walks the subtree with a
 // wave-uniform stack in LDS: a node's four children are tested against all 64
@@ -292,140 +439,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
     // results into the per-ray accumulators with LDS atomics: atomicMin on
     // slot_key(t, idx) for t < max_ray_len and a count for every accepted t > eps,
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
-    auto drain = [&]() {
-        if (nq == 0) return;
-        if (PROF && (lpc_dbg & 4)) { nq = 0; return; }   // TIMING EXPERIMENT ONLY (results wrong): no exact tests
-        {   // dense entries: one triangle for all its rays at once (its record by
-            // scalar loads); the sparse entries move to the front of the queue for
-            // the packed pairs below
-            const bool ve = lane < nq;
-            const int32_t my_idx = ve ? L.qidx[lane] : 0;
-            const uint64_t my_mask = ve ? L.qmask[lane] : 0ull;
-            const uint64_t dense = __builtin_amdgcn_ballot_w64(ve && __builtin_popcountll(my_mask) >= lpc_drain_u);
-            if (dense) {
-                const bool keep = ve && !((dense >> lane) & 1ull);
-                const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
-                if (keep) {
-                    const int pos = __builtin_popcountll(km & ((1ull << lane) - 1ull));
-                    L.qidx[pos] = my_idx;
-                    L.qmask[pos] = my_mask;
-                }
-                auto rl64 = [](uint64_t v, int l) -> uint64_t {
-                    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-                };
-                // this lane's own ray against each dense triangle, accumulated in
-                // registers with the same rule, then into its LDS accumulators
-                // (only this lane writes them here; the packed pairs' LDS atomics
-                // come later in this wave's program order)
-                unsigned long long ukey = key0;
-                int32_t ucnt = 0;
-                uint64_t dm = dense;
-                int32_t idx = __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dm));
-                ExactRec x = xrec[idx];
-                for (; dm; dm &= dm - 1) {
-                    const uint64_t m = rl64(my_mask, __builtin_ctzll(dm));
-                    // the next dense entry's record, loaded while this one is tested
-                    const uint64_t dn = dm & (dm - 1);
-                    const int32_t nidx = dn ? __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dn)) : idx;
-                    const ExactRec nx = xrec[nidx];
-                    if ((m >> lane) & 1ull) {
-                        float t;
-                        if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
-                                     mk3(x.e2x, x.e2y, x.e2z), &t) && t > eps) {
-                            ++ucnt;
-                            if (t < max_ray_len) {
-                                const unsigned long long k = slot_key(t, idx);
-                                ukey = k < ukey ? k : ukey;
-                            }
-                        }
-                        if (PROF) ++n_exact;
-                    }
-                    n_pairs += (uint32_t)__builtin_popcountll(m);
-                    idx = nidx;
-                    x = nx;
-                }
-                if (ucnt) {
-                    L.lcnt[lane] += ucnt;
-                    const unsigned long long kl = L.lkey[lane];
-                    L.lkey[lane] = ukey < kl ? ukey : kl;
-                }
-                nq = __builtin_popcountll(km);
-                if (nq == 0) return;
-            }
-        }
-        const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
-        int incl = pc;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        L.qscan[lane] = incl;
-        const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
-        n_pairs += (uint32_t)total;
-#if LPC_DRAIN_PIPE
-        // 64 pairs per step, one per lane; the next step's pair is located and its
-        // record requested before this step's tests (two gathers in flight)
-        auto locate = [&](int q, int &r, int32_t &idx) {
-            int e = 0;                             // first entry with qscan[e] > q
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
-            const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
-            r = select_bit(L.qmask[e], k);
-            idx = L.qidx[e];
-        };
-        int r0 = 0;
-        int32_t i0 = ~0;
-        if (lane < total) locate(lane, r0, i0);
-        ExactRec x0 = xrec[i0 >= 0 ? i0 : 0];
-        for (int base = 0; base < total; base += 64) {
-            const int q1 = base + 64 + lane;
-            int r1 = 0;
-            int32_t i1 = ~0;
-            if (q1 < total) locate(q1, r1, i1);
-            const ExactRec x1 = xrec[i1 >= 0 ? i1 : 0];
-            if (i0 >= 0) {
-                const f3 Or = mk3(L.ray[0][r0], L.ray[1][r0], L.ray[2][r0]);
-                const f3 Dr = mk3(L.ray[3][r0], L.ray[4][r0], L.ray[5][r0]);
-                float t;
-                if (mt_exact(Or, Dr, mk3(x0.v0x, x0.v0y, x0.v0z), mk3(x0.e1x, x0.e1y, x0.e1z),
-                             mk3(x0.e2x, x0.e2y, x0.e2z), &t) && t > eps) {
-                    atomicAdd(&L.lcnt[r0], 1);
-                    if (t < max_ray_len) atomicMin(&L.lkey[r0], slot_key(t, i0));
-                }
-                if (PROF) ++n_exact;
-            }
-            r0 = r1;
-            i0 = i1;
-            x0 = x1;
-        }
-#else
-        for (int base = 0; base < total; base += 64) {
-            const int q = base + lane;
-            if (q < total) {
-                int e = 0;                         // first entry with qscan[e] > q
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
-                const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
-                const int r = select_bit(L.qmask[e], k);
-                const int32_t idx = L.qidx[e];
-                const ExactRec x = xrec[idx];
-                const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
-                const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
-                float t;
-                if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
-                    t > eps) {
-                    atomicAdd(&L.lcnt[r], 1);
-                    if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
-                }
-                if (PROF) ++n_exact;
-            }
-        }
-#endif
-        nq = 0;
-    };
+    auto drain = [&]() { drain_queue<PROF>(L, nq, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact); };
     int budget = SP.budget;
     L.stack[top++] = start >= 0 ? start : P.root;
     while (top > 0) {

@@ -102,6 +102,7 @@ _POLICIES = [
     dict(LPC_WALK_NB="4", LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
     # work hand-over: budgets, a queue that overflows
     dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_BUDGET="0"),
+    dict(LPC_BUDGET="0", LPC_HALF="1"),
     dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
     dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"),
     dict(LPC_LARGE_N="1000"), dict(LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3"),
