@@ -1920,10 +1920,30 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         // iteration counters: fixed-order power sum, max |dir|^2
         double lp = 0.0, lm[LPC_MP_MAX] = {0.0, 0.0, 0.0, 0.0};
         float ld = 0.0f;
-        for (int64_t j = t; j < ntiles; j += LPC_ST_TILE) {
-            lp += A.tpow[j];
-            ld = fmaxf(ld, __uint_as_float(A.tdm[j]));
-            for (int m = 0; m < A.nmp; ++m) lm[m] += A.tmp[j * LPC_MP_MAX + m];
+        // eight of this thread's tiles per round, loaded before they are added
+        // (one load latency per round instead of one per tile; same order of adds)
+        constexpr int UB = 8;
+        for (int64_t j0 = t; j0 < ntiles; j0 += (int64_t)UB * LPC_ST_TILE) {
+            double vp[UB], vm[UB][LPC_MP_MAX];
+            uint32_t vd[UB];
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                const int64_t j = j0 + (int64_t)u * LPC_ST_TILE;
+                const bool ok = j < ntiles;
+                vp[u] = ok ? A.tpow[j] : 0.0;
+                vd[u] = ok ? A.tdm[j] : 0u;
+#pragma unroll
+                for (int m = 0; m < LPC_MP_MAX; ++m) vm[u][m] = (ok && m < A.nmp) ? A.tmp[j * LPC_MP_MAX + m] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                if (j0 + (int64_t)u * LPC_ST_TILE >= ntiles) break;
+                lp += vp[u];
+                ld = fmaxf(ld, __uint_as_float(vd[u]));
+#pragma unroll
+                for (int m = 0; m < LPC_MP_MAX; ++m)
+                    if (m < A.nmp) lm[m] += vm[u][m];
+            }
         }
         s_p[t] = lp;
         s_d[t] = ld;
