@@ -241,11 +241,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal of the multi-rank path on a one-GPU box (not a measurement):
+    # LPC_BENCH_REHEARSE=1 puts every rank on GPU 0 and exchanges over gloo
+    rehearse = os.environ.get("LPC_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group("gloo" if rehearse else "nccl")
         dist = tdist
 
     from lightpycl_amd.build import build
@@ -318,7 +323,7 @@ def main():
     if dist:
         import torch
         t = torch.tensor([dt, float(bounces), 0.0 if steps_identical else 1.0], dtype=torch.float64,
-                         device=f"cuda:{local}")
+                         device="cpu" if rehearse else f"cuda:{local}")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -387,7 +392,8 @@ def main():
         "ri_per_s": pairs_per_s,
         "exchange": {"per_iteration_us": prof["xchg_us"] / max(prof["xchg_calls"], 1),
                      "calls": prof["xchg_calls"], "transport": "lpc_shm_allreduce" if world > 1 else None,
-                     "trace_end": "RCCL all-reduce (histogram)" if world > 1 else None},
+                     "trace_end": (("gloo" if rehearse else "RCCL") + " all-reduce (histogram)") if world > 1 else None,
+                     "rehearsal_one_gpu": rehearse or None},
         "hist_total_power": hist_total,
         "cpu_baseline": None,
     }
