@@ -87,6 +87,7 @@ struct SpillArgs {
     uint32_t cap;
     int budget;                       // cost before hand-over (0: never), in node visits
     int pair_shift;                   // exact pairs per node visit = 1 << pair_shift (31: not counted)
+    uint32_t *tmask;                  // per ray: bit j set when a flush wrote slot j (NULL: not kept)
 };
 
 struct RaysIn {                       // a ray population (SoA)
@@ -144,6 +145,7 @@ struct SlotInit {                     // per-mesh slot initial state of a launch
     DevAcc *acc;                      // iteration counters to reset, may be NULL
     unsigned long long m_total;
     int uniform;                      // every slot (max_ray_len, idx -1): the traced path's clean state
+    uint32_t *tmask;                  // the written-slot masks to clear with the slots (or NULL)
 };
 
 struct CompactArgs {
@@ -194,6 +196,7 @@ struct StageArgs {
     int32_t mpm[LPC_MP_MAX];          // their mesh ids
     double *tmp;                      // [ntiles][LPC_MP_MAX] measured power per tile and measure mesh
     unsigned long long *gsum;         // per group of LPC_ST_GROUP tiles: counts (21 bits each), zero before
+    uint32_t *tmask;                  // the walk's written-slot masks (only those slots are read), or NULL
 };
 #define LPC_ST_GROUP 256                  // tiles per count group (k_stage_move prefixes: groups, then tiles)
 __host__ __device__ inline unsigned long long gsum_pack(uint32_t r, uint32_t t, uint32_t m)

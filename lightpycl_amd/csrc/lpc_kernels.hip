@@ -163,11 +163,14 @@ __global__ __launch_bounds__(256) void k_packet(RaysIn R, const float *__restric
 // Per-ray nearest-hit state and its flush into the run's slot (original ray
 // index q): only pieces with hits write; atomicMin on slot_key keeps the minimal
 // t and, among equal t, the lowest triangle index, so the flush order is free.
+// tmask (traced path): the ray's written-slot mask gets the slot's bit, so the
+// shading reads only the slots a flush wrote.
 static __device__ __forceinline__ void slot_flush(unsigned long long *skey, int32_t *scnt, int64_t o, int64_t q,
-                                                  float t, int32_t i, int32_t c)
+                                                  float t, int32_t i, int32_t c, uint32_t *tmask, int32_t slot)
 {
     if (c) atomicAdd(&scnt[o + q], c);
     if (i >= 0) atomicMin(&skey[o + q], slot_key(t, i));
+    if (tmask && (c || i >= 0)) atomicOr(&tmask[q], 1u << slot);
 }
 
 static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__restrict__ rs, int64_t n, int64_t q,
@@ -593,6 +596,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
         const int64_t o = (int64_t)P.slot * n, q = perm ? perm[s] : s;
         if (c) atomicAdd(&scnt[o + q], c);
         if (k != key0) atomicMin(&skey[o + q], k);
+        if (SP.tmask && (c || k != key0)) atomicOr(&SP.tmask[q], 1u << P.slot);
     }
 }
 
@@ -972,7 +976,7 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
                                                  int32_t *__restrict__ scnt,
                                                  unsigned long long *__restrict__ stats, int ppw,
                                                  float dmax, const long long *__restrict__ nd,
-                                                 const unsigned *__restrict__ dm2d)
+                                                 const unsigned *__restrict__ dm2d, uint32_t *__restrict__ tmask)
 {
     const int lane = threadIdx.x & 63;
     if (nd) {
@@ -1033,8 +1037,8 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
             if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
             n_exact += (uint32_t)r0 + (uint32_t)r1;
         }
-        if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0);
-        if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1);
+        if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0, tmask, P.slot);
+        if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1, tmask, P.slot);
     }
     if (stats) {
         for (int q = 32; q >= 1; q >>= 1) n_exact += __shfl_xor(n_exact, q, 64);
@@ -1075,6 +1079,7 @@ static __device__ __forceinline__ void slot_init_ray(const SlotInit &SI, int64_t
         *SI.acc = z;
     }
     if (r >= n || !SI.skey) return;
+    if (SI.tmask) SI.tmask[r] = 0u;
     for (int32_t j = 0; j < SI.K; ++j) {
         SI.skey[(int64_t)j * n + r] = slot_key(SI.max_ray_len, (SI.uniform || SI.live[j]) ? -1 : 0);
         SI.scnt[(int64_t)j * n + r] = 0;
@@ -1475,7 +1480,7 @@ __global__ __launch_bounds__(256) void k_filter_eval(int64_t n, const float *__r
 // memory round trip instead of one per mesh and loop).
 template <int KU = 0>
 static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_t r, PostOut &po, f3 &dest,
-                                                      uint64_t *touched = nullptr)
+                                                      uint64_t *touched = nullptr, uint32_t lmask = 0xffffffffu)
 {
     const f3 O = mk3(A.in.ox[r], A.in.oy[r], A.in.oz[r]);
     const f3 D = mk3(A.in.dx[r], A.in.dy[r], A.in.dz[r]);
@@ -1489,7 +1494,11 @@ static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_
 #pragma unroll
             for (int j = 0; j < KU; ++j) {
                 kr[j] = k0; cr[j] = 0;
-                if (j < A.K) { kr[j] = A.skey[(int64_t)j * n + r]; cr[j] = A.sc[(int64_t)j * n + r]; }
+                // lmask: the slots a flush wrote (the others hold the clean state)
+                if (j < A.K && ((lmask >> (j & 31)) & 1u)) {
+                    kr[j] = A.skey[(int64_t)j * n + r];
+                    cr[j] = A.sc[(int64_t)j * n + r];
+                }
             }
         }
         if (touched) {
@@ -1775,7 +1784,14 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     s.r_meas = -1; s.t_meas = -1;
     if (in) {
         uint64_t touched = 0;
-        s = shade_eval<KU>(S, r, po, dest, &touched);
+        // the walk's written-slot mask (K <= 32): only those slots are read, and
+        // the mask goes back to 0 with them
+        uint32_t lm = 0xffffffffu;
+        if (A.tmask) {
+            lm = A.tmask[r];
+            if (lm) A.tmask[r] = 0u;
+        }
+        s = shade_eval<KU>(S, r, po, dest, &touched, lm);
         // the slots just read back to the clean state: those a flush wrote (noted
         // while postproc read them; slots 64 and up are read again)
         const unsigned long long k0 = slot_key(S.max_ray_len, -1);

@@ -100,6 +100,7 @@ struct lpc_handle {
     DBuf w_key, w_sc, w_rs, w_shf, w_shi, w_blk_cnt, w_blk_off, w_blk_pow;
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf w_aos;                                     // rays as 32-byte rows for the coherence gather
+    DBuf w_tm;                                      // per ray: the slots a flush wrote (traced path, K <= 32)
     int64_t onesweep_min = 500000;                  // onesweep radix sort from this many rays (merge sort below)
     bool bsort = true;                              // counting sort (k_bkey..k_bsort2) for key windows <= 16 bits
     DBuf w_bhist;                                   // its per-block hi-digit counts + digit totals
@@ -133,6 +134,8 @@ struct lpc_handle {
     int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
     int64_t sort_min = 4096;                        // populations below this are traced unsorted
     int64_t resort_min = 2000000;                   // chained traced populations from this size are sorted again
+    bool tmask = true;                              // LPC_TMASK: written-slot masks (the shading reads those slots)
+    uint32_t *tm_cur = nullptr;                     // this launch's masks (the walk writes, k_shade_stage reads)
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 24;                          // node visits before a wave hands over (0 off)
@@ -654,6 +657,8 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_soa, (size_t)8 * C * 4));
         RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
         RETIF(dalloc(h, h->w_aos, (size_t)C * 32));
+        RETIF(dalloc(h, h->w_tm, (size_t)C * 4));
+        HIPCHK(h, hipMemsetAsync(h->w_tm.p, 0, h->w_tm.bytes, h->stream));
         RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
         RETIF(dalloc(h, h->w_bhist, ((size_t)LPC_BS_ND * ((C + LPC_BS_RPB - 1) / LPC_BS_RPB) + 2 * LPC_BS_ND + 8) * 4));
         size_t tb = 0;
@@ -742,7 +747,7 @@ struct DevSize {
 // Work hand-over (k_spill levels): queue, budget by population size.
 static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
 {
-    *SP = SpillArgs{nullptr, nullptr, 0u, 0, 31};
+    *SP = SpillArgs{nullptr, nullptr, 0u, 0, 31, h->tm_cur};
     if (h->spill_budget <= 0) return 0;
     RETIF(dalloc(h, h->w_spill, (size_t)2 * h->spill_cap * sizeof(SpillItem)));
     SP->items = (SpillItem *)h->w_spill.p;
@@ -968,6 +973,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     SI.acc = h->acc_pending ? (DevAcc *)h->d_acc.p : nullptr;
     SI.m_total = (unsigned long long)h->acc_pending_total;
     SI.uniform = 0;
+    SI.tmask = nullptr;
     h->acc_pending = false;
     // traced mode: the children come out in their parents' traced order and need
     // no sort of their own
@@ -992,12 +998,17 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     h->half_roots = in_trace && (h->half_now || h->half == 4 || (h->half == 3 && !emitted));
     const bool restore = traced && h->fuse_compact;
     const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
+    // written-slot masks: kept by every flush of this launch, read by its
+    // k_shade_stage (restore path only; a mask bit may be stale, never missing:
+    // the masks are cleared with the slots, and only the restore path reads them)
+    h->tm_cur = (restore && h->tmask && h->K <= 32) ? (uint32_t *)h->w_tm.p : nullptr;
     const bool misc_clean = restore && h->misc_clean;
     h->slots_clean = h->misc_clean = false;
     SlotInit SIk = SI;
     SIk.skey = nullptr; SIk.misc = nullptr; SIk.acc = nullptr;
     if (restore && !clean) {            // the whole array to the clean state (stride-independent)
         SI.uniform = 1;
+        SI.tmask = (uint32_t *)h->w_tm.p;
         const int64_t all = h->ws_rays;
         hipLaunchKernelGGL(k_slot_init, dim3(grid1(std::max<int64_t>(all, LPC_MISC_WORDS))), dim3(256), 0,
                            h->stream, all, SI);
@@ -1107,7 +1118,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                (PacketRec *)h->w_pk.p, nd_dev);
             hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
                                (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw, dmax_k, nd_dev, dm2_dev);
+                               scnt, stats, (int)ppw, dmax_k, nd_dev, dm2_dev, h->tm_cur);
             HIPCHK(h, hipGetLastError());
         }
         if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
@@ -1141,7 +1152,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             HIPCHK(h, hipMemsetAsync(h->d_wrec.p, 0, (size_t)h->wrec_count * 16, h->stream));
             wrec = (uint32_t *)h->d_wrec.p;
         }
-        SpillArgs SP{nullptr, nullptr, 0u, 0, 31};
+        SpillArgs SP{nullptr, nullptr, 0u, 0, 31, h->tm_cur};
         if (!wrec) RETIF(spill_setup(h, n, &SP));
         // pieces per wave: enough that the grid has about wave_target waves
         const int64_t bxw = (n + 255) / 256;
@@ -1285,6 +1296,7 @@ int lpc_open(int device, lpc_handle **out)
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->resort_min = std::max<int64_t>(1, env_int("LPC_RESORT_MIN", h->resort_min));
+    h->tmask = env_int("LPC_TMASK", h->tmask) != 0;
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
@@ -2045,6 +2057,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
             const int64_t ng = (nt_max + LPC_ST_GROUP - 1) / LPC_ST_GROUP;
             unsigned long long *gs = (unsigned long long *)h->w_gsum.p;
             G.gsum = gs + (size_t)h->gpar * (size_t)h->gcap;
+            G.tmask = h->tm_cur;            // set by this chunk's run_intersect
 
             if (ds) LPC_KU_LAUNCH2(h, k_shade_stage, true, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
             else LPC_KU_LAUNCH2(h, k_shade_stage, false, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
