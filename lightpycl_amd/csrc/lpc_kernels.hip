@@ -1974,11 +1974,17 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         }
         __syncthreads();
         if (t == 0) {
+            // the counters in registers (a DevAcc local indexed by m would live in
+            // scratch, on the iteration's critical path)
             DevAcc a;
-            memset(&a, 0, sizeof(a));
-            for (int m = 0; m < A.nmp; ++m) {         // the trace's running sums, in iteration order
-                A.mrun[m] = (m_base == 0 ? 0.0 : A.mrun[m]) + s_m[m][0];
-                a.mpow[m] = A.mrun[m];
+            double mp[LPC_MP_MAX];
+#pragma unroll
+            for (int m = 0; m < LPC_MP_MAX; ++m) {    // the trace's running sums, in iteration order
+                mp[m] = 0.0;
+                if (m < A.nmp) {
+                    mp[m] = (m_base == 0 ? 0.0 : A.mrun[m]) + s_m[m][0];
+                    A.mrun[m] = mp[m];
+                }
             }
             a.nR = (unsigned long long)s_tot[0]; a.nT = (unsigned long long)s_tot[1];
             a.m_total = m_base + (unsigned long long)s_tot[2];
@@ -1986,7 +1992,14 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
             a.pow_next = s_p[0];
             a.dmax2_bits = __float_as_uint(s_d[0]);
             a.qerr = A.acc->qerr;
-            *A.acc = a;
+            {
+                DevAcc *d = A.acc;
+                d->nR = a.nR; d->nT = a.nT; d->m_total = a.m_total; d->nM_iter = a.nM_iter;
+                d->pow_next = a.pow_next; d->dmax2_bits = a.dmax2_bits; d->qerr = a.qerr;
+                d->seq = 0u; d->pad = 0u;
+#pragma unroll
+                for (int m = 0; m < LPC_MP_MAX; ++m) d->mpow[m] = mp[m];
+            }
             if (A.ctl) {
                 // the next iteration's size for device-sized launches: 0 once the
                 // trace ends (trace_run's rules, iterative_tracer.py:383-391) or a
@@ -2011,9 +2024,11 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&o->dmax2_bits, a.dmax2_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&o->qerr, a.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                for (int m = 0; m < A.nmp; ++m)
-                    __hip_atomic_store((unsigned long long *)&o->mpow[m], __double_as_longlong(a.mpow[m]),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+                for (int m = 0; m < LPC_MP_MAX; ++m)
+                    if (m < A.nmp)
+                        __hip_atomic_store((unsigned long long *)&o->mpow[m], __double_as_longlong(mp[m]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(&o->seq, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
