@@ -566,3 +566,39 @@ def test_resort_equals_chained(monkeypatch, name, n):
         r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
         return r[np.lexsort(r.T[::-1])]
     np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n", [("synthetic", 50000), ("lens", 20000), ("nested_cubes", 2000)])
+def test_written_slot_masks_equal_full_reads(monkeypatch, name, n):
+    """Written-slot masks (LPC_TMASK, default on: the shading reads only the
+    slots a flush wrote) against the shading reading every slot: the same trace
+    bit for bit -- per-iteration counts, per-mesh power, measured rays in order.
+    Three back-to-back traces, so the masks' clearing between iterations and
+    traces is exercised too."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.BUILDERS[name](n=n, seed=37)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+    out = []
+    for tm in ("1", "0"):
+        monkeypatch.setenv("LPC_TMASK", tm)
+        e = Engine(0)
+        try:
+            e.upload_meshes(sc.meshes)
+            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+            runs = []
+            for rep in range(3):
+                e.reset()
+                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+                runs.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt,
+                             [float(x) for x in mp]))
+            pos, p, mm = e.fetch_measured()
+            out.append((runs, pos, p, mm))
+        finally:
+            e.close()
+    a, b = out
+    assert a[0] == b[0]
+    assert a[0][0] == a[0][1] == a[0][2]
+    for x, y in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
