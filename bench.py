@@ -9,7 +9,10 @@ device-to-device).  value = ray-bounces of all ranks / max-over-ranks time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rays R] [--no-cpu] [--no-configs]
 
-Multi-GPU: launched by torch.distributed.run; rays shard by rank (independent
+Multi-GPU: run under torch.distributed.run (the driver's form), or directly with
+--gpus N > 1, when the parent starts torch.distributed.run with N ranks as a child
+process (before touching the GPU) and exits with its status; the rank count must
+equal --gpus.  Rays shard by rank (independent
 seeds, weak scaling), the scene is replicated.  Each iteration's termination
 decision (iterative_tracer.py:383-391) is taken inside the library's trace loop
 on the stats all-reduced over the ranks of the node through the library's
@@ -189,8 +192,11 @@ def cpu_leg(sc, eng, o, d, p, nrays, first_stats, timed):
                           and abs(st.power_next - pw) <= 1e-6 * max(abs(pw), 1e-300))}
     base = None
     if timed:
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        model, affinity = cpu_info()
+        # the oracle's OpenMP team: OMP_NUM_THREADS when set, else the affinity mask
+        cores = min(int(os.environ.get("OMP_NUM_THREADS", affinity)), affinity)
         base = dict(value=n / dt, unit="ray-bounces/s", cores=cores, kind="port",
+                    cpu_model=model, cores_in_affinity_mask=affinity,
                     sample=f"first {n} rays of the workload, 1 bounce (intersect+postproc+Fresnel) over "
                            f"{S.tri_count} triangles, {dt:.2f} s",
                     ri_per_s=n * S.tri_count / dt)
@@ -235,11 +241,64 @@ def run_configs(Engine, ShardedTrace, scenes):
     return out
 
 
+def cpu_info():
+    """CPU model (/proc/cpuinfo) and the cores this process may run on (its
+    affinity mask, not the machine's count: BASELINE.md asks for both)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    return model, affinity
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N ranks with
+    torch.distributed.run as a child process and exit with its status.  Nothing
+    here touches the GPU (device_count does not initialise it on this image), and
+    the parent is never replaced (no exec)."""
+    import subprocess
+    rehearse = os.environ.get("LPC_BENCH_REHEARSE") == "1"
+    if not rehearse:
+        import torch
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(f"bench: --gpus {a.gpus} but only {have} HIP devices are visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     dist = None
     # rehearsal of the multi-rank path on a one-GPU box (not a measurement):
     # LPC_BENCH_REHEARSE=1 puts every rank on GPU 0 and exchanges over gloo
@@ -269,7 +328,9 @@ def main():
     eng.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
     in_pow = float(np.sum(p, dtype=np.float64))
     comm = TorchComm(dist, local) if dist else None
-    shm = ShmComm.from_dist(dist) if dist else None
+    # per-iteration exchange: the library's shared-memory hook on one node,
+    # torch.distributed through the hook when the ranks span nodes
+    shm = ShmComm.from_dist(dist, fallback=comm) if dist else None
     runner = ShardedTrace(eng, comm, iter_comm=shm)
     in_pow_all = float(comm.allreduce_sum([in_pow])[0]) if comm else in_pow
 
@@ -320,21 +381,31 @@ def main():
     hr = runner.run(sc.iterations, sc.tau, in_pow, hist=(sc.hist_limits, sc.hist_points),
                     input_power_global=in_pow_all)
     hist_total = float(np.sum(hr["hist"][0]) * ((sc.hist_limits[0][1] - sc.hist_limits[0][0]) / sc.hist_points) ** 2)
+    rank_ms = [dt / a.steps * 1e3]
     if dist:
         import torch
-        t = torch.tensor([dt, float(bounces), 0.0 if steps_identical else 1.0], dtype=torch.float64,
-                         device="cpu" if rehearse else f"cuda:{local}")
+        dev = "cpu" if rehearse else f"cuda:{local}"
+        t = torch.tensor([dt, float(bounces), 0.0 if steps_identical else 1.0], dtype=torch.float64, device=dev)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        # every rank's time per step, so load imbalance between shards shows
+        per = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(per, torch.tensor([dt / a.steps * 1e3], dtype=torch.float64, device=dev))
+        rank_ms = [float(x.item()) for x in per]
         dt, bounces_all = float(mx[0]), float(t[1])
         steps_identical = float(mx[2]) == 0.0
     else:
         bounces_all = float(bounces)
-    if rank != 0:
-        shm.close()
+    def finish():
+        runner.close()                          # the hook out of the engine before its comm closes
+        if isinstance(shm, ShmComm):
+            shm.close()
         if dist:
             dist.destroy_process_group()
+
+    if rank != 0:
+        finish()
         return
 
     M = eng.tri_count
@@ -358,6 +429,7 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": dt / a.steps * 1e3,
+        "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -391,7 +463,8 @@ def main():
                                   "filter skips almost all tests: not a utilisation figure"},
         "ri_per_s": pairs_per_s,
         "exchange": {"per_iteration_us": prof["xchg_us"] / max(prof["xchg_calls"], 1),
-                     "calls": prof["xchg_calls"], "transport": "lpc_shm_allreduce" if world > 1 else None,
+                     "calls": prof["xchg_calls"], "transport": (("lpc_shm_allreduce" if isinstance(shm, ShmComm) else "torch.distributed via hook")
+                                   if world > 1 else None),
                      "trace_end": (("gloo" if rehearse else "RCCL") + " all-reduce (histogram)") if world > 1 else None,
                      "rehearsal_one_gpu": rehearse or None},
         "hist_total_power": hist_total,
@@ -407,12 +480,12 @@ def main():
         out["cpu_baseline"] = base
     out["parity"] = par
     if world == 1 and not a.no_configs:
+        runner.close()
         eng.close()
         out["configs"] = run_configs(Engine, ShardedTrace, scenes)
     print(json.dumps(out))
-    if dist:
-        shm.close()
-        dist.destroy_process_group()
+    if world > 1:
+        finish()
 
 
 if __name__ == "__main__":

@@ -165,9 +165,15 @@ typedef int (*lpc_allreduce_fn)(void *ctx, double *vals, int32_t n);
 /* Install (fn != NULL) or remove the all-reduce hook of h.  With a hook, the
  * loop of lpc_trace_run(_async) all-reduces each iteration's stats and takes
  * the reference's termination decisions (iterative_tracer.py:383-391) on the
- * sums over all ranks, so every rank stops at the iteration a single device
- * tracing all rays would; *measured_count and mesh_power are then the sums over
- * all ranks too.  per_iter keeps this rank's own stats. */
+ * sums over all ranks, so every rank takes the same decision; *measured_count
+ * and mesh_power are then the sums over all ranks too.  per_iter keeps this
+ * rank's own stats.  The power left is a rank-order float64 sum of per-rank
+ * float64 sums: its rounding differs from a single device's tile-order sum
+ * (and both from the reference's float32 sorted sum, :372), so a trace whose
+ * power left lands within ~1e-12 relative of the threshold may stop one
+ * iteration apart from a single-device trace.  A rank whose trace fails
+ * locally still joins the exchange its peers wait in, with NaN values; a rank
+ * that receives NaN sums fails with LPC_E_STATE ("a peer rank failed"). */
 int lpc_set_allreduce(lpc_handle *h, lpc_allreduce_fn fn, void *ctx);
 /* The all-reduced per-iteration stats of the last lpc_trace_run(_async) (this
  * rank's own without a hook).  *n_iter = iterations; at most cap are copied. */
@@ -176,11 +182,16 @@ int lpc_trace_global_stats(lpc_handle *h, lpc_iter_stats *per_iter, int32_t cap,
  * segment `name`, created by the rank passing create != 0 (the others wait for
  * it); rank-order sums, so identical bits on every rank.  lpc_shm_allreduce is
  * an lpc_allreduce_fn (ctx = the comm).  lpc_shm_comm_unlink removes the name
- * once every rank has opened it (the mapping stays); close unmaps. */
+ * once every rank has opened it (the mapping stays); close unmaps.  A timed-out
+ * exchange (300 s) or lpc_shm_comm_abort breaks the comm for good: every later
+ * lpc_shm_allreduce on it fails, and so do the peers' current waits (they see
+ * the rank's abort word), since the ranks no longer agree on which exchange is
+ * which. */
 typedef struct lpc_shm_comm lpc_shm_comm;
 int lpc_shm_comm_open(const char *name, int32_t rank, int32_t world, int32_t create, lpc_shm_comm **out);
 int lpc_shm_comm_unlink(lpc_shm_comm *comm);
 int lpc_shm_allreduce(void *comm, double *vals, int32_t n);
+int lpc_shm_comm_abort(lpc_shm_comm *comm);
 int lpc_shm_comm_close(lpc_shm_comm *comm);
 
 /* Wait until the handle's stream has finished every queued kernel. */

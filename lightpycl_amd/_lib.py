@@ -81,6 +81,7 @@ _PROTOS = {
     "lpc_shm_comm_open": [ctypes.c_char_p, _I32, _I32, _I32, _P],
     "lpc_shm_comm_unlink": [_P],
     "lpc_shm_allreduce": [_P, _P, _I32],
+    "lpc_shm_comm_abort": [_P],
     "lpc_shm_comm_close": [_P],
 }
 

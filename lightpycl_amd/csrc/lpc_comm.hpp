@@ -44,7 +44,8 @@ struct alignas(64) ShmHdr {
 
 struct alignas(64) ShmSlot {
     volatile uint64_t seq;                // last exchange this rank published
-    uint64_t pad[7];
+    volatile uint64_t abort;              // != 0: this rank gave up; its peers fail fast
+    uint64_t pad[6];
     double v[2][kCap];                    // double-buffered by exchange parity
 };
 
@@ -55,6 +56,8 @@ struct ShmComm {
     size_t bytes = 0;
     void *base = nullptr;
     uint64_t seq = 0;
+    bool failed = false;                  // an exchange failed: the ranks' sequence numbers are
+                                          // out of step, every later exchange is an error
     std::string err;
     ShmHdr *hdr() const { return (ShmHdr *)base; }
     ShmSlot *slot(int r) const { return (ShmSlot *)((char *)base + sizeof(ShmHdr)) + r; }
@@ -126,13 +129,29 @@ inline int shm_open_comm(const char *name, int32_t rank, int32_t world, int crea
     return 0;
 }
 
+// Give up on the comm: every later exchange on it fails, and so do the peers'
+// waits (they see this rank's abort word instead of spinning to the timeout).
+inline void shm_abort(ShmComm *c, const std::string &why)
+{
+    if (!c) return;
+    if (!c->failed) c->err = why;
+    c->failed = true;
+    if (c->base) __atomic_store_n(&c->slot(c->rank)->abort, (uint64_t)1, __ATOMIC_RELEASE);
+}
+
 // In-place sum over all ranks, identical bits on every rank (rank-order sums).
 // Exchange s writes buffer s & 1 of this rank's slot: a rank starts exchange s
 // only after every rank published s - 1, i.e. finished reading exchange s - 2,
-// the last user of that buffer.
+// the last user of that buffer.  A timeout or a peer's abort word breaks the
+// comm for good (shm_abort): after a failed exchange the ranks no longer agree
+// on which call pairs with which, so no later sum could be trusted.
 inline int shm_allreduce(ShmComm *c, double *vals, int32_t n)
 {
     if (!c || (n > 0 && !vals) || n < 0) return -1;
+    if (c->failed) {
+        if (c->err.empty()) c->err = "shm comm: broken by an earlier failed exchange";
+        return -1;
+    }
     if (c->world == 1) return 0;
     for (int32_t off = 0; off < n || (n == 0 && off == 0); off += kCap) {
         const int32_t m = n - off < kCap ? n - off : kCap;
@@ -145,8 +164,14 @@ inline int shm_allreduce(ShmComm *c, double *vals, int32_t n)
         for (int r = 0; r < c->world; ++r) {
             uint64_t spins = 0;
             while (__atomic_load_n(&c->slot(r)->seq, __ATOMIC_ACQUIRE) < s) {
+                if (__atomic_load_n(&c->slot(r)->abort, __ATOMIC_ACQUIRE) != 0) {
+                    shm_abort(c, "shm comm: rank " + std::to_string(r) + " aborted before exchange " +
+                                     std::to_string(s));
+                    return -1;
+                }
                 if ((++spins & 1023u) == 0u && now_s() - t0 > kTimeoutS) {
-                    c->err = "shm comm: rank " + std::to_string(r) + " did not reach exchange " + std::to_string(s);
+                    shm_abort(c, "shm comm: rank " + std::to_string(r) + " did not reach exchange " +
+                                     std::to_string(s));
                     return -1;
                 }
                 __builtin_ia32_pause();

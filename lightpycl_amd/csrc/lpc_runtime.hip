@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <map>
 #include <string>
 #include <vector>
@@ -1815,6 +1816,8 @@ static int xchg_stats(lpc_handle *h, const lpc_iter_stats &S, lpc_iter_stats *G)
     h->xchg_us += host_us() - t0;
     h->xchg_calls += 1;
     if (rc != 0) return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
+    for (double x : v)
+        if (x != x) return set_err(h, LPC_E_STATE, "trace: a peer rank failed (NaN in the all-reduced stats)");
     G->n_in = (int64_t)v[0]; G->n_reflect = (int64_t)v[1]; G->n_refract = (int64_t)v[2];
     G->n_measured = (int64_t)v[3]; G->power_next = v[4];
     return 0;
@@ -1822,6 +1825,19 @@ static int xchg_stats(lpc_handle *h, const lpc_iter_stats &S, lpc_iter_stats *G)
 
 static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                      int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait);
+
+// A rank that fails locally still takes part in the exchange its peers wait in,
+// with NaN values: they see NaN in the sums and fail at once (xchg_stats)
+// instead of waiting for a rank that left, and every rank has made the same
+// number of exchanges.  The local error stays the one reported.
+static void xchg_poison(lpc_handle *h, int32_t n)
+{
+    if (!h->xchg) return;
+    std::vector<double> v((size_t)n, std::numeric_limits<double>::quiet_NaN());
+    const std::string keep = h->err;
+    (void)h->xchg(h->xchg_ctx, v.data(), n);
+    h->err = keep;
+}
 
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                   int32_t *n_iter, int64_t *measured_count, double *mesh_power)
@@ -1875,6 +1891,13 @@ int lpc_shm_allreduce(void *comm, double *vals, int32_t n)
     if (!c) return set_err(nullptr, LPC_E_ARG, "shm comm: null");
     if (lpcc::shm_allreduce(c, vals, n) != 0)
         return set_err(nullptr, LPC_E_STATE, c->err.empty() ? "shm comm: bad argument" : c->err);
+    return 0;
+}
+
+int lpc_shm_comm_abort(lpc_shm_comm *c)
+{
+    if (!c) return set_err(nullptr, LPC_E_ARG, "shm comm: null");
+    lpcc::shm_abort((lpcc::ShmComm *)c, "shm comm: aborted by this rank");
     return 0;
 }
 
@@ -2244,6 +2267,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     std::vector<int64_t> seen;
     h->ds_thr = power_threshold;
     int rc = 0;
+    bool exchanged = false;             // rc came from the exchange itself (no poison owed)
     Pending cur, nxt;
     bool have_cur = false, have_nxt = false;
     for (int32_t i = 0; i < max_iter; ++i) {
@@ -2278,7 +2302,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         // identical bits everywhere), so all stop at the iteration a single
         // device would (iterative_tracer.py:383-391)
         lpc_iter_stats G = S;
-        if (h->xchg && (rc = xchg_stats(h, S, &G))) break;
+        if (h->xchg && (rc = xchg_stats(h, S, &G))) { exchanged = true; break; }
         h->gstats.push_back(G);
         const bool stop = G.power_next < power_threshold || G.n_reflect + G.n_refract == 0;   // :383, :389
         if (have_nxt) {
@@ -2302,6 +2326,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         (void)hipStreamSynchronize(h->stream);
         iter_discard(h, cur);
     }
+    if (rc && !exchanged) xchg_poison(h, 5);               // the peers wait in this iteration's exchange
     RETIF(rc);
     // this trace's populations (relative to the first) predict the next trace's
     if (n0 > 0) {
@@ -2312,11 +2337,16 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     if (measured_count || mesh_power) {                     // the trace's aggregates, same call
         int64_t c = 0;
         std::vector<double> mp((size_t)h->K + 1, 0.0);
-        RETIF(lpc_trace_measured(h, &c, mp.data()));
+        if ((rc = lpc_trace_measured(h, &c, mp.data()))) {
+            xchg_poison(h, h->K + 1);
+            return rc;
+        }
         if (h->xchg) {                                      // trace-end sums over the ranks
             mp[(size_t)h->K] = (double)c;
             if (h->xchg(h->xchg_ctx, mp.data(), h->K + 1) != 0)
                 return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
+            for (double x : mp)
+                if (x != x) return set_err(h, LPC_E_STATE, "trace: a peer rank failed (NaN in the trace-end sums)");
             c = (int64_t)mp[(size_t)h->K];
         }
         if (measured_count) *measured_count = c;

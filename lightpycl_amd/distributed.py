@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+import socket
+import weakref
 
 import numpy as np
 
@@ -80,12 +82,25 @@ class ShmComm:
         _lib.check(self.L.lpc_shm_comm_open(name.encode(), self.rank, self.world, 1 if create else 0,
                                             ctypes.byref(c)))
         self.c = c
+        self._engines = weakref.WeakSet()     # engines whose loop calls this comm (native_hook)
+
+    @staticmethod
+    def single_node(dist):
+        """True when every rank of the job runs on this host (POSIX shared memory
+        reaches only the ranks of one node): the hostnames all-gathered."""
+        names = [None] * dist.get_world_size()
+        dist.all_gather_object(names, socket.gethostname())
+        return len(set(names)) == 1
 
     @classmethod
-    def from_dist(cls, dist):
+    def from_dist(cls, dist, fallback=None):
         """One segment per torch.distributed job: rank 0 names and creates it, the
-        others open it, then the name is unlinked (nothing is left in /dev/shm)."""
+        others open it, then the name is unlinked (nothing is left in /dev/shm).
+        On a multi-node job the segment cannot reach every rank: returns
+        ``fallback`` (e.g. a :class:`TorchComm`, called through the hook) instead."""
         import secrets
+        if not cls.single_node(dist):
+            return fallback
         rank, world = dist.get_rank(), dist.get_world_size()
         box = [f"lpc_{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
@@ -94,9 +109,19 @@ class ShmComm:
         comm.unlink()
         return comm
 
-    def native_hook(self):
+    def native_hook(self, engine=None):
+        if not self.c:
+            raise RuntimeError("ShmComm is closed")
+        if engine is not None:
+            self._engines.add(engine)
         fn = ctypes.cast(self.L.lpc_shm_allreduce, ctypes.c_void_p)
         return fn, self.c
+
+    def abort(self):
+        """Break the comm (lpc_shm_comm_abort): later exchanges fail here, and the
+        peers' current waits fail instead of running to the 300 s timeout."""
+        if self.c:
+            self.L.lpc_shm_comm_abort(self.c)
 
     def allreduce_sum(self, values):
         v = np.ascontiguousarray(np.asarray(values, dtype=np.float64).reshape(-1)).copy()
@@ -108,7 +133,12 @@ class ShmComm:
             self.L.lpc_shm_comm_unlink(self.c)
 
     def close(self):
+        """Unmap the segment.  The hook is removed first from every engine that
+        still has it installed, so no later trace calls into freed memory."""
         if getattr(self, "c", None):
+            for e in list(getattr(self, "_engines", ())):
+                if getattr(e, "_xchg", None) is not None and e._xchg[0] is self and getattr(e, "h", None):
+                    e.set_allreduce(None)
             self.L.lpc_shm_comm_close(self.c)
             self.c = None
 
@@ -142,6 +172,12 @@ class ShardedTrace:
         self.engine = engine
         self.comm = comm
         self.iter_comm = iter_comm if iter_comm is not None else comm
+        self._installed = None
+
+    def close(self):
+        """Remove the per-iteration hook from the engine (before its comm closes)."""
+        if self._installed is not None and hasattr(self.engine, "set_allreduce") and getattr(self.engine, "h", None):
+            self.engine.set_allreduce(None)
         self._installed = None
 
     def _sum(self, vals):

@@ -198,7 +198,7 @@ class Engine:
             return
         native = getattr(comm, "native_hook", None)
         if native is not None:
-            fn, ctx = native()
+            fn, ctx = native(self)
             self._xchg = (comm, fn)
             self._c(self.L.lpc_set_allreduce(self.h, fn, ctx))
             return

@@ -166,3 +166,76 @@ def test_sharded_trace_shm_comm(oracle_mod, tmp_path):
                                keep_results=False)
     assert got["counts"] == info["counts"]
     np.testing.assert_allclose(got["mesh_power"], info["mesh_power"], rtol=1e-12, atol=1e-12)
+
+
+def _abort_worker(rank, world, name, out_dir):
+    """Rank 1 exchanges once, then gives up (lpc_shm_comm_abort); rank 0's next
+    exchange must fail at once (not after the 300 s timeout), and every later
+    exchange on the broken comm too."""
+    import time
+    sys.path.insert(0, os.path.dirname(HERE))
+    from lightpycl_amd import _lib
+    from lightpycl_amd.distributed import ShmComm
+    c = ShmComm(name, rank, world, create=(rank == 0))
+    assert list(c.allreduce_sum([1.0])) == [float(world)]
+    res = {}
+    if rank == 1:
+        c.abort()
+        with pytest.raises(_lib.LpcError):
+            c.allreduce_sum([1.0])
+    else:
+        t = time.perf_counter()
+        try:
+            c.allreduce_sum([2.0])
+            res["first"] = "ok"
+        except _lib.LpcError as e:
+            res["first"] = str(e)
+        res["wait_s"] = time.perf_counter() - t
+        try:
+            c.allreduce_sum([3.0])
+            res["second"] = "ok"
+        except _lib.LpcError as e:
+            res["second"] = str(e)
+        with open(os.path.join(out_dir, "abort.json"), "w") as f:
+            json.dump(res, f)
+    c.close()
+
+
+def test_shm_comm_abort_fails_peers_fast(tmp_path):
+    import secrets
+    name = f"lpc_abort_{os.getpid()}_{secrets.token_hex(4)}"
+    mp.spawn(_abort_worker, args=(2, name, str(tmp_path)), nprocs=2, join=True)
+    got = json.load(open(tmp_path / "abort.json"))
+    assert "aborted" in got["first"], got
+    assert got["wait_s"] < 30.0, got
+    assert got["second"] != "ok", got          # the comm stays broken
+
+
+def test_shm_close_removes_installed_hook():
+    """Closing a ShmComm takes its hook out of every engine it was installed in
+    (an engine must not keep a pointer into the unmapped segment)."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    from lightpycl_amd.distributed import ShmComm
+
+    class FakeEngine:
+        h = 1
+
+        def __init__(self):
+            self._xchg = None
+            self.calls = []
+
+        def set_allreduce(self, comm):
+            if comm is None:
+                self._xchg = None
+            else:
+                fn, _ = comm.native_hook(self)
+                self._xchg = (comm, fn)
+            self.calls.append(comm)
+
+    c = ShmComm(f"lpc_hook_{os.getpid()}", 0, 1, create=True)
+    e = FakeEngine()
+    e.set_allreduce(c)
+    c.close()
+    assert e._xchg is None and e.calls[-1] is None
+    with pytest.raises(RuntimeError):
+        c.native_hook()
