@@ -45,6 +45,10 @@ typedef struct lpc_handle lpc_handle;
 int lpc_abi_version(void);
 /* Number of visible HIP devices (0 if none). */
 int lpc_device_count(int *count);
+/* Name, architecture (gcnArchName) and CU count of HIP device `device`
+ * without opening a handle: the drop-in's device selection by name
+ * (CL_Tracer(device_name=...), iterative_tracer.py:50-55). */
+int lpc_device_query(int device, char *name, int name_len, char *arch, int arch_len, int *cu_count);
 /* Open a handle on HIP device `device` (replaces CL_Tracer.__init__'s
  * platform/device/context/queue setup, iterative_tracer.py:36-74). */
 int lpc_open(int device, lpc_handle **out);

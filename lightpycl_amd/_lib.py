@@ -48,6 +48,7 @@ _INT = ctypes.c_int
 
 # name -> argtypes (all functions return int status except lpc_last_error)
 _PROTOS = {
+    "lpc_device_query": [_INT, _P, _INT, _P, _INT, _P],
     "lpc_abi_version": [],
     "lpc_device_count": [_P],
     "lpc_open": [_INT, _P],

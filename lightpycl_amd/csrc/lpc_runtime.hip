@@ -1247,6 +1247,19 @@ int lpc_device_count(int *count)
     return 0;
 }
 
+int lpc_device_query(int device, char *name, int name_len, char *arch, int arch_len, int *cu_count)
+{
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c)
+        return set_err(nullptr, LPC_E_ARG, "no HIP device " + std::to_string(device));
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return set_err(nullptr, LPC_E_HIP, "hipGetDeviceProperties");
+    if (name && name_len > 0) { strncpy(name, p.name, (size_t)name_len - 1); name[name_len - 1] = 0; }
+    if (arch && arch_len > 0) { strncpy(arch, p.gcnArchName, (size_t)arch_len - 1); arch[arch_len - 1] = 0; }
+    if (cu_count) *cu_count = p.multiProcessorCount;
+    return 0;
+}
+
 int lpc_open(int device, lpc_handle **out)
 {
     if (!out) return set_err(nullptr, LPC_E_ARG, "out is NULL");

@@ -51,6 +51,45 @@ def default_device() -> int:
     return 0
 
 
+def device_names():
+    """[(name, gcnArchName, CUs)] of the visible HIP devices (lpc_device_query)."""
+    L = _lib.load()
+    c = ctypes.c_int(0)
+    check(L.lpc_device_count(ctypes.byref(c)), None)
+    out = []
+    for k in range(c.value):
+        name, arch, cu = ctypes.create_string_buffer(256), ctypes.create_string_buffer(64), ctypes.c_int(0)
+        check(L.lpc_device_query(k, name, 256, arch, 64, ctypes.byref(cu)), None)
+        out.append((name.value.decode(errors="replace"), arch.value.decode(errors="replace"), cu.value))
+    return out
+
+
+def select_device(device_name=None, names=None) -> int:
+    """The HIP device for ``CL_Tracer(device_name=...)``, as the reference picks
+    its OpenCL device (iterative_tracer.py:50-55): an int is an ordinal; a string
+    is a substring of the device's name or architecture, and the LAST matching
+    device wins, as in the reference's loop (a string of digits that matches no
+    name is an ordinal if that device exists); no match -> the default device (``$LPC_DEVICE``, ``$LOCAL_RANK`` or 0), as
+    the reference falls back to its first device.  When several devices match
+    and the default one is among them, the default is kept (one process per GPU:
+    every rank asks for "MI355" and keeps its own)."""
+    dflt = default_device()
+    if device_name is None:
+        return dflt
+    if isinstance(device_name, (int, np.integer)):
+        return int(device_name)
+    names = device_names() if names is None else names
+    key = str(device_name)
+    hits = [k for k, (nm, arch, _) in enumerate(names) if key in nm or key in arch]
+    if hits:
+        return dflt if dflt in hits else hits[-1]
+    # a string of digits that names no device: an ordinal when there is such a
+    # device (the reference's default "770" is neither: default device)
+    if key.strip().isdigit() and int(key) < len(names):
+        return int(key)
+    return dflt
+
+
 class Engine:
     """A liblpc handle on one GPU (HIP device ordinal ``device``)."""
 

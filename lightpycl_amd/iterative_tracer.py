@@ -2,9 +2,10 @@
 per-bounce hot path on an MI355X through liblpc (HIP, gfx950).
 
 Mirrors ``/root/reference/iterative_tracer.py``:
-  * ``CL_Tracer(platform_name, device_name, debug)`` (:36-74): the platform /
-    device strings are accepted for compatibility; the GPU is the HIP device
-    ``device=`` (default: ``$LPC_DEVICE``, ``$LOCAL_RANK`` or 0);
+  * ``CL_Tracer(platform_name, device_name, debug)`` (:36-74): ``device_name``
+    picks the HIP device as the reference picks its OpenCL device (an ordinal, or
+    a substring of the device name / gfx architecture, last match wins, no match
+    -> ``$LPC_DEVICE``, ``$LOCAL_RANK`` or 0); ``device=`` (an ordinal) overrides;
   * ``iterative_tracer(light_source, meshes, trace_iterations, trace_until_dissipated,
     max_ray_len, ior_env)`` (:77-393) -> ``self.results``, a list of per-iteration
     tuples ``(rays_origin (N,4) f32, rays_dest (N,4) f32, rays_pow, rays_meas (N,) i32)``
@@ -29,7 +30,7 @@ import time
 
 import numpy as np
 
-from .engine import Engine, flatten_meshes
+from .engine import Engine, flatten_meshes, select_device
 
 
 def f32_sorted_sum(a):
@@ -63,7 +64,10 @@ class CL_Tracer:
         self.debug = debug
         self.verbose = verbose
         self.platform_name, self.device_name = platform_name, device_name
-        self.engine = Engine(device)
+        # device= (HIP ordinal) wins; else device_name selects as the reference's
+        # substring loop does (:50-55); the platform is always HIP (the reference
+        # falls back to its first platform when platform_name matches none)
+        self.engine = Engine(device if device is not None else select_device(device_name))
         name, cus = self.engine.info()
         self.device_label = f"{name} ({cus} CUs)"
         if self.verbose:

@@ -183,3 +183,24 @@ def test_pickle_results_protocol1_and_reference_module_names(tmp_path):
     assert type(tr3.meshes[0]).__name__ == "GeoObject"
     with pytest.raises(Exception):
         pickle.loads(ref_raw)                   # a plain loader cannot resolve the reference's module
+
+
+def test_select_device_by_name(monkeypatch):
+    """CL_Tracer(device_name=...) picks the HIP device as the reference's loop
+    picks its OpenCL device (iterative_tracer.py:50-55): ordinal, substring of the
+    name or gfx architecture (last match wins), no match -> the default device."""
+    from lightpycl_amd.engine import select_device
+    names = [("AMD Instinct MI355X", "gfx950:sramecc+:xnack-", 256)] * 4 + [("Other GPU", "gfx1100", 48)]
+    monkeypatch.delenv("LPC_DEVICE", raising=False)
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    assert select_device(3, names) == 3
+    assert select_device("2", names) == 2
+    assert select_device("770", names) == 0            # the reference's default string: no match
+    assert select_device("gfx1100", names) == 4
+    assert select_device("Other", names) == 4
+    assert select_device("MI355", names) == 0         # the default device is among the matches
+    monkeypatch.setenv("LOCAL_RANK", "2")
+    assert select_device("MI355", names) == 2         # one process per GPU keeps its own
+    assert select_device("Other", names) == 4
+    monkeypatch.setenv("LOCAL_RANK", "4")
+    assert select_device("gfx950", names) == 3        # default not among the matches: last match
