@@ -23,6 +23,7 @@
 #ifndef LPC_H
 #define LPC_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -120,6 +121,10 @@ typedef struct {
     int64_t n_refract;       /* kept refracted children                           */
     int64_t n_measured;      /* rays that hit a measure surface this iteration    */
     double power_next;       /* sum of next-population power (float64)            */
+    int64_t power_nonneg;    /* 1: every kept child's power is >= 0, 0: some is < 0
+                                or NaN, -1: not tracked (traced iterations); the
+                                host's bound on the reference's float32 sorted sum
+                                (:372) needs 1                                      */
 } lpc_iter_stats;
 
 /* Load the initial population from host (n,4) rows and power[n]; prev_mid = -2,
@@ -145,6 +150,21 @@ int lpc_trace_reset(lpc_handle *h);
  * and every copy to the host wait for it. */
 int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
                       int32_t *out_meas, float *out_next_pow, lpc_iter_stats *st);
+/* lpc_trace_iterate with the results tuple (:335-355) exported asynchronously:
+ * `host` is a block of the caller's (pinned: lpc_host_alloc, so the copy is a
+ * DMA that overlaps the next kernels) laid out over the iteration's N = st->n_in
+ * rays as [origin (N,4) if flags & 1][dest (N,4)][pow (N)][meas (N)] -- the
+ * results tuple's arrays, reference ray order, w = 0.  The call returns once
+ * the iteration's counters are read; the block is complete after lpc_sync (or
+ * any call that copies device data to the host).  The host must not reuse or
+ * free the block before then. */
+int lpc_trace_iterate_export(lpc_handle *h, void *host, int32_t flags, lpc_iter_stats *st);
+/* The current population's power (float32[n], n = lpc_trace_population): the
+ * values the reference sums at :372 after compaction. */
+int lpc_trace_population_power(lpc_handle *h, float *out);
+/* Page-locked host memory for lpc_trace_iterate_export (hipHostMalloc). */
+int lpc_host_alloc(size_t bytes, void **out);
+int lpc_host_free(void *p);
 /* The reference's iteration loop on one device (iterative_tracer.py:241-391):
  * lpc_trace_iterate until the next population's power is below
  * power_threshold (= (1 - trace_until_dissipated) * input power, :383) or no

@@ -24,7 +24,7 @@ class LpcError(RuntimeError):
 class IterStats(ctypes.Structure):
     _fields_ = [("n_in", ctypes.c_int64), ("n_reflect", ctypes.c_int64),
                 ("n_refract", ctypes.c_int64), ("n_measured", ctypes.c_int64),
-                ("power_next", ctypes.c_double)]
+                ("power_next", ctypes.c_double), ("power_nonneg", ctypes.c_int64)]
 
 
 class Prof(ctypes.Structure):
@@ -67,6 +67,10 @@ _PROTOS = {
     "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P],
     "lpc_trace_run_async": [_P, _I32, _F64, _P, _P, _P, _P],
     "lpc_sync": [_P],
+    "lpc_trace_iterate_export": [_P, _P, _I32, _P],
+    "lpc_trace_population_power": [_P, _P],
+    "lpc_host_alloc": [ctypes.c_size_t, _P],
+    "lpc_host_free": [_P],
     "lpc_trace_population": [_P, _P],
     "lpc_trace_measured": [_P, _P, _P],
     "lpc_trace_fetch_measured": [_P, _P, _P, _P],

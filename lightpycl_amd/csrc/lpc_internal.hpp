@@ -131,7 +131,7 @@ struct DevAcc {                       // device-side counters of one iteration
     unsigned int dmax2_bits;          // max |dir|^2 of kept children (float bits)
     unsigned int qerr;                // a consistency check failed on the device (QueueArgs::err)
     unsigned int seq;                 // host copy only: iteration number, written last (k_scan)
-    unsigned int pad;
+    unsigned int pneg;                // != 0: some kept child's power is negative or NaN (k_count)
     double mpow[LPC_MP_MAX];          // traced path: measured power of the trace so far per measure mesh
 };
 

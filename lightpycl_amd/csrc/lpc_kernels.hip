@@ -1584,11 +1584,13 @@ __global__ __launch_bounds__(256) void k_count(CompactArgs A)
     int32_t cR = 0, cT = 0, cM = 0;
     double pk = 0.0;
     float dm = 0.0f;
+    bool neg = false;                    // a kept child's power < 0 or NaN (the host's sum bound needs >= 0)
     for (int sub = 0; sub < 4; ++sub) {
         const int64_t r = tile + sub * 256 + threadIdx.x;
         if (r < A.n) {
             const bool fR = A.o.rms[r] == 0, fT = A.o.tms[r] == 0, fM = A.o.meas[r] == 1;
             cR += fR; cT += fT; cM += fM;
+            neg = neg || (fR && !(A.o.rpw[r] >= 0.0f)) || (fT && !(A.o.tpw[r] >= 0.0f));
             if (fR) {
                 pk += (double)A.o.rpw[r];
                 dm = fmaxf(dm, A.o.rdx[r] * A.o.rdx[r] + A.o.rdy[r] * A.o.rdy[r] + A.o.rdz[r] * A.o.rdz[r]);
@@ -1605,6 +1607,7 @@ __global__ __launch_bounds__(256) void k_count(CompactArgs A)
     }
     pk = wave_sum(pk);
     dm = wave_max(dm);
+    if (any_lane(neg) && lane == 0) atomicOr(&A.acc->pneg, 1u);
     if (lane == 0) {
         s_cnt[0][wv] = cR; s_cnt[1][wv] = cT; s_cnt[2][wv] = cM; s_pow[wv] = pk; s_dm[wv] = dm;
     }
@@ -1690,6 +1693,7 @@ __global__ __launch_bounds__(1024) void k_scan(CompactArgs A)
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&o->dmax2_bits, a.dmax2_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&o->qerr, a.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&o->pneg, a.pneg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             // every counter store acknowledged before the sequence number is sent
             // (a release fence would also write back the whole L2)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1996,7 +2000,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
                 DevAcc *d = A.acc;
                 d->nR = a.nR; d->nT = a.nT; d->m_total = a.m_total; d->nM_iter = a.nM_iter;
                 d->pow_next = a.pow_next; d->dmax2_bits = a.dmax2_bits; d->qerr = a.qerr;
-                d->seq = 0u; d->pad = 0u;
+                d->seq = 0u; d->pneg = 0u;
 #pragma unroll
                 for (int m = 0; m < LPC_MP_MAX; ++m) d->mpow[m] = mp[m];
             }
@@ -2128,6 +2132,23 @@ __global__ __launch_bounds__(256) void k_pack4(int64_t n, const float *__restric
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = make_float4(x[i], y[i], z[i], 0.0f);
+}
+
+// Results export (iterative_tracer.py:335-355): one chunk's part of the
+// iteration's results tuple in its host layout, so one DMA moves it:
+// [origin (n,4) if org][dest (n,4)][pow (n)][meas (n)], w = 0.  Each thread
+// writes whole 16-byte rows (coalesced); the copy to the caller's pinned block
+// runs on the export stream while the next kernels run.
+__global__ __launch_bounds__(256) void k_export(int64_t n, RaysIn in, ShadeOutPtrs o, int org,
+                                                float4 *__restrict__ xo, float4 *__restrict__ xd,
+                                                float *__restrict__ xp, int32_t *__restrict__ xm)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (org) xo[i] = make_float4(in.ox[i], in.oy[i], in.oz[i], 0.0f);
+    xd[i] = make_float4(o.destx[i], o.desty[i], o.destz[i], 0.0f);
+    xp[i] = o.pw[i];
+    xm[i] = o.meas[i];
 }
 
 // (n,4) rows -> SoA xyz

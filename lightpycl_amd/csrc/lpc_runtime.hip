@@ -182,6 +182,15 @@ struct lpc_handle {
     bool early_acc = true;                          // LPC_EARLY_ACC: read the counters before k_scatter ends
     bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
+    // results export (lpc_trace_iterate_export): k_export packs a chunk's part of
+    // the results tuple into xst[par] on the main stream, the export stream copies
+    // it to the caller's host block while the next kernels run
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_xready[2] = {nullptr, nullptr}, ev_xdone[2] = {nullptr, nullptr};
+    bool xdone_rec[2] = {false, false};             // ev_xdone[par] recorded (the staging may still be read)
+    DBuf xst[2];
+    int xpar = 0;
+    bool x_inflight = false;                        // copies queued on xstream
     hipEvent_t ev_side[2] = {nullptr, nullptr};     // rays ready (main -> side), slivers done (side -> main)
     double host_last = 0.0;
     bool pop_init = false;                          // the population is I (the emitted rays, set_rays)
@@ -269,6 +278,10 @@ static int settle(lpc_handle *h)
     if (h && h->inflight) {
         h->inflight = false;
         if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    if (h && h->x_inflight) {                       // results-export copies to the caller's host blocks
+        h->x_inflight = false;
+        if (h->xstream) HIPCHK(h, hipStreamSynchronize(h->xstream));
     }
     return 0;
 }
@@ -1392,6 +1405,12 @@ int lpc_close(lpc_handle *h)
     prof_resolve(h);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->stream2) { (void)hipStreamSynchronize(h->stream2); (void)hipStreamDestroy(h->stream2); }
+    if (h->xstream) { (void)hipStreamSynchronize(h->xstream); (void)hipStreamDestroy(h->xstream); }
+    for (int k = 0; k < 2; ++k) {
+        if (h->ev_xready[k]) (void)hipEventDestroy(h->ev_xready[k]);
+        if (h->ev_xdone[k]) (void)hipEventDestroy(h->ev_xdone[k]);
+        dfree(h->xst[k]);
+    }
     for (hipEvent_t e : h->ev_side) if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1973,7 +1992,7 @@ static int wait_mapped_acc(lpc_handle *h, unsigned seq, DevAcc *out)
     }
     out->nR = m->nR; out->nT = m->nT; out->m_total = m->m_total; out->nM_iter = m->nM_iter;
     out->pow_next = m->pow_next; out->dmax2_bits = m->dmax2_bits; out->qerr = m->qerr;
-    out->seq = m->seq; out->pad = 0;
+    out->seq = m->seq; out->pneg = m->pneg;
     for (int k = 0; k < LPC_MP_MAX; ++k) out->mpow[k] = m->mpow[k];
     return 0;
 }
@@ -1993,11 +2012,70 @@ struct Pending {
     bool was_init = false, was_traced = false, was_emitted = false;
 };
 
+// A results export (lpc_trace_iterate_export): the caller's host block and
+// whether it holds the origins.  Host layout over the iteration's N rays:
+// [origin (N,4) if org][dest (N,4)][pow (N)][meas (N)].
+struct ExportSpec {
+    char *host = nullptr;
+    int org = 0;
+};
+
+// One chunk's export: k_export packs it into a staging buffer in the host
+// layout, the export stream copies it to the caller's block (one DMA when the
+// chunk is the whole population) while the main stream runs on.  Two staging
+// buffers alternate; the main stream waits for a buffer's last copy before
+// packing into it again.
+static int export_chunk(lpc_handle *h, const RaysIn &in, const ShadeOutPtrs &o, int64_t nc, int64_t base,
+                        int64_t N, const ExportSpec &X)
+{
+    if (!h->xstream) {
+        HIPCHK(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k) {
+            HIPCHK(h, hipEventCreateWithFlags(&h->ev_xready[k], hipEventDisableTiming));
+            HIPCHK(h, hipEventCreateWithFlags(&h->ev_xdone[k], hipEventDisableTiming));
+        }
+    }
+    const int par = h->xpar;
+    h->xpar ^= 1;
+    const size_t orow = X.org ? 16 : 0;
+    const size_t row = orow + 16 + 4 + 4;
+    if (h->xst[par].bytes < (size_t)nc * row && h->xdone_rec[par])
+        HIPCHK(h, hipEventSynchronize(h->ev_xdone[par]));      // its last copy ends before it is freed
+    RETIF(dalloc(h, h->xst[par], (size_t)nc * row));
+    if (h->xdone_rec[par]) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_xdone[par], 0));
+    char *d = (char *)h->xst[par].p;
+    float4 *xo = (float4 *)d;
+    float4 *xd = (float4 *)(d + (size_t)nc * orow);
+    float *xp = (float *)(d + (size_t)nc * (orow + 16));
+    int32_t *xm = (int32_t *)(d + (size_t)nc * (orow + 20));
+    hipLaunchKernelGGL(k_export, dim3(grid1(nc)), dim3(256), 0, h->stream, nc, in, o, X.org, xo, xd, xp, xm);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev_xready[par], h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->xstream, h->ev_xready[par], 0));
+    if (nc == N) {
+        HIPCHK(h, hipMemcpyAsync(X.host, d, (size_t)nc * row, hipMemcpyDeviceToHost, h->xstream));
+    } else {                                                    // chunk: each section at its rays' offset
+        size_t hoff = 0, doff = 0;
+        const size_t elt[4] = {orow, 16, 4, 4};
+        for (int k = 0; k < 4; ++k) {
+            if (elt[k] == 0) continue;
+            HIPCHK(h, hipMemcpyAsync(X.host + hoff + (size_t)base * elt[k], d + doff, (size_t)nc * elt[k],
+                                     hipMemcpyDeviceToHost, h->xstream));
+            hoff += (size_t)N * elt[k];
+            doff += (size_t)nc * elt[k];
+        }
+    }
+    HIPCHK(h, hipEventRecord(h->ev_xdone[par], h->xstream));
+    h->xdone_rec[par] = true;
+    h->x_inflight = true;
+    return 0;
+}
+
 // Enqueue one iteration over the current population (host-sized: h->n_cur rays;
 // ds != NULL: device-sized, traced single-chunk only).  Host bookkeeping that
 // needs no counters (population roles) happens here; iter_collect the rest.
 static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow, int32_t *out_meas,
-                        float *out_next_pow, const DevSize *ds, Pending *P)
+                        float *out_next_pow, const DevSize *ds, Pending *P, const ExportSpec *X = nullptr)
 {
     *P = Pending();
     P->was_init = h->pop_init; P->was_traced = h->pop_traced; P->was_emitted = h->pop_emitted;
@@ -2027,7 +2105,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     float *mf = (float *)h->m_buf.p;
     // traced mode: one chunk, no per-ray export (the population then comes out in
     // its parents' coherence order; measured rays per iteration likewise)
-    const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow;
+    const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow || X;
     const bool traced = h->traced && C >= N && !exports;
     // the counters come back through the mapped host ring k_scan / k_stage_move
     // write, so the host decides and launches the next iteration while the rows
@@ -2134,6 +2212,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
         }
         RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
         hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
+        if (X) RETIF(export_chunk(h, in, o, nc, base, N, *X));
         if (out_origin4 || out_dest4 || out_pow || out_meas) {
             // the copies below run on the null stream: the shading on h->stream first
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2178,6 +2257,7 @@ static int iter_collect(lpc_handle *h, const Pending &P, float *out_next_pow, lp
     lpc_iter_stats S;
     memset(&S, 0, sizeof(S));
     S.n_in = P.n_in;
+    S.power_nonneg = 1;
     if (P.empty) { if (st) *st = S; return 0; }
     DevAcc acc;
     const double t_wait = h->host_prof ? host_us() : 0.0;
@@ -2209,6 +2289,7 @@ static int iter_collect(lpc_handle *h, const Pending &P, float *out_next_pow, lp
     if (h->mp_valid) memcpy(h->mp_last, acc.mpow, sizeof(h->mp_last));
     S.n_reflect = nR; S.n_refract = nT; S.n_measured = (int64_t)acc.nM_iter;
     S.power_next = acc.pow_next;
+    S.power_nonneg = P.fused ? -1 : (acc.pneg ? 0 : 1);
     float dm2;
     memcpy(&dm2, &acc.dmax2_bits, 4);
     RETIF(check_dcap(h, (double)dm2));
@@ -2241,6 +2322,46 @@ int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float
     if (h->host_prof && !P.empty)
         fprintf(stderr, "[lpc host] n %lld  launch %.1f us\n", (long long)P.n_in, host_us() - t_enter);
     return iter_collect(h, P, out_next_pow, st);
+}
+
+int lpc_trace_iterate_export(lpc_handle *h, void *host, int32_t flags, lpc_iter_stats *st)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!host) return set_err(h, LPC_E_ARG, "trace_iterate_export: null host block");
+    if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_iterate_export before trace_set_rays");
+    HIPCHK(h, hipSetDevice(h->device));
+    ExportSpec X;
+    X.host = (char *)host;
+    X.org = (flags & 1) ? 1 : 0;
+    Pending P;
+    RETIF(iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &P, &X));
+    return iter_collect(h, P, nullptr, st);
+}
+
+int lpc_trace_population_power(lpc_handle *h, float *out)
+{
+    if (!h || !out) return set_err(h, LPC_E_ARG, "null argument");
+    RETIF(settle(h));
+    if (h->n_cur > 0) {
+        const Pop &P = h->pop_init ? h->I : h->A;
+        HIPCHK(h, hipMemcpy(out, P.f(6), (size_t)h->n_cur * 4, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int lpc_host_alloc(size_t bytes, void **out)
+{
+    if (!out) return set_err(nullptr, LPC_E_ARG, "host_alloc: null output");
+    *out = nullptr;
+    const hipError_t e = hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault);
+    if (e != hipSuccess) return set_err(nullptr, LPC_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int lpc_host_free(void *p)
+{
+    if (p) (void)hipHostFree(p);
+    return 0;
 }
 
 // May the iteration after the one in flight (population <= bound rays, chained

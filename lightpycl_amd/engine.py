@@ -201,6 +201,37 @@ class Engine:
         return st, dict(origin=org, dest=dst, pow=pw, meas=ms,
                         next_pow=nxt[: st.n_reflect + st.n_refract])
 
+    def iterate_export(self, with_origin=True):
+        """One iteration with its results tuple exported asynchronously
+        (lpc_trace_iterate_export) into a pinned block: returns (stats, dict of
+        origin (N,4) [if with_origin], dest (N,4), pow (N,), meas (N,) numpy views).
+        The arrays are complete after :meth:`sync` (the copy overlaps the next
+        iteration's kernels)."""
+        from .pinned import POOL
+        n = self.population()
+        st = _lib.IterStats()
+        if n == 0:
+            self._c(self.L.lpc_trace_iterate(self.h, None, None, None, None, None, ctypes.byref(st)))
+            z = np.zeros((0, 4), np.float32)
+            return st, dict(origin=z, dest=z.copy(), pow=np.zeros(0, np.float32), meas=np.zeros(0, np.int32))
+        layout = ([(np.float32, (n, 4))] if with_origin else []) + [(np.float32, (n, 4)), (np.float32, (n,)),
+                                                                     (np.int32, (n,))]
+        blk = POOL.block(n * ((16 if with_origin else 0) + 24))
+        self._c(self.L.lpc_trace_iterate_export(self.h, ctypes.cast(blk, ctypes.c_void_p), 1 if with_origin else 0,
+                                                ctypes.byref(st)))
+        v = POOL.views(blk, layout)
+        if not with_origin:
+            v = [None] + v
+        return st, dict(origin=v[0], dest=v[1], pow=v[2], meas=v[3])
+
+    def population_power(self):
+        """The current population's power (lpc_trace_population_power)."""
+        n = self.population()
+        out = np.empty(n, np.float32)
+        if n:
+            self._c(self.L.lpc_trace_population_power(self.h, ptr(out)))
+        return out
+
     def sync(self):
         """lpc_sync: wait for every kernel queued on the engine's stream."""
         self._c(self.L.lpc_sync(self.h))

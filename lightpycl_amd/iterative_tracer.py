@@ -114,29 +114,64 @@ class CL_Tracer:
         self.iteration_counts = []
         self.power_left = []
         self._aggregate = not keep_results
+        self.exact_sums = 0                     # stop tests that needed the powers (_power_decision)
         thr = (1.0 - trace_until_dissipated) * input_power              # :383
         t0 = time.time()
-        for t_iter in range(int(trace_iterations)):                     # :241
-            self.iteration_counts.append(n)
-            st, ex = self.engine.iterate(export=keep_results)
-            if keep_results:
-                org = origin if t_iter == 0 else ex["origin"]
-                pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
-                self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355
-                power_in_scene = f32_sorted_sum(ex["next_pow"])         # :372
-            else:
-                power_in_scene = st.power_next
-            n = st.n_reflect + st.n_refract
-            self.power_left.append(float(power_in_scene) / float(input_power) if input_power else 0.0)
-            if self.verbose:
-                print(f"iteration {t_iter + 1}: {st.n_in} rays, {n} children kept, "
-                      f"{100.0 * self.power_left[-1]:.4f} % power left")
-            if power_in_scene < thr:
-                break
-            if n == 0:
-                break
+        try:
+            for t_iter in range(int(trace_iterations)):                 # :241
+                self.iteration_counts.append(n)
+                if keep_results:
+                    # the results tuple (:335-355) copied to pinned host arrays on
+                    # the export stream while the next iterations run (complete
+                    # after the sync below); iteration 0's origins are the host's
+                    st, ex = self.engine.iterate_export(with_origin=t_iter > 0)
+                    org = origin if t_iter == 0 else ex["origin"]
+                    pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
+                    self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355
+                    power_in_scene, below = self._power_decision(st, thr)    # :372, :383
+                else:
+                    st, _ = self.engine.iterate()
+                    power_in_scene = st.power_next
+                    below = power_in_scene < thr
+                n = st.n_reflect + st.n_refract
+                self.power_left.append(float(power_in_scene) / float(input_power) if input_power else 0.0)
+                if self.verbose:
+                    print(f"iteration {t_iter + 1}: {st.n_in} rays, {n} children kept, "
+                          f"{100.0 * self.power_left[-1]:.4f} % power left")
+                if below:
+                    break
+                if n == 0:
+                    break
+        finally:
+            self.engine.sync()                  # the exported results arrays are complete
         self.sim_time = time.time() - t0
         return self.results
+
+    # float32 unit roundoff; a sequential float32 sum of n non-negative values in
+    # ascending order is within 1.2 * u * S * (n + 1) / 2 of the exact sum S when
+    # n * u <= 0.1 (each partial sum s_k <= k S / n, first-order error u * sum s_k,
+    # the factor covers the higher-order terms)
+    _U32 = 2.0 ** -24
+
+    def _power_decision(self, st, thr):
+        """The reference's stop test ``sum(np.sort(rays_pow)) < thr`` (:372, :383)
+        on the next population, decided without copying its powers when the
+        device's float64 sum S is farther from thr than the float32 sorted sum's
+        error bound allows; otherwise the powers are fetched and summed exactly
+        as the reference does.  Returns (power left, stop)."""
+        n = int(st.n_reflect + st.n_refract)
+        S = float(st.power_next)
+        if n == 0:
+            return np.float32(0.0), np.float32(0.0) < thr
+        if st.power_nonneg == 1 and n * self._U32 <= 0.1:
+            B = 1.2 * self._U32 * abs(S) * (n + 1) / 2.0
+            if S + B < float(thr):
+                return S, True
+            if S - B >= float(thr):
+                return S, False
+        v = f32_sorted_sum(self.engine.population_power())
+        self.exact_sums = getattr(self, "exact_sums", 0) + 1
+        return v, v < thr
 
     # ------------------------------------------------------------------------
     def ray_bounces(self):
@@ -289,7 +324,12 @@ class CL_Tracer:
     def pickle_results(self, fname=None):
         """Pickle (results, meshes) with protocol 1 to ./<timestamp>-tracer_results.txt,
         as the reference writes them (``pickle.dumps((results, meshes), 1)``, :711-733).
-        Aggregate-mode traces have no per-ray results: they are fetched first."""
+        An aggregate-mode trace (``keep_results=False``) kept no per-ray results
+        on the host or the device, so there is nothing the reference's loader
+        could read: it raises ValueError instead of writing an empty record."""
+        if self._aggregate:
+            raise ValueError("pickle_results: this trace ran with keep_results=False and kept no per-ray "
+                             "results; trace with keep_results=True (the reference's mode) to pickle them")
         if fname is None:
             fname = "./{0}-tracer_results.txt".format(time.strftime("%Y.%m.%d.%H.%M.%S"))
         try:

@@ -183,6 +183,12 @@ def test_pickle_results_protocol1_and_reference_module_names(tmp_path):
     assert type(tr3.meshes[0]).__name__ == "GeoObject"
     with pytest.raises(Exception):
         pickle.loads(ref_raw)                   # a plain loader cannot resolve the reference's module
+    # an aggregate-mode trace kept no per-ray results: no empty record is written
+    tr4 = CL_Tracer.__new__(CL_Tracer)
+    tr4.results, tr4.meshes, tr4._aggregate = [], sc.meshes, True
+    with pytest.raises(ValueError):
+        tr4.pickle_results(str(tmp_path / "agg.txt"))
+    assert not (tmp_path / "agg.txt").exists()
 
 
 def test_select_device_by_name(monkeypatch):
@@ -204,3 +210,53 @@ def test_select_device_by_name(monkeypatch):
     assert select_device("Other", names) == 4
     monkeypatch.setenv("LOCAL_RANK", "4")
     assert select_device("gfx950", names) == 3        # default not among the matches: last match
+
+
+def test_power_decision_bound():
+    """The results-mode stop test (iterative_tracer.py:372, :383) decided from the
+    device's float64 sum when the float32 sorted sum's error bound cannot cross
+    the threshold; the bound holds on adversarial non-negative data."""
+    import numpy as np
+    from lightpycl_amd.iterative_tracer import CL_Tracer, f32_sorted_sum
+    rng = np.random.default_rng(5)
+    U = CL_Tracer._U32
+    for n in (1, 10, 1000, 100000, 1000000):
+        for kind in range(3):
+            if kind == 0:
+                x = rng.random(n).astype(np.float32)
+            elif kind == 1:
+                x = (rng.random(n) ** 8).astype(np.float32) * np.float32(1e-3)
+            else:
+                x = np.full(n, np.float32(1.0 + 2.0 ** -23))
+            exact = float(np.sum(x, dtype=np.float64))
+            f32 = float(f32_sorted_sum(x))
+            if n * U <= 0.1:
+                B = 1.2 * U * exact * (n + 1) / 2.0
+                assert abs(f32 - exact) <= B, (n, kind, f32, exact, B)
+
+    class St:
+        pass
+
+    class Eng:
+        def __init__(self, p):
+            self.p = p
+            self.fetched = 0
+
+        def population_power(self):
+            self.fetched += 1
+            return self.p
+
+    p = rng.random(200000).astype(np.float32)
+    S = float(np.sum(p, dtype=np.float64))
+    tr = CL_Tracer.__new__(CL_Tracer)
+    tr.engine = Eng(p)
+    st = St()
+    st.n_reflect, st.n_refract, st.power_next, st.power_nonneg = 150000, 50000, S, 1
+    for thr in (np.float32(S * 0.5), np.float32(S * 1.5)):                  # far: no fetch
+        v, stop = tr._power_decision(st, thr)
+        assert stop == (f32_sorted_sum(p) < thr) and tr.engine.fetched == 0
+    v, stop = tr._power_decision(st, np.float32(S))                          # near: exact, as the reference
+    assert tr.engine.fetched == 1 and v == f32_sorted_sum(p) and stop == (v < np.float32(S))
+    st.power_nonneg = 0                                                      # negative powers: always exact
+    tr._power_decision(st, np.float32(S * 0.5))
+    assert tr.engine.fetched == 2
