@@ -57,7 +57,14 @@ TRI_BYTES = 40                 # per triangle per bounce-iterati
 MT_FLOPS = 46                  # Moller-Trumbore flops per ray-triangle test
 WALK_KERNEL = "k_rootwalk"     # the hierarchy-walk kernel the HIP events time
 # BASELINE.json configs 2-4: scene, rays, depth (full size, one GPU)
-CONFIGS = [("parabolic", 1_000_000, 4), ("lens", 10_000_000, 8), ("eye", 10_000_000, 16)]
+CONFIGS = [("parabolic", 1_000_000, 4), ("lens", 10_000_000, 8), ("eye", 10_000_000, 16),
+           # beside the headline: the synthetic generator with ~79 % of the
+           # rays entering a refractive sphere, so the secondaries are most of the work
+           ("synthetic_dense", 1_000_000, 16)]
+# the drop-in's default results mode end to end, as the reference's examples time
+# it (example_directivity_parabolic_mirror.py:88-102: time() around
+# CL_Tracer.iterative_tracer with per-iteration results tuples on the host)
+RESULTS_CONFIG = ("parabolic", 1_000_000, 4)
 
 
 def parse():
@@ -238,6 +245,36 @@ def run_configs(Engine, ShardedTrace, scenes):
                      "steps_identical": all(x["global_counts"] == r["global_counts"] for x in res),
                      "measured_power": float(np.sum(r["mesh_power"])), "input_power": in_pow}
         e.close()
+    out["results_mode"] = run_results_mode()
+    return out
+
+
+def run_results_mode():
+    """RESULTS_CONFIG through the drop-in exactly as a reference user calls it:
+    CL_Tracer.iterative_tracer(keep_results=True) end to end (mesh flattening and
+    upload, per-iteration results tuples exported to host numpy arrays, the
+    reference's stop test), ray-bounces = sum of the results tuples' lengths."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    name, n, depth = RESULTS_CONFIG
+    sc = scenes.BUILDERS[name](n=n, seed=7, iterations=depth)
+    tr = CL_Tracer(device=0)
+    kw = dict(trace_iterations=depth, trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env)
+    tr.iterative_tracer(sc.sources, sc.meshes, **kw)                 # warm-up (allocations, pinned blocks)
+    times = []
+    for _ in range(5):
+        t = time.perf_counter()
+        res = tr.iterative_tracer(sc.sources, sc.meshes, **kw)
+        times.append(time.perf_counter() - t)
+    b = sum(len(r[3]) for r in res)
+    dt = sorted(times)[len(times) // 2]
+    out = {"scene": name, "rays": n, "depth": depth, "iterations": len(res), "ray_bounces": b,
+           "ms_per_trace_median": dt * 1e3, "ms_per_trace_all": [x * 1e3 for x in times],
+           "ray_bounces_per_s": b / dt, "exact_power_sums": int(getattr(tr, "exact_sums", 0)),
+           "host_bytes_per_trace": int(sum(sum(a.nbytes for a in r) for r in res)),
+           "note": "CL_Tracer(...).iterative_tracer(keep_results=True) end to end: the results tuples "
+                   "(iterative_tracer.py:355) land in host numpy arrays; PCIe-inclusive, not the headline value"}
+    tr.engine.close()
     return out
 
 

@@ -141,5 +141,17 @@ def synthetic(n=1_000_000, seed=7, iterations=16, grid=3, spacing=30.0, radius=1
                      hist_points=100)
 
 
+def synthetic_dense(n=1_000_000, seed=7, iterations=16):
+    """The synthetic generator with the nine spheres packed in front of the source
+    (21-unit grid at z = 13, the central sphere subtending 50 degrees): ~79 % of
+    the emitted rays enter a refractive sphere (measured on 20 k rays with the
+    oracle), so bounces/s covers the secondaries, not only iteration 1
+    ("place the objects so most rays hit refractive
+    surfaces").  Same 103,660 triangles."""
+    sc = synthetic(n=n, seed=seed, iterations=iterations, spacing=21.0, z=13.0)
+    sc.name = "synthetic_dense"
+    return sc
+
+
 BUILDERS = dict(parabolic=parabolic, lens=lens, eye=eye, cube=cube, nested_cubes=nested_cubes,
-                synthetic=synthetic)
+                synthetic=synthetic, synthetic_dense=synthetic_dense)
