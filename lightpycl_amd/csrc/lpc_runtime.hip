@@ -2298,6 +2298,21 @@ static int iter_collect(lpc_handle *h, const Pending &P, float *out_next_pow, lp
     return 0;
 }
 
+// A sharded trace's dropped speculative iteration may have run non-empty: its
+// k_stage_move added its measured power to the trace's running sums on the
+// device; they go back to the last read iteration's (the host copy).  Its
+// measured rows lie past m_total and its children in the scratch population,
+// both ignored.
+static int restore_mrun(lpc_handle *h)
+{
+    if (!h->mp_valid || !h->d_mrun.p) return 0;
+    // rare (a misprediction at the trace's end): after the dropped iteration's
+    // kernels, a synchronous copy from the handle's host copy
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(h->d_mrun.p, h->mp_last, sizeof(h->mp_last), hipMemcpyHostToDevice));
+    return 0;
+}
+
 // A speculative iteration the trace did not need (it ran empty on the device:
 // IterCtl said 0): the population roles go back to before its enqueue.
 static void iter_discard(lpc_handle *h, const Pending &P)
@@ -2366,11 +2381,12 @@ int lpc_host_free(void *p)
 
 // May the iteration after the one in flight (population <= bound rays, chained
 // traced) be enqueued device-sized?  Single chunk, fused compaction, mapped
-// counters, root-item path, no all-reduce hook (a sharded trace decides on the
-// sums over all ranks, which the device does not see), no per-kernel profiling.
+// counters, root-item path, no per-kernel profiling.  A sharded trace (all-reduce
+// hook) speculates too: the device then stops only on an empty local population,
+// and the host drops the iteration when the ranks' sums end the trace.
 static bool ds_ok(const lpc_handle *h, int64_t bound)
 {
-    return h->spec && !h->xchg && h->traced && h->fuse_compact && h->early_acc && h->acc_map_dev &&
+    return h->spec && h->traced && h->fuse_compact && h->early_acc && h->acc_map_dev &&
            (!h->prof || h->prof_light) && h->queue == 2 && !h->prof_waves && h->roots_s > 0 && bound > 0 &&
            bound <= chunk_rays(h) && bound < h->resort_min && (bound + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
            (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES && h->K <= LPC_Q_MAX_SLOTS;
@@ -2399,7 +2415,11 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     const bool hist_ok = n0 > 0 && h->hist_iter == max_iter && !h->hist_r.empty();
     h->dcap_rebuilt = false;
     std::vector<int64_t> seen;
-    h->ds_thr = power_threshold;
+    // the device's stop rule for speculative iterations (k_stage_move): the
+    // threshold on this device's own power left -- or, in a sharded trace, none:
+    // the power left is a sum over all ranks, only the host sees it after the
+    // exchange, and a speculative iteration the ranks' sums end is dropped
+    h->ds_thr = h->xchg ? -INFINITY : power_threshold;
     int rc = 0;
     bool exchanged = false;             // rc came from the exchange itself (no poison owed)
     Pending cur, nxt;
@@ -2443,11 +2463,14 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
             const bool rebuilt = h->dcap_rebuilt;
             h->dcap_rebuilt = false;
             if (stop || rebuilt || i + 1 >= max_iter) {
-                // ran empty on the device (its IterCtl size was 0): not part of the trace
+                // not part of the trace: it ran empty on the device (its IterCtl
+                // size was 0) -- or, sharded, it may have run on this rank's kept
+                // children when the ranks' sums stopped the trace
                 iter_discard(h, nxt);
                 have_nxt = false;
+                if (h->xchg) RETIF(restore_mrun(h));
             } else {
-                nxt.n_in = G.n_reflect + G.n_refract;
+                nxt.n_in = S.n_reflect + S.n_refract;           // this rank's population
                 cur = nxt;
                 have_cur = true;
                 have_nxt = false;
