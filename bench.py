@@ -47,11 +47,26 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector peak
-# VALU issue peak: each CU has 4 SIMDs of 16 lanes, so a wave64 VALU instruction
-# occupies its SIMD for 4 cycles; 256 CUs x 4 SIMDs x 2.4 GHz / 4 = 614.4 G
-# wave-instructions per second (x 64 lanes x 2 flops = the 78.6 TF FP32 FMA peak
-# without packing; packed FP32 doubles the flops, not the instruction rate)
-VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4
+# VALU issue peak: MI355X_MICROARCH.md:54,473 -- a CU has 4 SIMD-32 units and a
+# wave64 v_fma_f32 issues in 2 cycles when several waves share a SIMD (4 for one
+# wave alone): 256 CUs x 4 SIMDs x 2.4 GHz / 2 = 1.229 T wave-instructions/s.
+# Rounds 2-3 used 4 cycles (half this peak, so twice the fraction).  When the
+# committed microbenchmark (tools/valu_issue.hip, profiles/r04_valu_issue.json)
+# is present, its best measured chip rate replaces the guide's figure.
+VALU_ISSUE_PEAK_GUIDE = 256 * 4 * 2.4e9 / 2
+VALU_ISSUE_FILE = os.path.join(ROOT, "profiles", "r04_valu_issue.json")
+
+
+def valu_issue_peak():
+    """(peak wave-instructions/s, source): the measured v_fma_f32 rate of the
+    committed microbenchmark (best over 1-8 waves per SIMD), else the guide's."""
+    try:
+        with open(VALU_ISSUE_FILE) as f:
+            rows = json.load(f)["rows"]
+        best = max(r["wave_instr_per_s"] for r in rows if r["op"] == "v_fma_f32")
+        return best, "measured: profiles/r04_valu_issue.json (tools/valu_issue.hip, v_fma_f32, best over waves/SIMD)"
+    except (OSError, KeyError, ValueError):
+        return VALU_ISSUE_PEAK_GUIDE, "MI355X_MICROARCH.md:54,473 (2 cycles per wave64 VALU instruction per SIMD)"
 RAY_BYTES = 156                # SURVEY.md 8(d): algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # SURVEY.md 8(d): per triangle per bounce-iteration
 MT_FLOPS = 46                  # SURVEY.md 8(d): Moller-Trumbore flops per ray-triangle test
@@ -458,6 +473,7 @@ def main():
     traffic = None if stale else pmc.get("hbm_bytes_per_launch")
     valu_per_launch = None if stale else pmc.get("sq_insts_valu_mean")
     valu_rate = valu_per_launch / (avg_ms * 1e-3) if valu_per_launch and avg_ms > 0 else None
+    valu_peak, valu_peak_src = valu_issue_peak()
     out = {
         "metric": "ray-bounces/sec @ 1M rays x 100k tris",
         "value": bounces_all / dt,
@@ -486,12 +502,12 @@ def main():
                              f"(null when that summary was collected on other kernel sources)"},
         # the bound that actually limits the walk kernel: executed VALU issue
         "roofline_valu": {"bound": "valu", "kernel": WALK_KERNEL,
-                          "achieved": valu_rate, "peak": VALU_ISSUE_PEAK, "unit": "wave-instr/s",
-                          "frac": valu_rate / VALU_ISSUE_PEAK if valu_rate else None,
+                          "achieved": valu_rate, "peak": valu_peak, "peak_source": valu_peak_src,
+                          "unit": "wave-instr/s", "frac": valu_rate / valu_peak if valu_rate else None,
                           "valu_insts_per_launch": valu_per_launch, "pmc_stale": stale,
                           "note": f"executed VALU wave-instructions per {WALK_KERNEL} launch (PMC SQ_INSTS_VALU, "
-                                  "profiles/pmc_intersect.json) / its live average launch time / chip issue "
-                                  "peak (256 CU x 4 SIMD x 2.4 GHz / 4 cycles per wave64 instruction on a 16-lane SIMD)"},
+                                  "profiles/pmc_intersect.json) / its live average launch time / the chip's "
+                                  "VALU issue peak (peak_source)"},
         # brute-force equivalent: what the reference's O(N*M) loop would have to sustain
         "ri_equivalent": {"ri_per_s": pairs_per_s, "mt_tflops_equiv": mt_tflops,
                           "fp32_peak_tflops": FP32_PEAK_TFLOPS,
