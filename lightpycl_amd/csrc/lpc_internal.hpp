@@ -231,6 +231,17 @@ struct MoveArgs {
                                       //   ngroups and m_base from ctl[par] as well)
     double thr;                       // trace_run's power threshold (-inf: none)
     double dcap2;                     // Dcap^2 (1 - 1e-6), check_dcap's bound
+    // an iteration in several chunks (population > one chunk): each chunk's launch
+    // places its rows after the earlier chunks' -- reflected into popR, refracted
+    // into the staging popT (k_append moves them behind all reflected), measured
+    // rays after the record -- from the running bases of cbase_in (written by the
+    // previous chunk's block 0, ping-pong), and block 0 adds the chunk's counters
+    // to the iteration's (acc).  popT == NULL: one chunk, refracted after reflected.
+    float *popT;
+    int64_t capT;
+    const unsigned long long *cbase_in;   // [3] R, T, M bases (first chunk: 0, 0, m_base)
+    unsigned long long *cbase_out;
+    int first, last;
 };
 
 struct PostprocAosArgs {

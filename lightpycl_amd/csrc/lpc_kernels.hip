@@ -1898,6 +1898,10 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     // block also publishes an empty iteration's counters)
     int64_t ntiles = A.ntiles, ngroups = A.ngroups;
     unsigned long long m_base = A.m_base;
+    // chunked iteration: this chunk's rows go after the earlier chunks'
+    const bool chunked = !DS && A.popT != nullptr;
+    unsigned long long r_base = 0, t_base = 0;
+    if (chunked && !A.first) { r_base = A.cbase_in[0]; t_base = A.cbase_in[1]; m_base = A.cbase_in[2]; }
     if constexpr (DS) {
         const long long n = A.ctl->n[A.par];
         ntiles = (n + LPC_ST_TILE - 1) / LPC_ST_TILE;
@@ -1996,6 +2000,20 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
             a.pow_next = s_p[0];
             a.dmax2_bits = __float_as_uint(s_d[0]);
             a.qerr = A.acc->qerr;
+            if (chunked) {
+                // the next chunk's bases, and this chunk's counters added to the
+                // iteration's (the earlier chunks' in acc; chunk order, so the
+                // float64 power sum is deterministic)
+                A.cbase_out[0] = r_base + a.nR;
+                A.cbase_out[1] = t_base + a.nT;
+                A.cbase_out[2] = a.m_total;
+                if (!A.first) {
+                    const DevAcc &p = *A.acc;
+                    a.nR += p.nR; a.nT += p.nT; a.nM_iter += p.nM_iter;
+                    a.pow_next = p.pow_next + a.pow_next;
+                    a.dmax2_bits = __float_as_uint(fmaxf(__uint_as_float(p.dmax2_bits), s_d[0]));
+                }
+            }
             {
                 DevAcc *d = A.acc;
                 d->nR = a.nR; d->nT = a.nT; d->m_total = a.m_total; d->nM_iter = a.nM_iter;
@@ -2049,14 +2067,17 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     const int64_t c = A.cst, cb = A.capR, cm = A.capM, s0 = tile * LPC_ST_TILE;
     float row[2][8];
     int64_t dst[2] = {-1, -1};
+    bool toT[2] = {false, false};             // chunked: a refracted row into the staging population
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int i = t + h * LPC_ST_TILE;
         if (i < cR + cT) {
             const bool isR = i < cR;
+            toT[h] = chunked && !isR;
             const float *src = isR ? A.stR : A.stT;
             const int64_t q = s0 + (isR ? i : i - cR);
-            dst[h] = isR ? s_pre[0] + i : s_tot[0] + s_pre[1] + (i - cR);
+            dst[h] = isR ? (int64_t)r_base + s_pre[0] + i
+                         : chunked ? (int64_t)t_base + s_pre[1] + (i - cR) : s_tot[0] + s_pre[1] + (i - cR);
 #pragma unroll
             for (int a = 0; a < 8; ++a) row[h][a] = src[a * c + q];
         }
@@ -2069,8 +2090,10 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (dst[h] < 0) continue;
+        float *P = toT[h] ? A.popT : A.popR;
+        const int64_t pc = toT[h] ? A.capT : cb;
 #pragma unroll
-        for (int a = 0; a < 8; ++a) A.popR[a * cb + dst[h]] = row[h][a];
+        for (int a = 0; a < 8; ++a) P[a * pc + dst[h]] = row[h][a];
     }
     if (hasM) {
         const int64_t d = (int64_t)m_base + s_pre[2] + t;

@@ -196,6 +196,7 @@ struct lpc_handle {
     bool pop_init = false;                          // the population is I (the emitted rays, set_rays)
     bool mp_valid = false;                          // mp_last = the trace's measured power per measure mesh
     DBuf d_mrun;                                    // its running sums on the device (k_stage_move)
+    DBuf d_cbase;                                   // chunked traced iterations: running row bases (ping-pong)
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;
@@ -1395,7 +1396,7 @@ int lpc_close(lpc_handle *h)
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->w_bhist, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->d_misc, &h->d_wrec, &h->w_spill, &h->w_qroots,
-                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl};
+                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl, &h->d_cbase};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -2106,17 +2107,20 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     // traced mode: one chunk, no per-ray export (the population then comes out in
     // its parents' coherence order; measured rays per iteration likewise)
     const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow || X;
-    const bool traced = h->traced && C >= N && !exports;
+    const bool traced = h->traced && !exports;
     // the counters come back through the mapped host ring k_scan / k_stage_move
     // write, so the host decides and launches the next iteration while the rows
     // still move (profiling: only the light level, whose events end before)
-    const bool early = h->early_acc && h->acc_map_dev && C >= N && !out_next_pow && (!h->prof || h->prof_light);
+    const bool early = h->early_acc && h->acc_map_dev && (C >= N || (traced && h->fuse_compact)) && !out_next_pow &&
+                       (!h->prof || h->prof_light);
     ++h->acc_seq;
     P->seq = h->acc_seq;
     P->early = early;
     P->traced = traced;
-    // traced single chunk: k_shade_stage + k_stage_move
-    const bool fused = traced && h->fuse_compact && C >= N;
+    // traced: k_shade_stage + k_stage_move (several chunks: each places its rows
+    // after the earlier chunks', refracted rows staged in T, k_append at the end)
+    const bool fused = traced && h->fuse_compact;
+    if (fused && C < N) RETIF(dalloc(h, h->d_cbase, 8 * sizeof(unsigned long long)));
     if (ds && !(fused && early)) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the fused path");
     P->fused = fused;
     const size_t Cs = (size_t)h->ws_rays;
@@ -2197,6 +2201,17 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
             M.par = par;
             M.thr = h->ds_thr;
             M.dcap2 = h->dcap * h->dcap * (1.0 - 1e-6);
+            M.popT = nullptr; M.capT = 0; M.cbase_in = nullptr; M.cbase_out = nullptr;
+            M.first = 1; M.last = 1;
+            if (C < N) {                        // chunk base / C of several
+                const int64_t k = base / C;
+                unsigned long long *cb = (unsigned long long *)h->d_cbase.p;
+                M.popT = h->T.f(0); M.capT = h->T.cap;
+                M.cbase_in = cb + (k & 1) * 3; M.cbase_out = cb + ((k & 1) ^ 1) * 3;
+                M.first = base == 0 ? 1 : 0;
+                M.last = base + nc >= N ? 1 : 0;
+                if (!M.last) { M.host_acc = nullptr; M.ctl = nullptr; }   // the last chunk publishes the totals
+            }
             h->gdirty[1 - h->gpar] = 0;
             h->gdirty[h->gpar] = ng;            // this launch's k_shade_stage adds into its first ng groups
             h->gpar = 1 - h->gpar;

@@ -338,13 +338,15 @@ def test_trace_run_matches_host_loop(oracle_mod, checker):
 
 
 @pytest.mark.parametrize("name,n,chunk", [("synthetic", 20000, 0), ("lens", 20000, 0), ("eye", 3000, 0),
-                                          ("lens", 20000, 7000)])
+                                          ("lens", 20000, 7000), ("eye", 6000, 5000), ("synthetic", 30000, 6000)])
 def test_traced_order_equals_reference_order(monkeypatch, name, n, chunk):
     """Aggregate iterations in the launch's coherence order (traced mode, the
     default without per-ray export) against the same trace in the reference's
     ray order (LPC_TRACED=0): identical per-iteration counts, identical measured
-    rays as a set (bit for bit), per-mesh power to float64 summation order.  A
-    chunked population falls back to reference order."""
+    rays as a set (bit for bit), per-mesh power to float64 summation order.
+    With a chunk size below the population the traced iterations run chunk by
+    chunk (k_shade_stage + k_stage_move per chunk, running row bases, k_append
+    of the staged refracted block)."""
     from lightpycl_amd.engine import Engine
     sc = scenes.BUILDERS[name](n=n, seed=21)
     o4, d4, pw = rays_of(sc)
