@@ -140,6 +140,7 @@ struct lpc_handle {
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
     int spill_budget = 24;                          // node visits before a wave hands over (0 off)
+    int spill_budget_small = -1;                    // ... for populations below spill_small_n rays (-1: spill_budget)
     int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
     int64_t spill_large_n = 0;                      // 0: spill_large_per_tri x triangles
     int64_t spill_large_per_tri = 16;
@@ -769,7 +770,8 @@ static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
     SP->ctr = (uint32_t *)h->d_misc.p + LPC_MISC_SPILL;
     SP->cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
     const int64_t large_n = h->spill_large_n > 0 ? h->spill_large_n : h->spill_large_per_tri * (int64_t)h->M;
-    SP->budget = n >= large_n ? h->spill_budget_large : h->spill_budget;
+    SP->budget = n >= large_n ? h->spill_budget_large
+                 : (n < h->spill_small_n && h->spill_budget_small >= 0) ? h->spill_budget_small : h->spill_budget;
     SP->pair_shift = h->spill_pair_shift;
     return 0;
 }
@@ -1334,6 +1336,7 @@ int lpc_open(int device, lpc_handle **out)
     h->dcap_init = (double)env_int("LPC_DCAP_MILLI", 16000) / 1000.0;
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
+    h->spill_budget_small = (int)env_int("LPC_BUDGET_SMALL", h->spill_budget_small);
     h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
     h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
