@@ -58,15 +58,19 @@ VALU_ISSUE_FILE = os.path.join(ROOT, "profiles", "r04_valu_issue.json")
 
 
 def valu_issue_peak():
-    """(peak wave-instructions/s, source): the measured v_fma_f32 rate of the
-    committed microbenchmark (best over 1-8 waves per SIMD), else the guide's."""
+    """(peak wave-instructions/s, packed-FMA peak or None, source): the measured
+    v_fma_f32 rate of the committed microbenchmark (best over 1-8 waves per SIMD)
+    and its v_pk_fma_f32 rate (a packed FMA takes two issue slots), else the
+    guide's figure."""
     try:
         with open(VALU_ISSUE_FILE) as f:
             rows = json.load(f)["rows"]
         best = max(r["wave_instr_per_s"] for r in rows if r["op"] == "v_fma_f32")
-        return best, "measured: profiles/r04_valu_issue.json (tools/valu_issue.hip, v_fma_f32, best over waves/SIMD)"
+        pk = max(r["wave_instr_per_s"] for r in rows if r["op"] == "v_pk_fma_f32")
+        return best, pk, ("measured: profiles/r04_valu_issue.json (tools/valu_issue.hip: v_fma_f32 best over "
+                          "waves/SIMD; v_pk_fma_f32 issues at half that rate)")
     except (OSError, KeyError, ValueError):
-        return VALU_ISSUE_PEAK_GUIDE, "MI355X_MICROARCH.md:54,473 (2 cycles per wave64 VALU instruction per SIMD)"
+        return VALU_ISSUE_PEAK_GUIDE, None, "MI355X_MICROARCH.md:54,473 (2 cycles per wave64 VALU instruction per SIMD)"
 RAY_BYTES = 156                # SURVEY.md 8(d): algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # SURVEY.md 8(d): per triangle per bounce-iteration
 MT_FLOPS = 46                  # SURVEY.md 8(d): Moller-Trumbore flops per ray-triangle test
@@ -473,7 +477,7 @@ def main():
     traffic = None if stale else pmc.get("hbm_bytes_per_launch")
     valu_per_launch = None if stale else pmc.get("sq_insts_valu_mean")
     valu_rate = valu_per_launch / (avg_ms * 1e-3) if valu_per_launch and avg_ms > 0 else None
-    valu_peak, valu_peak_src = valu_issue_peak()
+    valu_peak, valu_peak_pk, valu_peak_src = valu_issue_peak()
     out = {
         "metric": "ray-bounces/sec @ 1M rays x 100k tris",
         "value": bounces_all / dt,
@@ -504,6 +508,7 @@ def main():
         "roofline_valu": {"bound": "valu", "kernel": WALK_KERNEL,
                           "achieved": valu_rate, "peak": valu_peak, "peak_source": valu_peak_src,
                           "unit": "wave-instr/s", "frac": valu_rate / valu_peak if valu_rate else None,
+                          "frac_if_all_packed": valu_rate / valu_peak_pk if valu_rate and valu_peak_pk else None,
                           "valu_insts_per_launch": valu_per_launch, "pmc_stale": stale,
                           "note": f"executed VALU wave-instructions per {WALK_KERNEL} launch (PMC SQ_INSTS_VALU, "
                                   "profiles/pmc_intersect.json) / its live average launch time / the chip's "

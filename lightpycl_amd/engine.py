@@ -7,12 +7,42 @@ per-bounce entry points of ``include/lpc.h`` with numpy arrays.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 
 import numpy as np
 
 from . import _lib
 from ._lib import check, f32, i32, ptr
+
+
+def _rows(x, w):
+    """x as an (n, w) ndarray without changing a value (an ndarray as is, a list of
+    rows through np.asarray), or None when it is not such a table."""
+    if type(x) is list:
+        try:
+            x = np.asarray(x)
+        except Exception:
+            return None
+    if type(x) is not np.ndarray or x.ndim != 2 or x.shape[1] != w or x.dtype.kind not in "fiu":
+        return None
+    return x
+
+
+def _tri_vertices(mesh):
+    """tribuf()'s three vertex lists as float32 (n,4) arrays, gathered at once when
+    the mesh holds an ndarray of vertex rows and integer triangles (the
+    generators' meshes): the same rows, rounded to float32 the same way, as
+    np.array(tribuf()[k], dtype=np.float32), without a Python loop over
+    triangles.  None for other containers (the caller uses tribuf())."""
+    V, T = _rows(getattr(mesh, "vertices", None), 4), _rows(getattr(mesh, "triangles", None), 3)
+    if V is None or T is None or V.dtype.kind != "f":
+        return None
+    if T.ndim != 2 or T.shape[1] != 3 or T.dtype.kind not in "iu":
+        return None
+    if len(T) and (T.min() < -len(V) or T.max() >= len(V)):
+        return None
+    return [np.ascontiguousarray(V[T[:, k]], dtype=np.float32) for k in range(3)]
 
 
 def flatten_meshes(meshes):
@@ -32,11 +62,14 @@ def flatten_meshes(meshes):
         ior[j] = np.float32(mat.get("IOR"))
         refl[j] = np.float32(mat.get("R"))
         diss[j] = np.float32(mat.get("dissipation"))
-        tb = mesh.tribuf()
-        v0s.append(np.array(tb[0], dtype=np.float32).reshape(-1, 4))
-        v1s.append(np.array(tb[1], dtype=np.float32).reshape(-1, 4))
-        v2s.append(np.array(tb[2], dtype=np.float32).reshape(-1, 4))
-        ids.append(np.zeros(len(tb[0]), np.int32) + j)
+        tv = _tri_vertices(mesh)
+        if tv is None:                          # general vertex containers: the reference's tribuf() lists
+            tb = mesh.tribuf()
+            tv = [np.array(tb[k], dtype=np.float32).reshape(-1, 4) for k in range(3)]
+        v0s.append(tv[0])
+        v1s.append(tv[1])
+        v2s.append(tv[2])
+        ids.append(np.zeros(len(tv[0]), np.int32) + j)
     v0 = np.ascontiguousarray(np.concatenate(v0s), dtype=np.float32)
     v1 = np.ascontiguousarray(np.concatenate(v1s), dtype=np.float32)
     v2 = np.ascontiguousarray(np.concatenate(v2s), dtype=np.float32)
@@ -129,10 +162,22 @@ class Engine:
         mesh_id, mat_type = i32(mesh_id), i32(mat_type)
         ior, refl, diss = f32(ior), f32(refl), f32(diss)
         M, K = v0.shape[0], mat_type.shape[0]
+        # the same scene as the last upload (a tracer called again on its meshes,
+        # as the reference's examples do): keep the device records, skip the
+        # rebuild (the filter hierarchy is built on the host at every upload)
+        h = hashlib.blake2b(digest_size=16)
+        for a in (v0, v1, v2, mesh_id, mat_type, ior, refl, diss):
+            h.update(np.int64(a.size).tobytes())
+            h.update(a.tobytes())
+        key = h.digest()
+        if key == getattr(self, "_scene_key", None):
+            return
+        self._scene_key = None
         self._c(self.L.lpc_scene_upload(self.h, M, ptr(v0), ptr(v1), ptr(v2), ptr(mesh_id), K,
                                         ptr(mat_type), ptr(ior), ptr(refl), ptr(diss)))
         self.tri_count, self.mesh_count = M, K
         self.mat_type = mat_type
+        self._scene_key = key
 
     def upload_meshes(self, meshes):
         arrs = flatten_meshes(meshes)

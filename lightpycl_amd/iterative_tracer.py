@@ -87,6 +87,9 @@ class CL_Tracer:
         left (iterative_tracer.py:241-391).  Returns ``self.results``."""
         max_ray_len = np.float32(max_ray_len)
         ior_env = np.float32(ior_env)
+        clk = time.perf_counter
+        ph = {}                                 # host-side phases of this call (self.phase_s)
+        t_ph = clk()
         origin = dirs = power = None
         for k, light in enumerate(light_source):                       # :99-113
             if k == 0:
@@ -104,11 +107,15 @@ class CL_Tracer:
         pow_shape0 = power.shape
 
         arrs = flatten_meshes(meshes)                                  # :121-151
-        self.engine.upload_arrays(*arrs)
+        ph["flatten"] = clk() - t_ph
+        t_ph = clk()
+        self.engine.upload_arrays(*arrs)                                # skipped for an unchanged scene
         self.tri_count = np.int32(arrs[0].shape[0])
         self.meshes = meshes
         self.geometry = (arrs[0], arrs[1], arrs[2])
         n = self.engine.set_rays(origin, dirs, power.reshape(-1), max_ray_len, ior_env)
+        ph["upload"] = clk() - t_ph
+        t_ph = clk()
 
         self.results = []
         self.iteration_counts = []
@@ -142,8 +149,12 @@ class CL_Tracer:
                     break
                 if n == 0:
                     break
+            ph["loop"] = clk() - t_ph
+            t_ph = clk()
         finally:
             self.engine.sync()                  # the exported results arrays are complete
+        ph["sync"] = clk() - t_ph
+        self.phase_s = ph
         self.sim_time = time.time() - t0
         return self.results
 

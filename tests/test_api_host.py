@@ -260,3 +260,26 @@ def test_power_decision_bound():
     st.power_nonneg = 0                                                      # negative powers: always exact
     tr._power_decision(st, np.float32(S * 0.5))
     assert tr.engine.fetched == 2
+
+
+def test_flatten_meshes_equals_tribuf_rows():
+    """The drop-in's mesh flattening (iterative_tracer.py:121-151) gathers the
+    triangles' vertex rows at once; bit for bit the rows of tribuf() converted to
+    float32 as the reference does, on every scene builder's meshes."""
+    import numpy as np
+    from lightpycl_amd import engine, scenes
+    for name, build in scenes.BUILDERS.items():
+        sc = build(n=4)
+        v0, v1, v2, mid, *_ = engine.flatten_meshes(sc.meshes)
+        ref = [[], [], []]
+        ids = []
+        for j, m in enumerate(sc.meshes):
+            tb = m.tribuf()
+            for k in range(3):
+                ref[k].append(np.array(tb[k], dtype=np.float32).reshape(-1, 4))
+            ids.append(np.full(len(tb[0]), j, np.int32))
+        for got, want in zip((v0, v1, v2), ref):
+            want = np.concatenate(want)
+            assert got.dtype == want.dtype and got.shape == want.shape, name
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), name
+        assert np.array_equal(mid, np.concatenate(ids)), name
