@@ -1,11 +1,34 @@
 #!/bin/bash
-R=$(pwd); mkdir -p gpurun_out/r4a
-timeout -k 10 60 ./tools/_valu_issue 4096 > gpurun_out/r4a/valu_issue.json 2>&1 || { echo valu failed; cat gpurun_out/r4a/valu_issue.json; exit 1; }
-cat gpurun_out/r4a/valu_issue.json
-( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $R/gpurun_out/r4a/valu_pmc -o pmc --output-format csv -- $R/tools/_valu_issue 4096 > $R/gpurun_out/r4a/valu_pmc.log 2>&1 ) || { echo valu pmc failed; exit 1; }
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4a/pytest.log 2>&1; rc=$?; tail -5 gpurun_out/r4a/pytest.log
-[ $rc -ge 124 ] && exit $rc
-timeout -k 10 300 python -u tools/results_mode.py parabolic 1000000 3 > gpurun_out/r4a/results_mode.json 2>&1 || { tail gpurun_out/r4a/results_mode.json; exit 1; }
-cat gpurun_out/r4a/results_mode.json
-timeout -k 10 600 python -u bench.py > gpurun_out/r4a/bench.json 2> gpurun_out/r4a/bench.err || { tail -20 gpurun_out/r4a/bench.err; exit 1; }
-cut -c1-600 gpurun_out/r4a/bench.json
+# One GPU-box round of evidence (tools/gpu_round.sh [stage]): every GPU step under
+# its own time limit, chained so that a failure or timeout ends the script.
+R=$(pwd); O=gpurun_out/${TAG:-r4}; mkdir -p $O
+run() { local lim=$1 log=$2; shift 2
+  timeout -k 10 $lim "$@" > $O/$log 2>&1; local rc=$?
+  echo "rc=$rc" >> $O/$log
+  if [ $rc -ne 0 ]; then echo "step $log failed rc=$rc"; tail -20 $O/$log; exit $rc; fi; }
+prof() { local lim=$1 dir=$2; shift 2
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 $lim rocprofv3 "$@" ) ; }
+case "${1:-all}" in
+tests)
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+  rc=$?; tail -5 $O/pytest.log; [ $rc -ne 0 ] && exit $rc ;;
+profile)
+  # kernel trace of 3 bench steps, the dense scene's trace, per-iteration statistics
+  prof 300 kt --kernel-trace --stats -d $R/$O/kt -o kt --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-configs > $O/kt.log 2>&1 || { echo kt failed; exit 1; }
+  python tools/kt_timeline.py $O/kt 60 > $O/timeline.txt; python tools/kt_steps.py $O/kt > $O/steps.txt
+  prof 300 ktd --kernel-trace --stats -d $R/$O/ktd -o kt --output-format csv -- python3 $R/tools/cfg_trace.py synthetic_dense 1000000 16 1 > $O/ktd.log 2>&1 || { echo ktd failed; exit 1; }
+  run 300 stats_dense.log python -u tools/trace_stats.py synthetic_dense 200000
+  run 300 stats_synth.log python -u tools/trace_stats.py synthetic 1000000 ;;
+pmc)
+  for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+    tag=$(echo $grp | cut -c1-10 | tr ' ' '_')
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp -d $R/$O/pmc_$tag -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu --no-configs > $R/$O/pmc_$tag.log 2>&1 ) || { echo "pmc $grp failed"; exit 1; }
+  done
+  ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $R/$O/valu_pmc -o pmc --output-format csv -- $R/tools/_valu_issue 4096 > $R/$O/valu_pmc.log 2>&1 ) || { echo valu pmc failed; exit 1; } ;;
+results)
+  run 300 results_mode.json python -u tools/results_mode.py parabolic 1000000 5 ;;
+ab)
+  run 900 ab.log python -u tools/ab.py ${AB_REPS:-3} $AB_CFGS ;;
+bench)
+  run 900 bench.json python -u bench.py ;;
+esac
