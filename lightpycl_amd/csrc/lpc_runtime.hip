@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <thread>
 #include <limits>
 #include <map>
 #include <string>
@@ -1524,14 +1525,44 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     return 0;
 }
 
+// Host passes over the caller's rays (set_rays, bounce_host) split over threads:
+// fn(lo, hi, part) for T contiguous parts, results combined by the caller in
+// part order (so every combine is deterministic).
+static void host_parts(int64_t n, int T, const std::function<void(int64_t, int64_t, int)> &fn)
+{
+    if (T <= 1 || n < (1 << 16)) { fn(0, n, 0); return; }
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back([&, t]() { fn(n * t / T, n * (t + 1) / T, t); });
+    fn(0, n / T, 0);
+    for (auto &x : th) x.join();
+}
+
+static int host_threads()
+{
+    static int t = [] {
+        const char *v = getenv("LPC_HOST_THREADS");
+        int k = v && *v ? atoi(v) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(k, 16));
+    }();
+    return t;
+}
+
 static double host_dmax2(int64_t n, const float *dir4)
 {
+    const int T = host_threads();
+    std::vector<double> part((size_t)T, 0.0);
+    host_parts(n, T, [&](int64_t lo, int64_t hi, int t) {
+        double m = 0.0;
+        for (int64_t i = lo; i < hi; ++i) {
+            const float *d = dir4 + 4 * i;
+            double q = (double)d[0] * d[0] + (double)d[1] * d[1] + (double)d[2] * d[2];
+            if (!(q <= m)) m = q;   // NaN propagates as "large"
+        }
+        part[(size_t)t] = m;
+    });
     double m = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        const float *d = dir4 + 4 * i;
-        double q = (double)d[0] * d[0] + (double)d[1] * d[1] + (double)d[2] * d[2];
-        if (!(q <= m)) m = q;   // NaN propagates as "large"
-    }
+    for (double q : part)
+        if (!(q <= m)) m = q;
     return m;
 }
 
@@ -1551,9 +1582,9 @@ static int upload_rays(lpc_handle *h, Pop &P, int64_t n, const float *origin4, c
     HIPCHK(h, hipMemcpy(P.f(6), pow, (size_t)n * 4, hipMemcpyHostToDevice));
     if (prev_mid) {
         HIPCHK(h, hipMemcpy(P.pmid(), prev_mid, (size_t)n * 4, hipMemcpyHostToDevice));
-    } else {
-        std::vector<int32_t> m2((size_t)n, -2);
-        HIPCHK(h, hipMemcpy(P.pmid(), m2.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    } else {                                    // just emitted (-2, iterative_tracer.py:118), filled on the device
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)P.pmid(), -2, (size_t)n, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     return 0;
 }
@@ -1766,8 +1797,11 @@ static bool bsort_fits(const lpc_handle *h, int64_t n, const float *o4, const fl
                                     return (x | (x << 1)) & 0x5555; };
     auto spread3 = [](uint32_t x) { x &= 0x1f; x = (x | (x << 8)) & 0x100f; x = (x | (x << 4)) & 0x10c3;
                                     return (x | (x << 2)) & 0x1249; };
-    uint32_t mx = 0;
-    for (int64_t i = 0; i < n; ++i) {
+    const int T = host_threads();
+    std::vector<std::vector<uint32_t>> cp((size_t)T, std::vector<uint32_t>((size_t)1 << hb, 0u));
+    host_parts(n, T, [&](int64_t lo, int64_t hi, int t) {
+    std::vector<uint32_t> &c = cp[(size_t)t];
+    for (int64_t i = lo; i < hi; ++i) {
         const float dx = d4[4 * i], dy = d4[4 * i + 1], dz = d4[4 * i + 2];
         const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
         float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
@@ -1783,7 +1817,14 @@ static bool bsort_fits(const lpc_handle *h, int64_t n, const float *o4, const fl
             oc[k] = (uint32_t)fminf(fmaxf((o4[4 * i + k] - h->box_lo[k]) * h->box_scale[k], 0.0f), 31.0f);
         const uint32_t key = ((spread3(oc[0]) | (spread3(oc[1]) << 1) | (spread3(oc[2]) << 2)) << 16) |
                              spread2(du) | (spread2(dv) << 1);
-        mx = std::max(mx, ++c[(key >> (h->init_key_lo + lb)) & ((1u << hb) - 1u)]);
+        ++c[(key >> (h->init_key_lo + lb)) & ((1u << hb) - 1u)];
+    }
+    });
+    uint32_t mx = 0;
+    for (size_t b = 0; b < ((size_t)1 << hb); ++b) {
+        uint32_t v = 0;
+        for (int t = 0; t < T; ++t) v += cp[(size_t)t][b];
+        mx = std::max(mx, v);
     }
     return mx <= (uint32_t)LPC_BS_MAXB;
 }
@@ -1801,13 +1842,19 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
     {   // coherence key bits that can vary over these rays (k_raykey, key mode 0:
         // [class | origin cell 15 | direction 16]): a point source has one origin
         // cell, a collimated beam one direction, and the sort skips the rest
+        const int T = host_threads();
+        std::vector<char> so((size_t)T, 1), sd((size_t)T, 1);
+        host_parts(n, T, [&](int64_t lo, int64_t hi, int t) {
+            bool a = true, b = true;
+            for (int64_t i = std::max<int64_t>(lo, 1); i < hi && (a || b); ++i)
+                for (int k = 0; k < 3; ++k) {
+                    if (origin4[4 * i + k] != origin4[k]) a = false;
+                    if (dir4[4 * i + k] != dir4[k]) b = false;
+                }
+            so[(size_t)t] = a; sd[(size_t)t] = b;
+        });
         bool same_o = true, same_d = true;
-        for (int64_t i = 1; i < n && (same_o || same_d); ++i) {
-            for (int k = 0; k < 3; ++k) {
-                if (origin4[4 * i + k] != origin4[k]) same_o = false;
-                if (dir4[4 * i + k] != dir4[k]) same_d = false;
-            }
-        }
+        for (int t = 0; t < T; ++t) { same_o = same_o && so[(size_t)t]; same_d = same_d && sd[(size_t)t]; }
         h->init_key_lo = 0;
         h->init_key_hi = 31;
         if (same_o) h->init_key_hi = 16;
