@@ -70,7 +70,10 @@ struct QueueArgs {
     uint32_t *err;                    // DevAcc::qerr: set if a shard overflows rcap (never expected; the
                                       //   host then reports the launch as incomplete instead of losing hits)
     uint32_t rcap;
+    int xpiece;                       // k_roots_s: an item's shard = its piece % 8 (else the block's)
+    int claim;                        // k_rootwalk: waves claim items (LPC_Q_HEAD), their XCD's shard first
 };
+#define LPC_Q_HEAD(c) (32 * (1 + (c)) + 16)   // claim head of shard c (k_rootwalk claim mode)
 // root shard of a k_roots* block
 __host__ __device__ inline int q_shard(uint32_t block) { return (int)(block % LPC_Q_CSHARDS); }
 

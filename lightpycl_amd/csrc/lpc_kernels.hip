@@ -807,7 +807,8 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
                                                    const Piece *__restrict__ pieces, int npieces,
                                                    const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
                                                    int S, int pb, int64_t vb, unsigned long long *s_m,
-                                                   uint32_t *s_off, const RootsLds &L);
+                                                   uint32_t *s_off, uint32_t (*s_x)[LPC_Q_CSHARDS],
+                                                   const RootsLds &L);
 
 template <bool HALF>
 __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restrict__ rs, int64_t n,
@@ -817,6 +818,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
 {
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
+    __shared__ uint32_t s_x[LPC_ROOTS_TASKS + 1][LPC_Q_CSHARDS];   // xpiece: per task and shard, then bases
     __shared__ RootsLds L;
     if (nd) n = *nd;
     for (int i = threadIdx.x; i < npieces; i += 256) {
@@ -832,7 +834,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
     __syncthreads();
     const int64_t nvb = ((n + 63) / 64 + pb - 1) / pb;
     for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off, L);
+        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off, s_x, L);
         __syncthreads();                          // s_m / s_off reused by the next virtual block
     }
 }
@@ -842,7 +844,8 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
                                                    const Piece *__restrict__ pieces, int npieces,
                                                    const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
                                                    int S, int pb, int64_t vb, unsigned long long *s_m,
-                                                   uint32_t *s_off, const RootsLds &L)
+                                                   uint32_t *s_off, uint32_t (*s_x)[LPC_Q_CSHARDS],
+                                                   const RootsLds &L)
 {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -901,6 +904,50 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
         if (lane == 0) s_m[t] = m;
     }
     __syncthreads();
+    if (Q.xpiece) {
+        // an item goes to shard (piece % 8): the XCD that walks a shard first keeps
+        // its pieces' records in its own L2 (k_rootwalk claim mode).  Per task and
+        // shard counts by ballots, then one claim atomic per shard and block.
+        for (int t = wv; t < ntask; t += 4) {
+            const uint64_t m = s_m[t];
+            const int cl = (t % S + S * lane) & (LPC_Q_CSHARDS - 1);
+            const bool bit = (m >> lane) & 1ull;
+#pragma unroll
+            for (int x = 0; x < LPC_Q_CSHARDS; ++x) {
+                const uint64_t bm = __builtin_amdgcn_ballot_w64(bit && cl == x);
+                if (lane == 0) s_x[t][x] = (uint32_t)__builtin_popcountll(bm);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < LPC_Q_CSHARDS) {
+            const int x = threadIdx.x;
+            uint32_t tot = 0;
+            for (int t = 0; t < ntask; ++t) { const uint32_t v = s_x[t][x]; s_x[t][x] = tot; tot += v; }
+            s_x[LPC_ROOTS_TASKS][x] = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(x), tot) : 0u;
+        }
+        __syncthreads();
+        for (int t = wv; t < ntask; t += 4) {
+            const uint64_t m = s_m[t];
+            const int p = t % S + S * lane;
+            const int cl = p & (LPC_Q_CSHARDS - 1);
+            const bool bit = (m >> lane) & 1ull;
+            uint32_t rank = 0;
+#pragma unroll
+            for (int x = 0; x < LPC_Q_CSHARDS; ++x) {
+                const uint64_t bm = __builtin_amdgcn_ballot_w64(bit && cl == x);
+                if (cl == x) rank = (uint32_t)__builtin_popcountll(bm & ((1ull << lane) - 1ull));
+            }
+            if (!bit) continue;
+            const int64_t w = vb * pb + t / S;
+            const uint32_t pos = s_x[LPC_ROOTS_TASKS][cl] + s_x[t][cl] + rank;
+            if (pos < Q.rcap)
+                Q.roots[(size_t)cl * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)pieces[p].root,
+                                                            (uint32_t)pieces[p].slot);
+            else
+                atomicOr(Q.err, 2u);
+        }
+        return;
+    }
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
         for (int t = 0; t < ntask; ++t) { s_off[t] = tot; tot += (uint32_t)__builtin_popcountll(s_m[t]); }
@@ -939,6 +986,32 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
 {
     __shared__ WaveLds lds;
     if (nd) n = *nd;
+    if (Q.claim) {
+        // claim mode: a resident grid; each wave claims items one at a time from
+        // the shard of its XCD (block b runs on XCD b % 8), then from the others
+        // (a returning atomic per item: items run for microseconds, a claim ~1 us)
+        const int x0 = (int)(blockIdx.x % LPC_Q_CSHARDS);
+        for (int k = 0; k < LPC_Q_CSHARDS; ++k) {
+            const int c = (x0 + k) & (LPC_Q_CSHARDS - 1);
+            const uint32_t cnt = min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
+            uint32_t *head = Q.ctl + LPC_Q_HEAD(c);
+            for (;;) {
+                if (__hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cnt) break;
+                uint32_t i = 0;
+                if ((threadIdx.x & 63) == 0) i = atomicAdd(head, 1u);
+                i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+                if (i >= cnt) break;
+                const uint64_t it = Q.roots[(size_t)c * Q.rcap + i];
+                Piece P;
+                memset(&P, 0, sizeof(P));
+                P.root = (int32_t)q_node(it);
+                P.slot = (int32_t)q_slot(it);
+                trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot,
+                                                        eps, max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
+            }
+        }
+        return;
+    }
     uint32_t pre[LPC_Q_CSHARDS + 1];
     pre[0] = 0;
 #pragma unroll

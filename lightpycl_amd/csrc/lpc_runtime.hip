@@ -166,6 +166,8 @@ struct lpc_handle {
     bool init_bsort = false;                        // their sort may be the counting sort (bsort_fits)
     int queue = 2;                                  // LPC_QUEUE: 2 root items + k_rootwalk (default), 0 k_intersect
     int64_t q_walk_blocks = 16384;                  // k_rootwalk grid in 4-wave units (grid-stride)
+    int xcd_claim = 0;                              // LPC_XCD_CLAIM: items sharded by piece % 8, walked by
+                                                    //   claims from the own XCD's shard first (resident grid)
     int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
     DBuf w_qroots;                                  // root items
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
@@ -906,8 +908,12 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     const int64_t rs_vblocks = !ds ? rs_blocks : (((ds->bound + 63) / 64) + rs_pb - 1) / rs_pb;
     // per shard: at most its blocks' packets x pieces items (k_roots* flag an
     // overflow through Q.err instead of dropping items silently)
-    const int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
-                                  ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+    int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
+                            ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+    const bool xpiece = h->xcd_claim && roots_s;
+    if (xpiece)                         // a shard takes every packet's items of its pieces (piece % 8)
+        rcap = std::max<int64_t>(rcap, rs_vblocks * rs_pb *
+                                           (int64_t)((pt->npieces + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS));
     if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "root items: too many per shard");
     RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
     QueueArgs Q;
@@ -915,6 +921,8 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     Q.ctl = (uint32_t *)h->d_misc.p;
     Q.err = (uint32_t *)((char *)h->d_acc.p + offsetof(DevAcc, qerr));
     Q.rcap = (uint32_t)rcap;
+    Q.xpiece = xpiece ? 1 : 0;
+    Q.claim = h->xcd_claim ? 1 : 0;
     if (h->host_prof)
         fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d groups %d S %d pb %d blocks %lld rcap %lld\n",
                 (long long)n, (long long)npk, (int)pt->npieces, (int)pt->ngroups, rs_S, rs_pb, (long long)rs_blocks,
@@ -940,7 +948,9 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     SpillArgs SP;
     RETIF(spill_setup(h, n, &SP));
     // the grid in waves (LPC_Q_WALK_BLOCKS x 4), single-wave blocks
-    const unsigned grid = (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4);
+    // (claim mode: as many single-wave blocks as the chip holds at once)
+    const unsigned grid = h->xcd_claim ? (unsigned)std::max(1, h->cus * 4 * LPC_WALK_MINB)
+                                       : (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4);
     // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -1354,6 +1364,7 @@ int lpc_open(int device, lpc_handle **out)
     h->queue = env_int("LPC_QUEUE", h->queue) == 0 ? 0 : 2;
     h->traced = env_int("LPC_TRACED", h->traced) != 0;
     h->q_walk_blocks = std::max<int64_t>(1, env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks));
+    h->xcd_claim = (int)env_int("LPC_XCD_CLAIM", h->xcd_claim);
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));

@@ -106,6 +106,9 @@ _POLICIES = [
     dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
     dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"),
     dict(LPC_LARGE_N="1000"), dict(LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3"),
+    # items sharded by piece and claimed XCD-first by a resident grid; small budgets
+    dict(LPC_XCD_CLAIM="1"), dict(LPC_XCD_CLAIM="1", LPC_Q_TARGET="1000000"),
+    dict(LPC_XCD_CLAIM="1", LPC_BUDGET="3"), dict(LPC_BUDGET_SMALL="0"), dict(LPC_BUDGET_SMALL="5"),
     # the k_intersect alternative and its knobs
     dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
     dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
