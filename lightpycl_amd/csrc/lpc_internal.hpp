@@ -200,6 +200,8 @@ struct StageArgs {
     double *tmp;                      // [ntiles][LPC_MP_MAX] measured power per tile and measure mesh
     unsigned long long *gsum;         // per group of LPC_ST_GROUP tiles: counts (21 bits each), zero before
     uint32_t *tmask;                  // the walk's written-slot masks (only those slots are read), or NULL
+    uint32_t *tbox;                   // [ntiles][6] box of the tile's kept children origins (ord_f32 min xyz,
+                                      //   max xyz), or NULL: the next population's coherence key box
 };
 #define LPC_ST_GROUP 256                  // tiles per count group (k_stage_move prefixes: groups, then tiles)
 __host__ __device__ inline unsigned long long gsum_pack(uint32_t r, uint32_t t, uint32_t m)
@@ -233,6 +235,8 @@ struct MoveArgs {
     int par;                          // this iteration's parity in ctl (k_stage_move<true>: ntiles,
                                       //   ngroups and m_base from ctl[par] as well)
     double thr;                       // trace_run's power threshold (-inf: none)
+    long long nmax;                   // a device-sized next iteration holds at most this many rays: more
+                                      //   kept children -> its size 0 (the host re-runs it host-sized)
     double dcap2;                     // Dcap^2 (1 - 1e-6), check_dcap's bound
     // an iteration in several chunks (population > one chunk): each chunk's launch
     // places its rows after the earlier chunks' -- reflected into popR, refracted
@@ -245,7 +249,19 @@ struct MoveArgs {
     const unsigned long long *cbase_in;   // [3] R, T, M bases (first chunk: 0, 0, m_base)
     unsigned long long *cbase_out;
     int first, last;
+    const uint32_t *tbox;             // StageArgs::tbox (NULL: no box)
+    uint32_t *pbox;                   // [6] the next population's origin box (block 0; chunks combine)
 };
+// Order-preserving float bits (min / max of the uint = of the float).
+__host__ __device__ inline uint32_t ord_f32(float f)
+{
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float ord_f32_inv(uint32_t u)
+{
+    return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
 
 struct PostprocAosArgs {
     int64_t n;

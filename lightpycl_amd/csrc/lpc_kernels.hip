@@ -1232,9 +1232,20 @@ static __device__ __forceinline__ uint32_t raykey_ray(const RaysIn &R, int64_t i
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
                                                 float sx, float sy, float sz, uint32_t *__restrict__ keys,
                                                 int32_t *__restrict__ vals, float4 *__restrict__ aos,
-                                                SlotInit SI)
+                                                SlotInit SI, const uint32_t *__restrict__ pbox)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pbox) {         // the population's own origin box (the previous k_stage_move), per axis
+        float *b0[3] = {&bx0, &by0, &bz0}, *sc[3] = {&sx, &sy, &sz};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t a = pbox[k], b = pbox[3 + k];
+            if (a > b) continue;                 // empty: the scene box
+            const float lo = ord_f32_inv(a), ext = ord_f32_inv(b) - lo;
+            *b0[k] = lo;
+            *sc[k] = (ext > 0.0f && isfinite(ext)) ? 32.0f / ext : 1.0f;
+        }
+    }
     if (SI.skey || SI.misc || SI.acc) slot_init_ray(SI, n, i);     // k_slot_init folded in (one launch fewer)
     if (i >= n) return;
     keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
@@ -1845,6 +1856,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     __shared__ int32_t s_w[3][LPC_ST_TILE / 64];
     __shared__ double s_pow[LPC_ST_TILE / 64];
     __shared__ float s_dm[LPC_ST_TILE / 64];
+    __shared__ uint32_t s_bx[LPC_ST_TILE / 64][6];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     // the shading inputs as a local (a device-sized launch sets its n; writing the
     // kernel argument itself would put the whole argument block in scratch)
@@ -1901,6 +1913,15 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
     }
     pk = wave_sum(pk);
     dm = wave_max(dm);
+    if (A.tbox) {       // the kept children's origins (= dest): the next population's key box
+        const bool kb = (fR || fT) && isfinite(dest.x) && isfinite(dest.y) && isfinite(dest.z);
+        const float v[3] = {dest.x, dest.y, dest.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float lo = wave_red(kb ? v[k] : INFINITY, 0), hi = wave_red(kb ? v[k] : -INFINITY, 1);
+            if (lane == 0) { s_bx[wv][k] = ord_f32(lo); s_bx[wv][3 + k] = ord_f32(hi); }
+        }
+    }
     // measured power per measure mesh (fixed order: waves, then tiles in k_stage_move)
     for (int m = 0; m < A.nmp; ++m) {
         const double v = wave_sum((fM && po.hit_mesh == A.mpm[m]) ? (double)s.pow : 0.0);
@@ -1943,6 +1964,18 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
         A.tcnt[tile] = cR | (cT << 9) | (cM << 18);
         A.tpow[tile] = tp;
         A.tdm[tile] = __float_as_uint(td);
+        if (A.tbox) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                uint32_t lo = s_bx[0][k], hi = s_bx[0][3 + k];
+                for (int w = 1; w < LPC_ST_TILE / 64; ++w) {
+                    lo = min(lo, s_bx[w][k]);
+                    hi = max(hi, s_bx[w][3 + k]);
+                }
+                A.tbox[tile * 6 + k] = lo;
+                A.tbox[tile * 6 + 3 + k] = hi;
+            }
+        }
         if (cR | cT | cM) atomicAdd(&A.gsum[tile / LPC_ST_GROUP], gsum_pack(cR, cT, cM));
     }
     };
@@ -1965,6 +1998,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
     __shared__ double s_p[LPC_ST_TILE];
     __shared__ float s_d[LPC_ST_TILE];
     __shared__ double s_m[LPC_MP_MAX][LPC_ST_TILE];
+    __shared__ uint32_t s_b[6][LPC_ST_TILE / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     // device-sized launch (DS): the population size and measured-record length
     // the previous iteration left in A.ctl; grid-stride over the tiles (tile 0's
@@ -2054,6 +2088,31 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
             }
         }
         __syncthreads();
+        if (A.tbox && A.pbox) {     // the next population's origin box over the tiles (order-free)
+            uint32_t b[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+            for (int64_t j = t; j < ntiles; j += LPC_ST_TILE)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    b[k] = min(b[k], A.tbox[j * 6 + k]);
+                    b[3 + k] = max(b[3 + k], A.tbox[j * 6 + 3 + k]);
+                }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                uint32_t v = b[k];
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+                    v = k < 3 ? min(v, u) : max(v, u);
+                }
+                if (lane == 0) s_b[k][wv] = v;
+            }
+            __syncthreads();
+            if (t < 6) {
+                uint32_t v = s_b[t][0];
+                for (int w = 1; w < LPC_ST_TILE / 64; ++w) v = t < 3 ? min(v, s_b[t][w]) : max(v, s_b[t][w]);
+                if (chunked && !A.first) v = t < 3 ? min(v, A.pbox[t]) : max(v, A.pbox[t]);
+                A.pbox[t] = v;
+            }
+        }
         if (t == 0) {
             // the counters in registers (a DevAcc local indexed by m would live in
             // scratch, on the iteration's critical path)
@@ -2101,7 +2160,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
                 // kept direction exceeds the filter records' Dcap (the host rebuilds)
                 const unsigned long long kept = a.nR + a.nT;
                 const bool dc = !((double)s_d[0] <= A.dcap2);
-                const bool stop = a.pow_next < A.thr || kept == 0 || dc;
+                const bool stop = a.pow_next < A.thr || kept == 0 || dc || (long long)kept > A.nmax;
                 A.ctl->n[A.par ^ 1] = stop ? 0 : (long long)kept;
                 A.ctl->m[A.par ^ 1] = a.m_total;
                 A.ctl->dm2[A.par ^ 1] = a.dmax2_bits;

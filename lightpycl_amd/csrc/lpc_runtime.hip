@@ -201,6 +201,9 @@ struct lpc_handle {
     bool mp_valid = false;                          // mp_last = the trace's measured power per measure mesh
     DBuf d_mrun;                                    // its running sums on the device (k_stage_move)
     DBuf d_cbase;                                   // chunked traced iterations: running row bases (ping-pong)
+    bool pop_box = true;                            // LPC_POPBOX: re-sorted chained populations keyed in their own box
+    DBuf w_tbox, d_pbox;                            // per-tile boxes (k_shade_stage), the population's box (k_stage_move)
+    bool pbox_ok = false;                           // d_pbox holds the current population's origin box
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;
@@ -656,6 +659,15 @@ static int64_t chunk_rays(const lpc_handle *h)
     return std::max<int64_t>((int64_t)1 << 20, std::min<int64_t>((int64_t)128 << 20, c));
 }
 
+// The largest population a device-sized iteration may hold: below the re-sort
+// size (a device-sized iteration keeps its parents' order), one chunk, the
+// root-item encoding's packet bound.  k_stage_move sizes the next iteration 0
+// (it runs empty) when more children are kept, and the host re-runs it.
+static int64_t ds_cap(const lpc_handle *h)
+{
+    return std::max<int64_t>(0, std::min<int64_t>({h->resort_min - 1, chunk_rays(h), (int64_t)LPC_Q_MAX_PACKETS * 64}));
+}
+
 // Workspace for a chunk of `n` rays.
 static int ensure_ws(lpc_handle *h, int64_t n)
 {
@@ -677,6 +689,8 @@ static int ensure_ws(lpc_handle *h, int64_t n)
         RETIF(dalloc(h, h->w_stage, (size_t)C * 16));
         RETIF(dalloc(h, h->w_aos, (size_t)C * 32));
         RETIF(dalloc(h, h->w_tm, (size_t)C * 4));
+        RETIF(dalloc(h, h->w_tbox, (size_t)((C + LPC_ST_TILE - 1) / LPC_ST_TILE + 1) * 6 * 4));
+        RETIF(dalloc(h, h->d_pbox, 6 * 4));
         HIPCHK(h, hipMemsetAsync(h->w_tm.p, 0, h->w_tm.bytes, h->stream));
         RETIF(dalloc(h, h->w_sort, (size_t)C * 16));    // keys in/out, values in/out
         RETIF(dalloc(h, h->w_bhist, ((size_t)LPC_BS_ND * ((C + LPC_BS_RPB - 1) / LPC_BS_RPB) + 2 * LPC_BS_ND + 8) * 4));
@@ -1083,9 +1097,12 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                    (const uint8_t *)kout,
                                    (const int32_t *)vin, lb, (const uint32_t *)bst, vout);
         } else {
+            // a re-sorted chained population: the key's origin cells span its own
+            // box (k_stage_move of the iteration that made it), not the scene's
+            const uint32_t *pbox = (traced && chained_pop && h->pbox_ok) ? (const uint32_t *)h->d_pbox.p : nullptr;
             hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                                h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
-                               (float4 *)h->w_aos.p, SIk);
+                               (float4 *)h->w_aos.p, SIk, pbox);
             size_t tb = h->sort_tmp_bytes;
             if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
                 HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
@@ -1365,6 +1382,7 @@ int lpc_open(int device, lpc_handle **out)
     h->traced = env_int("LPC_TRACED", h->traced) != 0;
     h->q_walk_blocks = std::max<int64_t>(1, env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks));
     h->xcd_claim = (int)env_int("LPC_XCD_CLAIM", h->xcd_claim);
+    h->pop_box = env_int("LPC_POPBOX", h->pop_box) != 0;
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
@@ -1411,7 +1429,7 @@ int lpc_close(lpc_handle *h)
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->w_bhist, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
                     &h->d_acc, &h->d_tmp, &h->d_stats, &h->d_misc, &h->d_wrec, &h->w_spill, &h->w_qroots,
-                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl, &h->d_cbase};
+                    &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl, &h->d_cbase, &h->w_tbox, &h->d_pbox};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
     h->acc_host = nullptr;
@@ -1896,6 +1914,7 @@ int lpc_trace_reset(lpc_handle *h)
     h->pop_traced = false;
     h->pop_emitted = true;
     h->pop_dmax2 = h->init_dmax2;
+    h->pbox_ok = false;
     h->m_total = 0;                             // measured record emptied (the first iteration resets the counters)
     h->m_inflight = 0;
     return 0;
@@ -2071,7 +2090,7 @@ struct Pending {
     bool empty = false;         // nothing to do (n_in 0, host-sized)
     int64_t n_bound = 0;        // device-sized: population bound
     // host state before its enqueue (undo of a discarded speculative iteration)
-    bool was_init = false, was_traced = false, was_emitted = false;
+    bool was_init = false, was_traced = false, was_emitted = false, was_pbox = false;
 };
 
 // A results export (lpc_trace_iterate_export): the caller's host block and
@@ -2141,6 +2160,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
 {
     *P = Pending();
     P->was_init = h->pop_init; P->was_traced = h->pop_traced; P->was_emitted = h->pop_emitted;
+    P->was_pbox = h->pbox_ok;
     const int64_t N = ds ? ds->bound : h->n_cur;
     P->n_in = ds ? -1 : N;
     P->ds = ds != nullptr;
@@ -2188,6 +2208,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     const int64_t ntc = (int64_t)((Cs + LPC_ST_TILE - 1) / LPC_ST_TILE);   // staging tile arrays' stride
     IterCtl *ctl = (IterCtl *)h->d_ctl.p;
     const int par = h->ctl_par;
+    bool box_made = false;                  // the fused chunks wrote the children's box (d_pbox)
     for (int64_t base = 0; base < N; base += C) {
         const int64_t nc = std::min(C, N - base);
         RaysIn in = (h->pop_init ? h->I : h->A).in(base);
@@ -2237,6 +2258,9 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
             unsigned long long *gs = (unsigned long long *)h->w_gsum.p;
             G.gsum = gs + (size_t)h->gpar * (size_t)h->gcap;
             G.tmask = h->tm_cur;            // set by this chunk's run_intersect
+            // the children's origin box when they may be re-sorted (population >= LPC_RESORT_MIN)
+            const bool want_box = h->pop_box && !ds && 2 * N >= h->resort_min;
+            G.tbox = want_box ? (uint32_t *)h->w_tbox.p : nullptr;
 
             if (ds) LPC_KU_LAUNCH2(h, k_shade_stage, true, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
             else LPC_KU_LAUNCH2(h, k_shade_stage, false, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
@@ -2261,7 +2285,11 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
             M.ctl = ctl;
             M.par = par;
             M.thr = h->ds_thr;
+            M.nmax = ds_cap(h);
             M.dcap2 = h->dcap * h->dcap * (1.0 - 1e-6);
+            M.tbox = G.tbox;
+            M.pbox = G.tbox ? (uint32_t *)h->d_pbox.p : nullptr;
+            box_made = G.tbox != nullptr;
             M.popT = nullptr; M.capT = 0; M.cbase_in = nullptr; M.cbase_out = nullptr;
             M.first = 1; M.last = 1;
             if (C < N) {                        // chunk base / C of several
@@ -2318,6 +2346,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     }
     h->ctl_par ^= 1;                    // the next iteration reads the entry this one's k_stage_move writes
     // the children are the next population (their counts come with iter_collect)
+    h->pbox_ok = box_made;
     std::swap(h->A, h->B);
     h->pop_init = false;
     h->pop_traced = traced;
@@ -2399,6 +2428,7 @@ static void iter_discard(lpc_handle *h, const Pending &P)
     h->pop_init = P.was_init;
     h->pop_traced = P.was_traced;
     h->pop_emitted = P.was_emitted;
+    h->pbox_ok = P.was_pbox;
 }
 
 int lpc_trace_iterate(lpc_handle *h, float *out_origin4, float *out_dest4, float *out_pow,
@@ -2509,13 +2539,16 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         // known: host-sized, or the kept children of iteration i - 1)
         if (hist_ok && i + 1 < max_iter && (int64_t)h->hist_r.size() > i + 1 && cur.fused && !cur.empty &&
             cur.n_in > 0) {
-            const int64_t bound = 2 * cur.n_in;
-            if (ds_ok(h, bound)) {
+            // its bound: all children of the current population, capped at
+            // ds_cap (more kept children: it runs empty and is re-run host-sized)
+            const int64_t bound = std::min<int64_t>(2 * cur.n_in, ds_cap(h));
+            const int64_t pred_n = (int64_t)llround(h->hist_r[(size_t)i + 1] * (double)n0);
+            if (pred_n <= bound && ds_ok(h, bound)) {
                 IterCtl *ctl = (IterCtl *)h->d_ctl.p;
                 DevSize D;
                 D.nd = &ctl->n[h->ctl_par];
                 D.dm2 = &ctl->dm2[h->ctl_par];
-                D.pred = std::max<int64_t>(1, std::min((int64_t)llround(h->hist_r[(size_t)i + 1] * (double)n0), bound));
+                D.pred = std::max<int64_t>(1, std::min(pred_n, bound));
                 D.bound = bound;
                 if ((rc = iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, &D, &nxt))) break;
                 have_nxt = true;
@@ -2545,6 +2578,11 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
                 iter_discard(h, nxt);
                 have_nxt = false;
                 if (h->xchg) RETIF(restore_mrun(h));
+            } else if (S.n_reflect + S.n_refract > nxt.n_bound) {
+                // more children than it was sized for: it ran empty on the device;
+                // the next pass of the loop runs the iteration host-sized
+                iter_discard(h, nxt);
+                have_nxt = false;
             } else {
                 nxt.n_in = S.n_reflect + S.n_refract;           // this rank's population
                 cur = nxt;

@@ -2,7 +2,8 @@
 configurations alternated round-robin `reps` times): prints one JSON line per
 run and a summary (median ms/step per configuration).
 
-    python tools/ab.py reps 'NAME:VAR=V,VAR=V' 'NAME:...' ...   ('base:' = defaults)
+    python tools/ab.py reps 'NAME:VAR=V,VAR=V' 'NAME:...' ...   ('base:' = defaults;
+    ARGS=... passes extra bench.py arguments, e.g. 'noprof:ARGS=--no-prof'; AB_STEPS, default 300)
 """
 import json
 import os
@@ -20,9 +21,11 @@ for a in sys.argv[2:]:
 res = {n: [] for n, _ in cfgs}
 for r in range(reps):
     for name, env in cfgs:
-        e = dict(os.environ, **env)
-        out = subprocess.run([sys.executable, "bench.py", "--no-cpu", "--no-configs", "--steps", "30", "--warmup", "3"],
-                             cwd=root, env=e, capture_output=True, text=True, timeout=300)
+        e = dict(os.environ, **{k: v for k, v in env.items() if k != "ARGS"})
+        extra = env.get("ARGS", "").split()
+        steps = os.environ.get("AB_STEPS", "300")
+        out = subprocess.run([sys.executable, "bench.py", "--no-cpu", "--no-configs", "--steps", steps, "--warmup", "5"]
+                             + extra, cwd=root, env=e, capture_output=True, text=True, timeout=300)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if out.returncode != 0 or not line:
             print(json.dumps(dict(cfg=name, rc=out.returncode, err=out.stderr[-2000:])), flush=True)
