@@ -1229,10 +1229,37 @@ static __device__ __forceinline__ uint32_t raykey_ray(const RaysIn &R, int64_t i
     return (okey << 16) | dkey;
 }
 
+// Key with ob origin bits per axis and db direction bits per octahedral axis
+// (3 ob + 2 db <= 32), Morton-interleaved, origin cells above direction: the
+// re-sorted chained populations' key in their own box (LPC_KEY_OBITS).
+static __device__ __forceinline__ uint32_t raykey_ray_bits(const RaysIn &R, int64_t i, float bx0, float by0,
+                                                           float bz0, float sx, float sy, float sz, int ob, int db)
+{
+    const float dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
+    const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
+    float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
+    if (dz < 0.0f) {
+        const float tx = (1.0f - fabsf(py)) * (px >= 0.0f ? 1.0f : -1.0f);
+        const float ty = (1.0f - fabsf(px)) * (py >= 0.0f ? 1.0f : -1.0f);
+        px = tx; py = ty;
+    }
+    const float dn = (float)(1 << db), on = (float)(1 << ob), sc = on / 32.0f;
+    const uint32_t du = (uint32_t)fminf(fmaxf((px * 0.5f + 0.5f) * dn, 0.0f), dn - 1.0f);
+    const uint32_t dv = (uint32_t)fminf(fmaxf((py * 0.5f + 0.5f) * dn, 0.0f), dn - 1.0f);
+    const uint32_t o[3] = {(uint32_t)fminf(fmaxf((R.ox[i] - bx0) * sx * sc, 0.0f), on - 1.0f),
+                           (uint32_t)fminf(fmaxf((R.oy[i] - by0) * sy * sc, 0.0f), on - 1.0f),
+                           (uint32_t)fminf(fmaxf((R.oz[i] - bz0) * sz * sc, 0.0f), on - 1.0f)};
+    uint32_t okey = 0, dkey = 0;
+    for (int b = 0; b < ob; ++b)
+        for (int k = 0; k < 3; ++k) okey |= ((o[k] >> b) & 1u) << (3 * b + k);
+    for (int b = 0; b < db; ++b) dkey |= (((du >> b) & 1u) << (2 * b)) | (((dv >> b) & 1u) << (2 * b + 1));
+    return (okey << (2 * db)) | dkey;
+}
+
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
                                                 float sx, float sy, float sz, uint32_t *__restrict__ keys,
                                                 int32_t *__restrict__ vals, float4 *__restrict__ aos,
-                                                SlotInit SI, const uint32_t *__restrict__ pbox)
+                                                SlotInit SI, const uint32_t *__restrict__ pbox, int obits)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (pbox) {         // the population's own origin box (the previous k_stage_move), per axis
@@ -1248,7 +1275,10 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     }
     if (SI.skey || SI.misc || SI.acc) slot_init_ray(SI, n, i);     // k_slot_init folded in (one launch fewer)
     if (i >= n) return;
-    keys[i] = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
+    uint32_t key = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
+    if (obits != 5)                             // another origin / direction split (pbox populations)
+        key = raykey_ray_bits(R, i, bx0, by0, bz0, sx, sy, sz, obits, (32 - 3 * obits) / 2);
+    keys[i] = key;
     vals[i] = (int32_t)i;
 }
 

@@ -204,6 +204,7 @@ struct lpc_handle {
     bool pop_box = true;                            // LPC_POPBOX: re-sorted chained populations keyed in their own box
     DBuf w_tbox, d_pbox;                            // per-tile boxes (k_shade_stage), the population's box (k_stage_move)
     bool pbox_ok = false;                           // d_pbox holds the current population's origin box
+    int key_obits = 5;                              // LPC_KEY_OBITS: origin bits per axis of that key (4..8)
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;
@@ -1102,7 +1103,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             const uint32_t *pbox = (traced && chained_pop && h->pbox_ok) ? (const uint32_t *)h->d_pbox.p : nullptr;
             hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                                h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
-                               (float4 *)h->w_aos.p, SIk, pbox);
+                               (float4 *)h->w_aos.p, SIk, pbox, pbox ? h->key_obits : 5);
             size_t tb = h->sort_tmp_bytes;
             if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
                 HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
@@ -1383,6 +1384,7 @@ int lpc_open(int device, lpc_handle **out)
     h->q_walk_blocks = std::max<int64_t>(1, env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks));
     h->xcd_claim = (int)env_int("LPC_XCD_CLAIM", h->xcd_claim);
     h->pop_box = env_int("LPC_POPBOX", h->pop_box) != 0;
+    h->key_obits = (int)std::min<int64_t>(8, std::max<int64_t>(4, env_int("LPC_KEY_OBITS", h->key_obits)));
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));

@@ -607,3 +607,43 @@ def test_written_slot_masks_equal_full_reads(monkeypatch, name, n):
     assert a[0][0] == a[0][1] == a[0][2]
     for x, y in zip(a[1:], b[1:]):
         np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+
+
+@pytest.mark.parametrize("env", [dict(LPC_POPBOX="0"), dict(LPC_KEY_OBITS="7"), dict(LPC_KEY_OBITS="4"),
+                                 dict(LPC_XCD_CLAIM="1")])
+def test_resorted_populations_keys(monkeypatch, env):
+    """Re-sorted chained populations (LPC_RESORT_MIN lowered so that every
+    iteration of the dense synthetic scene is re-sorted): the coherence key in the
+    population's own origin box (default), in the scene box, or with another
+    origin/direction split changes only the order of the work -- identical
+    per-iteration counts, the measured rays as a set, per-mesh power to float64
+    summation order."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.synthetic_dense(n=20000, seed=31, iterations=8)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+    out = []
+    for e_env in (dict(), env):
+        for k in ("LPC_POPBOX", "LPC_KEY_OBITS", "LPC_XCD_CLAIM"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in e_env.items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("LPC_RESORT_MIN", "4096")
+        e = Engine(0)
+        try:
+            e.upload_meshes(sc.meshes)
+            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+            stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+            pos, p, mm = e.fetch_measured()
+            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm))
+        finally:
+            e.close()
+    a, b = out
+    assert len(a[0]) >= 4
+    assert a[0] == b[0] and a[1] == b[1]
+    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)
+
+    def rows(pos, p, mm):
+        r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
+        return r[np.lexsort(r.T[::-1])]
+    np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
