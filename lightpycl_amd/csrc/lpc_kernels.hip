@@ -1233,7 +1233,8 @@ static __device__ __forceinline__ uint32_t raykey_ray(const RaysIn &R, int64_t i
 // (3 ob + 2 db <= 32), Morton-interleaved, origin cells above direction: the
 // re-sorted chained populations' key in their own box (LPC_KEY_OBITS).
 static __device__ __forceinline__ uint32_t raykey_ray_bits(const RaysIn &R, int64_t i, float bx0, float by0,
-                                                           float bz0, float sx, float sy, float sz, int ob, int db)
+                                                           float bz0, float sx, float sy, float sz, int ob, int db,
+                                                           int mode)
 {
     const float dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
     const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
@@ -1249,17 +1250,30 @@ static __device__ __forceinline__ uint32_t raykey_ray_bits(const RaysIn &R, int6
     const uint32_t o[3] = {(uint32_t)fminf(fmaxf((R.ox[i] - bx0) * sx * sc, 0.0f), on - 1.0f),
                            (uint32_t)fminf(fmaxf((R.oy[i] - by0) * sy * sc, 0.0f), on - 1.0f),
                            (uint32_t)fminf(fmaxf((R.oz[i] - bz0) * sz * sc, 0.0f), on - 1.0f)};
+    if (mode == 1) {    // 5-D Morton: origin and direction bits interleaved from the top
+        uint32_t key = 0;
+        int pos = 3 * ob + 2 * db;
+        const int top = ob > db ? ob : db;
+        for (int b = top - 1; b >= 0; --b) {
+            if (b < ob)
+                for (int k = 0; k < 3; ++k) key |= ((o[k] >> b) & 1u) << --pos;
+            if (b < db) { key |= ((du >> b) & 1u) << --pos; key |= ((dv >> b) & 1u) << --pos; }
+        }
+        return key;
+    }
     uint32_t okey = 0, dkey = 0;
     for (int b = 0; b < ob; ++b)
         for (int k = 0; k < 3; ++k) okey |= ((o[k] >> b) & 1u) << (3 * b + k);
     for (int b = 0; b < db; ++b) dkey |= (((du >> b) & 1u) << (2 * b)) | (((dv >> b) & 1u) << (2 * b + 1));
+    if (mode == 2) return (dkey << (3 * ob)) | okey;             // direction-major
     return (okey << (2 * db)) | dkey;
 }
 
 __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, float by0, float bz0,
                                                 float sx, float sy, float sz, uint32_t *__restrict__ keys,
                                                 int32_t *__restrict__ vals, float4 *__restrict__ aos,
-                                                SlotInit SI, const uint32_t *__restrict__ pbox, int obits)
+                                                SlotInit SI, const uint32_t *__restrict__ pbox, int obits,
+                                                int kmode)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (pbox) {         // the population's own origin box (the previous k_stage_move), per axis
@@ -1276,8 +1290,8 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     if (SI.skey || SI.misc || SI.acc) slot_init_ray(SI, n, i);     // k_slot_init folded in (one launch fewer)
     if (i >= n) return;
     uint32_t key = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, aos);
-    if (obits != 5)                             // another origin / direction split (pbox populations)
-        key = raykey_ray_bits(R, i, bx0, by0, bz0, sx, sy, sz, obits, (32 - 3 * obits) / 2);
+    if (obits != 5 || kmode != 0)               // another origin / direction split (pbox populations)
+        key = raykey_ray_bits(R, i, bx0, by0, bz0, sx, sy, sz, obits, (32 - 3 * obits) / 2, kmode);
     keys[i] = key;
     vals[i] = (int32_t)i;
 }

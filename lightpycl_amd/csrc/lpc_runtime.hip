@@ -205,6 +205,7 @@ struct lpc_handle {
     DBuf w_tbox, d_pbox;                            // per-tile boxes (k_shade_stage), the population's box (k_stage_move)
     bool pbox_ok = false;                           // d_pbox holds the current population's origin box
     int key_obits = 5;                              // LPC_KEY_OBITS: origin bits per axis of that key (4..8)
+    int key_mode = 0;                               // LPC_KEY_MODE: 0 origin-major, 1 5-D Morton, 2 direction-major
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;
@@ -1103,7 +1104,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             const uint32_t *pbox = (traced && chained_pop && h->pbox_ok) ? (const uint32_t *)h->d_pbox.p : nullptr;
             hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                                h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
-                               (float4 *)h->w_aos.p, SIk, pbox, pbox ? h->key_obits : 5);
+                               (float4 *)h->w_aos.p, SIk, pbox, pbox ? h->key_obits : 5, pbox ? h->key_mode : 0);
             size_t tb = h->sort_tmp_bytes;
             if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
                 HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
@@ -1385,6 +1386,7 @@ int lpc_open(int device, lpc_handle **out)
     h->xcd_claim = (int)env_int("LPC_XCD_CLAIM", h->xcd_claim);
     h->pop_box = env_int("LPC_POPBOX", h->pop_box) != 0;
     h->key_obits = (int)std::min<int64_t>(8, std::max<int64_t>(4, env_int("LPC_KEY_OBITS", h->key_obits)));
+    h->key_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_KEY_MODE", h->key_mode)));
     {
         const int dbg = (int)env_int("LPC_DBG", 0);
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));

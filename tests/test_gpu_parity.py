@@ -610,7 +610,8 @@ def test_written_slot_masks_equal_full_reads(monkeypatch, name, n):
 
 
 @pytest.mark.parametrize("env", [dict(LPC_POPBOX="0"), dict(LPC_KEY_OBITS="7"), dict(LPC_KEY_OBITS="4"),
-                                 dict(LPC_XCD_CLAIM="1")])
+                                 dict(LPC_XCD_CLAIM="1"), dict(LPC_KEY_MODE="1", LPC_KEY_OBITS="6"),
+                                 dict(LPC_KEY_MODE="2")])
 def test_resorted_populations_keys(monkeypatch, env):
     """Re-sorted chained populations (LPC_RESORT_MIN lowered so that every
     iteration of the dense synthetic scene is re-sorted): the coherence key in the
@@ -624,7 +625,7 @@ def test_resorted_populations_keys(monkeypatch, env):
     thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
     out = []
     for e_env in (dict(), env):
-        for k in ("LPC_POPBOX", "LPC_KEY_OBITS", "LPC_XCD_CLAIM"):
+        for k in ("LPC_POPBOX", "LPC_KEY_OBITS", "LPC_XCD_CLAIM", "LPC_KEY_MODE"):
             monkeypatch.delenv(k, raising=False)
         for k, v in e_env.items():
             monkeypatch.setenv(k, v)
