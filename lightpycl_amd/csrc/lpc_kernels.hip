@@ -1312,7 +1312,9 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
 // 2 histogram and 2 look-back pass kernels for 1 M rays).  set_rays takes this
 // path only when a host estimate puts at most LPC_BS_MAXB rays into a hi bucket.
 #define LPC_BS_T 1024                      // threads per block
-#define LPC_BS_RPB 4096                    // rays per k_bkey / k_bscatter block
+#ifndef LPC_BS_RPB
+#define LPC_BS_RPB 4096                    // rays per k_bkey / k_bscatter block (-D: compile-time A/B)
+#endif
 #define LPC_BS_HB 8                        // hi digit bits (at most); lo digit <= 8 bits
 #define LPC_BS_ND (1 << LPC_BS_HB)
 #define LPC_BS_MAXB 16384                  // largest hi bucket the host estimate admits (k_bsort2 chunks)

@@ -204,8 +204,8 @@ struct lpc_handle {
     bool pop_box = true;                            // LPC_POPBOX: re-sorted chained populations keyed in their own box
     DBuf w_tbox, d_pbox;                            // per-tile boxes (k_shade_stage), the population's box (k_stage_move)
     bool pbox_ok = false;                           // d_pbox holds the current population's origin box
-    int key_obits = 5;                              // LPC_KEY_OBITS: origin bits per axis of that key (4..8)
-    int key_mode = 0;                               // LPC_KEY_MODE: 0 origin-major, 1 5-D Morton, 2 direction-major
+    int key_obits = 6;                              // LPC_KEY_OBITS: origin bits per axis of that key (4..8)
+    int key_mode = 1;                               // LPC_KEY_MODE: 0 origin-major, 1 5-D Morton, 2 direction-major
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;

@@ -610,7 +610,7 @@ def test_written_slot_masks_equal_full_reads(monkeypatch, name, n):
 
 
 @pytest.mark.parametrize("env", [dict(LPC_POPBOX="0"), dict(LPC_KEY_OBITS="7"), dict(LPC_KEY_OBITS="4"),
-                                 dict(LPC_XCD_CLAIM="1"), dict(LPC_KEY_MODE="1", LPC_KEY_OBITS="6"),
+                                 dict(LPC_XCD_CLAIM="1"), dict(LPC_KEY_MODE="0", LPC_KEY_OBITS="5"),
                                  dict(LPC_KEY_MODE="2")])
 def test_resorted_populations_keys(monkeypatch, env):
     """Re-sorted chained populations (LPC_RESORT_MIN lowered so that every
