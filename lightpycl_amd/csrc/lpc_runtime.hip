@@ -2455,11 +2455,14 @@ int lpc_trace_iterate_export(lpc_handle *h, void *host, int32_t flags, lpc_iter_
     if (!host) return set_err(h, LPC_E_ARG, "trace_iterate_export: null host block");
     if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_iterate_export before trace_set_rays");
     HIPCHK(h, hipSetDevice(h->device));
+    const double t_enter = h->host_prof ? host_us() : 0.0;
     ExportSpec X;
     X.host = (char *)host;
     X.org = (flags & 1) ? 1 : 0;
     Pending P;
     RETIF(iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &P, &X));
+    if (h->host_prof && !P.empty)
+        fprintf(stderr, "[lpc host] n %lld  export launch %.1f us\n", (long long)P.n_in, host_us() - t_enter);
     return iter_collect(h, P, nullptr, st);
 }
 

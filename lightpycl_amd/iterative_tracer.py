@@ -131,7 +131,9 @@ class CL_Tracer:
                     # the results tuple (:335-355) copied to pinned host arrays on
                     # the export stream while the next iterations run (complete
                     # after the sync below); iteration 0's origins are the host's
+                    t_it = clk()
                     st, ex = self.engine.iterate_export(with_origin=t_iter > 0)
+                    ph.setdefault("iterate_export", []).append(clk() - t_it)
                     org = origin if t_iter == 0 else ex["origin"]
                     pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
                     self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355

@@ -30,5 +30,6 @@ for _ in range(reps):
 bounces = sum(len(r[3]) for r in res)
 dt = min(times)
 print(json.dumps(dict(scene=name, rays=n, iterations=len(res), ray_bounces=bounces, s_per_trace=times,
-                      ray_bounces_per_s=bounces / dt, phases={k: round(v * 1e3, 3) for k, v in getattr(tr, "phase_s", {}).items()},
+                      ray_bounces_per_s=bounces / dt, phases={k: (round(v * 1e3, 3) if not isinstance(v, list) else [round(x * 1e3, 3) for x in v])
+                              for k, v in getattr(tr, "phase_s", {}).items()},
                       measured_power=float(np.sum(tr.get_measured_rays()[1], dtype=np.float64)))), flush=True)
