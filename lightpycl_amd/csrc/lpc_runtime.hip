@@ -125,6 +125,7 @@ struct lpc_handle {
     bool misc_clean = false;                        // the launch words were reset for the next launch
     bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
     int half = 3;                                   // LPC_HALF: half-line cull (see run_intersect; 3: piece roots, not for emitted rays)
+    int half_small = 0;                             // LPC_HALF_SMALL: 1 = node-level cull for small chained populations
     bool half_now = false;                          // ... for the launch in progress
     bool half_roots = false;                        // ... at the piece roots (k_roots)
     bool in_trace = false;                          // run_intersect called from lpc_trace_iterate
@@ -1038,7 +1039,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // population) are never culled.
     const bool in_trace = h->in_trace;
     const bool emitted = h->pop_emitted;
-    h->half_now = in_trace && (h->half == 2 || (h->half == 1 && !emitted));
+    // LPC_HALF_SMALL 1: also every node test of chained populations below
+    // spill_small_n rays (the headline's secondaries)
+    h->half_now = in_trace && (h->half == 2 || (h->half == 1 && !emitted) ||
+                               (h->half_small == 1 && !emitted && n < h->spill_small_n));
     h->half_roots = in_trace && (h->half_now || h->half == 4 || (h->half == 3 && !emitted));
     const bool restore = traced && h->fuse_compact;
     const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
@@ -1353,6 +1357,7 @@ int lpc_open(int device, lpc_handle **out)
     h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
     h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
     h->half = (int)env_int("LPC_HALF", h->half);
+    h->half_small = (int)env_int("LPC_HALF_SMALL", h->half_small);
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->resort_min = std::max<int64_t>(1, env_int("LPC_RESORT_MIN", h->resort_min));
