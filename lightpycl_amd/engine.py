@@ -261,9 +261,13 @@ class Engine:
             return st, dict(origin=z, dest=z.copy(), pow=np.zeros(0, np.float32), meas=np.zeros(0, np.int32))
         layout = ([(np.float32, (n, 4))] if with_origin else []) + [(np.float32, (n, 4)), (np.float32, (n,)),
                                                                      (np.int32, (n,))]
+        import time as _t
+        t0 = _t.perf_counter()
         blk = POOL.block(n * ((16 if with_origin else 0) + 24))
+        t1 = _t.perf_counter()
         self._c(self.L.lpc_trace_iterate_export(self.h, ctypes.cast(blk, ctypes.c_void_p), 1 if with_origin else 0,
                                                 ctypes.byref(st)))
+        self.export_times = (t1 - t0, _t.perf_counter() - t1)
         v = POOL.views(blk, layout)
         if not with_origin:
             v = [None] + v

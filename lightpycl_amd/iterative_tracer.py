@@ -134,6 +134,7 @@ class CL_Tracer:
                     t_it = clk()
                     st, ex = self.engine.iterate_export(with_origin=t_iter > 0)
                     ph.setdefault("iterate_export", []).append(clk() - t_it)
+                    ph.setdefault("export_pool_call", []).extend(getattr(self.engine, "export_times", ()))
                     org = origin if t_iter == 0 else ex["origin"]
                     pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
                     self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355

@@ -32,4 +32,5 @@ dt = min(times)
 print(json.dumps(dict(scene=name, rays=n, iterations=len(res), ray_bounces=bounces, s_per_trace=times,
                       ray_bounces_per_s=bounces / dt, phases={k: (round(v * 1e3, 3) if not isinstance(v, list) else [round(x * 1e3, 3) for x in v])
                               for k, v in getattr(tr, "phase_s", {}).items()},
+                      pinned_allocs=__import__("lightpycl_amd.pinned", fromlist=["POOL"]).POOL.allocated,
                       measured_power=float(np.sum(tr.get_measured_rays()[1], dtype=np.float64)))), flush=True)
