@@ -206,6 +206,7 @@ struct lpc_handle {
     DBuf w_tbox, d_pbox;                            // per-tile boxes (k_shade_stage), the population's box (k_stage_move)
     bool pbox_ok = false;                           // d_pbox holds the current population's origin box
     int key_obits = 6;                              // LPC_KEY_OBITS: origin bits per axis of that key (4..8)
+    int64_t ds_cap_max = INT64_MAX;                 // LPC_DS_CAP: largest device-sized (speculative) population
     int key_mode = 1;                               // LPC_KEY_MODE: 0 origin-major, 1 5-D Morton, 2 direction-major
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
@@ -668,7 +669,8 @@ static int64_t chunk_rays(const lpc_handle *h)
 // (it runs empty) when more children are kept, and the host re-runs it.
 static int64_t ds_cap(const lpc_handle *h)
 {
-    return std::max<int64_t>(0, std::min<int64_t>({h->resort_min - 1, chunk_rays(h), (int64_t)LPC_Q_MAX_PACKETS * 64}));
+    return std::max<int64_t>(0, std::min<int64_t>({h->resort_min - 1, chunk_rays(h), (int64_t)LPC_Q_MAX_PACKETS * 64,
+                                                   h->ds_cap_max}));
 }
 
 // Workspace for a chunk of `n` rays.
@@ -1391,6 +1393,7 @@ int lpc_open(int device, lpc_handle **out)
     h->q_walk_blocks = std::max<int64_t>(1, env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks));
     h->xcd_claim = (int)env_int("LPC_XCD_CLAIM", h->xcd_claim);
     h->pop_box = env_int("LPC_POPBOX", h->pop_box) != 0;
+    h->ds_cap_max = std::max<int64_t>(0, env_int("LPC_DS_CAP", h->ds_cap_max));
     h->key_obits = (int)std::min<int64_t>(8, std::max<int64_t>(4, env_int("LPC_KEY_OBITS", h->key_obits)));
     h->key_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_KEY_MODE", h->key_mode)));
     {
