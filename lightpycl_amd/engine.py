@@ -265,8 +265,11 @@ class Engine:
         t0 = _t.perf_counter()
         blk = POOL.block(n * ((16 if with_origin else 0) + 24))
         t1 = _t.perf_counter()
-        self._c(self.L.lpc_trace_iterate_export(self.h, ctypes.cast(blk, ctypes.c_void_p), 1 if with_origin else 0,
-                                                ctypes.byref(st)))
+        # the block's address as a plain integer: ctypes.cast would tie the block and
+        # the cast result into a reference cycle, and the block would return to the
+        # pool only when the cyclic GC happens to run
+        self._c(self.L.lpc_trace_iterate_export(self.h, ctypes.c_void_p(ctypes.addressof(blk)),
+                                                1 if with_origin else 0, ctypes.byref(st)))
         self.export_times = (t1 - t0, _t.perf_counter() - t1)
         v = POOL.views(blk, layout)
         if not with_origin:

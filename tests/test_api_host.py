@@ -283,3 +283,47 @@ def test_flatten_meshes_equals_tribuf_rows():
             assert got.dtype == want.dtype and got.shape == want.shape, name
             assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), name
         assert np.array_equal(mid, np.concatenate(ids)), name
+
+
+def test_pinned_pool_recycles_blocks(monkeypatch):
+    """The results export's page-locked blocks (lightpycl_amd/pinned.py) return
+    to the pool as soon as no numpy view of them is left (reference counting, no
+    cyclic-GC pass needed), so repeated traces reuse them instead of pinning new
+    memory."""
+    import ctypes
+    import gc
+
+    import numpy as np
+    from lightpycl_amd import _lib, pinned
+    libc = ctypes.CDLL("libc.so.6")
+    libc.malloc.restype = ctypes.c_void_p
+    libc.free.argtypes = [ctypes.c_void_p]
+
+    class FakeL:
+        def lpc_host_alloc(self, size, pp):
+            ctypes.cast(pp, ctypes.POINTER(ctypes.c_void_p))[0] = libc.malloc(size)
+            return 0
+
+        def lpc_host_free(self, p):
+            libc.free(p)
+            return 0
+
+    monkeypatch.setattr(_lib, "load", lambda: FakeL())
+    monkeypatch.setattr(_lib, "check", lambda rc, h: None)
+    pool = pinned.PinnedPool()
+    gc.disable()
+    try:
+        def trace():
+            out = []
+            for size in (24_000_000, 40_000_000):
+                blk = pool.block(size)
+                _ = ctypes.c_void_p(ctypes.addressof(blk))       # what the engine passes to the library
+                out.append(pool.views(blk, [(np.float32, (1000, 4)), (np.int32, (1000,))]))
+            return out
+        res = trace()
+        for _ in range(5):
+            res = trace()
+        assert pool.allocated == 4, pool.allocated              # two traces' blocks, then reuse
+        assert res[1][0].shape == (1000, 4) and res[1][1].dtype == np.int32
+    finally:
+        gc.enable()
