@@ -242,8 +242,9 @@ def run_configs(Engine, ShardedTrace, scenes):
         in_pow = float(np.sum(p, dtype=np.float64))
         run = ShardedTrace(e)
         steps = 1 if name == "eye" else 5
-        e.reset()
-        run.run(depth, sc.tau, in_pow, wait=False)            # warm-up (allocations)
+        for _ in range(1 if name == "eye" else 2):               # warm-up: allocations, then a trace with
+            e.reset()                                            # the first's prediction (speculation)
+            run.run(depth, sc.tau, in_pow, wait=False)
         e.sync()
         e.prof_enable(True, light=True)
         e.prof_read(reset=True)

@@ -986,22 +986,6 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
 {
     __shared__ WaveLds lds;
     if (nd) n = *nd;
-    if (Q.claim == 2) {
-        // static XCD partition: block b (on XCD b % 8) walks shard b % 8's items
-        // grid-stride (items sharded by piece: each XCD's L2 holds its pieces' records)
-        const uint32_t c = blockIdx.x % LPC_Q_CSHARDS, nb = gridDim.x / LPC_Q_CSHARDS;
-        const uint32_t cnt = min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-        for (uint32_t i = blockIdx.x / LPC_Q_CSHARDS; nb > 0 && i < cnt; i += nb) {
-            const uint64_t it = Q.roots[(size_t)c * Q.rcap + i];
-            Piece P;
-            memset(&P, 0, sizeof(P));
-            P.root = (int32_t)q_node(it);
-            P.slot = (int32_t)q_slot(it);
-            trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot, eps,
-                                                    max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
-        }
-        return;
-    }
     if (Q.claim) {
         // claim mode: a resident grid; each wave claims items one at a time from
         // the shard of its XCD (block b runs on XCD b % 8), then from the others

@@ -941,7 +941,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     Q.err = (uint32_t *)((char *)h->d_acc.p + offsetof(DevAcc, qerr));
     Q.rcap = (uint32_t)rcap;
     Q.xpiece = xpiece ? 1 : 0;
-    Q.claim = h->xcd_claim;
+    Q.claim = h->xcd_claim ? 1 : 0;
     if (h->host_prof)
         fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d groups %d S %d pb %d blocks %lld rcap %lld\n",
                 (long long)n, (long long)npk, (int)pt->npieces, (int)pt->ngroups, rs_S, rs_pb, (long long)rs_blocks,
@@ -968,9 +968,8 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     RETIF(spill_setup(h, n, &SP));
     // the grid in waves (LPC_Q_WALK_BLOCKS x 4), single-wave blocks
     // (claim mode: as many single-wave blocks as the chip holds at once)
-    // (claim mode 2: the usual grid, a multiple of the 8 XCDs)
-    const unsigned grid = h->xcd_claim == 1 ? (unsigned)std::max(1, h->cus * 4 * LPC_WALK_MINB)
-                                            : (unsigned)std::max<int64_t>(8, (h->q_walk_blocks * 4) & ~7ll);
+    const unsigned grid = h->xcd_claim ? (unsigned)std::max(1, h->cus * 4 * LPC_WALK_MINB)
+                                       : (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4);
     // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;

@@ -109,7 +109,7 @@ _POLICIES = [
     # items sharded by piece and claimed XCD-first by a resident grid; small budgets
     dict(LPC_XCD_CLAIM="1"), dict(LPC_XCD_CLAIM="1", LPC_Q_TARGET="1000000"),
     dict(LPC_XCD_CLAIM="1", LPC_BUDGET="3"), dict(LPC_BUDGET_SMALL="0"), dict(LPC_BUDGET_SMALL="5"),
-    dict(LPC_XCD_CLAIM="2"), dict(LPC_XCD_CLAIM="2", LPC_Q_WALK_BLOCKS="3"), dict(LPC_HALF_SMALL="1"),
+    dict(LPC_HALF_SMALL="1"), dict(LPC_DS_CAP="0"),
     # the k_intersect alternative and its knobs
     dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
     dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),

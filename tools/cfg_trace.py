@@ -29,8 +29,9 @@ e.upload_meshes(sc.meshes)
 e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
 in_pow = float(np.sum(p, dtype=np.float64))
 run = ShardedTrace(e)
-e.reset()
-run.run(depth, sc.tau, in_pow)
+for _ in range(2):          # two warm-up traces: the second runs with the first's prediction (speculative
+    e.reset()               # iterations' allocations happen before the timed traces)
+    run.run(depth, sc.tau, in_pow)
 e.sync()
 t = time.perf_counter()
 for _ in range(reps):
