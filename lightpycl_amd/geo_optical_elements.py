@@ -205,7 +205,10 @@ class optical_elements:
                 base = i * 4 + 4 * k * nseg
                 tris.append([0, 1, 2] + base)
                 tris.append([2, 3, 1] + base)
-        return GeoObject(verts, tris)
+        # one (n, 4) float32 table (the same rows as a list of them) so that
+        # flattening a scene is one gather, not a pass over Python rows
+        return GeoObject(np.array(verts, dtype=np.float32).reshape(-1, 4),
+                         np.array(tris, dtype=np.int64).reshape(-1, 3))
 
     def extrude_by_vector(self, curve, vector, capped=True):
         verts, tris = [], []
@@ -216,7 +219,8 @@ class optical_elements:
             if k < len(curve) - 1:
                 tris.append([2 * k + 0, 2 * k + 1, 2 * k + 2])
                 tris.append([2 * k + 2, 2 * k + 3, 2 * k + 1])
-        gobj = GeoObject(verts, tris)
+        gobj = GeoObject(np.array(verts, dtype=np.float32).reshape(-1, 4),
+                         np.array(tris, dtype=np.int64).reshape(-1, 3))
         if capped:
             cap = self.curve_to_mesh(curve)
             gobj.append(cap.vertices, cap.triangles)
