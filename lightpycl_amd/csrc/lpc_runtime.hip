@@ -2527,6 +2527,8 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
     if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_run before trace_set_rays");
+    if (h->host_prof)                           // the caller's time between traces
+        fprintf(stderr, "[lpc host] trace enter  since last %.1f us\n", host_us() - h->host_last);
     HIPCHK(h, hipSetDevice(h->device));
     *n_iter = 0;
     h->gstats.clear();
@@ -2639,6 +2641,11 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         if (mesh_power) memcpy(mesh_power, mp.data(), (size_t)h->K * 8);
     }
     if (wait) RETIF(settle(h));                             // the trace's last kernels too
+    if (h->host_prof) {
+        const double t = host_us();
+        fprintf(stderr, "[lpc host] trace leave  since last %.1f us\n", t - h->host_last);
+        h->host_last = t;
+    }
     return 0;
 }
 

@@ -7,7 +7,6 @@ per-bounce entry points of ``include/lpc.h`` with numpy arrays.
 from __future__ import annotations
 
 import ctypes
-import hashlib
 import os
 
 import numpy as np
@@ -164,20 +163,19 @@ class Engine:
         M, K = v0.shape[0], mat_type.shape[0]
         # the same scene as the last upload (a tracer called again on its meshes,
         # as the reference's examples do): keep the device records, skip the
-        # rebuild (the filter hierarchy is built on the host at every upload)
-        h = hashlib.blake2b(digest_size=16)
-        for a in (v0, v1, v2, mesh_id, mat_type, ior, refl, diss):
-            h.update(np.int64(a.size).tobytes())
-            h.update(a.tobytes())
-        key = h.digest()
-        if key == getattr(self, "_scene_key", None):
+        # rebuild (the filter hierarchy is built on the host at every upload).
+        # Compared bit for bit with a kept copy (as integers: -0.0 is not 0.0).
+        arrs = (v0, v1, v2, mesh_id, mat_type, ior, refl, diss)
+        last = getattr(self, "_scene_last", None)
+        if last is not None and all(a.shape == b.shape and np.array_equal(a.view(np.int32), b)
+                                    for a, b in zip(arrs, last)):
             return
-        self._scene_key = None
+        self._scene_last = None
         self._c(self.L.lpc_scene_upload(self.h, M, ptr(v0), ptr(v1), ptr(v2), ptr(mesh_id), K,
                                         ptr(mat_type), ptr(ior), ptr(refl), ptr(diss)))
         self.tri_count, self.mesh_count = M, K
         self.mat_type = mat_type
-        self._scene_key = key
+        self._scene_last = tuple(np.array(a, copy=True).view(np.int32) for a in arrs)
 
     def upload_meshes(self, meshes):
         arrs = flatten_meshes(meshes)

@@ -94,3 +94,45 @@ def test_pickle_traced_scene_roundtrip(tmp_path):
     p1, w1 = tr2.get_measured_rays()
     np.testing.assert_array_equal(p0, p1)
     np.testing.assert_array_equal(w0, w1)
+
+
+def test_scene_upload_skipped_only_for_identical_bits():
+    """A tracer called again on its meshes keeps the device scene (Engine.
+    upload_arrays compares bit for bit with the last upload); a moved mesh, or a
+    vertex whose only change is the sign of a zero, is uploaded again."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import Engine, flatten_meshes
+    sc = scenes.lens(n=4000, seed=5)
+    o, d, p = _rays(sc)
+    arrs = [np.array(a) for a in flatten_meshes(sc.meshes)]
+    e = Engine(0)
+
+    def trace(a):
+        e.upload_arrays(*a)
+        e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+        out = []
+        while e.population() and len(out) < 4:
+            st, ex = e.iterate(export=True)
+            out.append((st.n_reflect, st.n_refract, ex["dest"].copy()))
+        return out
+
+    base = trace(arrs)
+    kept = e._scene_last
+    assert trace([a.copy() for a in arrs]) and e._scene_last is kept      # identical bits: no upload
+    moved = [a.copy() for a in arrs]
+    for k in range(3):
+        moved[k][:, 0] += np.float32(0.25)
+    got = trace(moved)
+    assert e._scene_last is not kept
+    assert any(not np.array_equal(x[2], y[2]) for x, y in zip(base, got))
+    z = [a.copy() for a in arrs]
+    zero = np.flatnonzero(z[0][:, 3] == 0)[0]
+    z[0][zero, 3] = -0.0                                        # w: bits differ, value equal
+    kept = e._scene_last
+    trace(z)
+    assert e._scene_last is not kept
+    back = trace(arrs)
+    for x, y in zip(base, back):
+        assert x[:2] == y[:2]
+        np.testing.assert_array_equal(x[2], y[2])
+    e.close()
