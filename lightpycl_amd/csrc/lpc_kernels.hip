@@ -2037,7 +2037,7 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_shade_stage(StageArgs A)
 }
 
 template <bool DS>
-__global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
+static __device__ __forceinline__ void stage_move(MoveArgs A)
 {
     __shared__ long long s_red[LPC_ST_TILE / 64][6];
     __shared__ long long s_pre[3], s_tot[3];
@@ -2098,10 +2098,13 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
         double lp = 0.0, lm[LPC_MP_MAX] = {0.0, 0.0, 0.0, 0.0};
         float ld = 0.0f;
         // eight of this thread's tiles per round, loaded before they are added
-        // (one load latency per round instead of one per tile; same order of adds)
+        // (one load latency per round instead of one per tile; same order of adds).
+        // The first measure mesh's sums ride with the power sums; further measure
+        // meshes take rounds of their own, so the round's registers stay few (this
+        // path sets the VGPR count, i.e. the occupancy, of every block's row moves)
         constexpr int UB = 8;
         for (int64_t j0 = t; j0 < ntiles; j0 += (int64_t)UB * LPC_ST_TILE) {
-            double vp[UB], vm[UB][LPC_MP_MAX];
+            double vp[UB], v0[UB];
             uint32_t vd[UB];
 #pragma unroll
             for (int u = 0; u < UB; ++u) {
@@ -2109,18 +2112,34 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
                 const bool ok = j < ntiles;
                 vp[u] = ok ? A.tpow[j] : 0.0;
                 vd[u] = ok ? A.tdm[j] : 0u;
-#pragma unroll
-                for (int m = 0; m < LPC_MP_MAX; ++m) vm[u][m] = (ok && m < A.nmp) ? A.tmp[j * LPC_MP_MAX + m] : 0.0;
+                v0[u] = (ok && A.nmp > 0) ? A.tmp[j * LPC_MP_MAX] : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < UB; ++u) {
                 if (j0 + (int64_t)u * LPC_ST_TILE >= ntiles) break;
                 lp += vp[u];
                 ld = fmaxf(ld, __uint_as_float(vd[u]));
-#pragma unroll
-                for (int m = 0; m < LPC_MP_MAX; ++m)
-                    if (m < A.nmp) lm[m] += vm[u][m];
+                if (A.nmp > 0) lm[0] += v0[u];
             }
+        }
+#pragma unroll
+        for (int m = 1; m < LPC_MP_MAX; ++m) {
+            if (m >= A.nmp) break;
+            double a = 0.0;
+            for (int64_t j0 = t; j0 < ntiles; j0 += (int64_t)UB * LPC_ST_TILE) {
+                double vm[UB];
+#pragma unroll
+                for (int u = 0; u < UB; ++u) {
+                    const int64_t j = j0 + (int64_t)u * LPC_ST_TILE;
+                    vm[u] = j < ntiles ? A.tmp[j * LPC_MP_MAX + m] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < UB; ++u) {
+                    if (j0 + (int64_t)u * LPC_ST_TILE >= ntiles) break;
+                    a += vm[u];
+                }
+            }
+            lm[m] = a;
         }
         s_p[t] = lp;
         s_d[t] = ld;
@@ -2287,6 +2306,31 @@ __global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A)
             __syncthreads();                      // s_red / s_pre / s_tot reused by the next tile
         }
     }
+}
+
+// The one-tile-per-block form at 8 waves per SIMD (64 VGPRs, no scratch): its
+// blocks are row moves, more of them in flight hide the loads' latency; the
+// grid-stride device-sized form keeps more live across its tile loop and would
+// spill at that bound.
+#ifndef LPC_MOVE_OCC
+#define LPC_MOVE_OCC 1
+#endif
+#if LPC_MOVE_OCC
+#define LPC_MOVE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#else
+#define LPC_MOVE_ATTR
+#endif
+template <bool DS>
+__global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move(MoveArgs A);
+template <>
+__global__ __launch_bounds__(LPC_ST_TILE) LPC_MOVE_ATTR void k_stage_move<false>(MoveArgs A)
+{
+    stage_move<false>(A);
+}
+template <>
+__global__ __launch_bounds__(LPC_ST_TILE) void k_stage_move<true>(MoveArgs A)
+{
+    stage_move<true>(A);
 }
 
 // Append the refracted block after the reflected one (next population).

@@ -25,6 +25,12 @@ pmc)
     ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp -d $R/$O/pmc_$tag -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu --no-configs > $R/$O/pmc_$tag.log 2>&1 ) || { echo "pmc $grp failed"; exit 1; }
   done
   ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $R/$O/valu_pmc -o pmc --output-format csv -- $R/tools/_valu_issue 4096 > $R/$O/valu_pmc.log 2>&1 ) || { echo valu pmc failed; exit 1; } ;;
+atomics)
+  # where the walk's writes go: memory-side atomic requests (64 B each) against
+  # all write requests, per launch (one bench step: the primary and two secondaries)
+  ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_ATOMIC_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum -d $R/$O/pmc_atomics -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu --no-configs > $R/$O/pmc_atomics.log 2>&1 ) || { echo "pmc atomics failed"; exit 1; } ;;
+hostgap)
+  LPC_HOSTPROF=1 run 120 host_gap.log python -u tools/host_gap.py 20 ;;
 results)
   run 300 results_mode.json python -u tools/results_mode.py parabolic 1000000 5 ;;
 ab)
