@@ -7,3 +7,4 @@ tail -1 $O/ab_move.log
 timeout -k 10 400 python -u tools/trace_stats.py eye 300000 > $O/stats_eye.log 2>&1 || { tail $O/stats_eye.log; exit 1; }
 tail -30 $O/stats_eye.log
 TAG=r4l bash tools/gpu_round.sh atomics && echo atomics ok
+TAG=r4l bash tools/gpu_round.sh pmc && echo pmc ok
