@@ -1012,15 +1012,21 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
         }
         return;
     }
-    uint32_t pre[LPC_Q_CSHARDS + 1];
-    pre[0] = 0;
+    // the shards' item prefix in LDS: a register array indexed by a loop variable
+    // would hold 9 VGPRs for the whole walk (the walk then spills at 6 waves/SIMD)
+    __shared__ uint32_t s_pre[LPC_Q_CSHARDS + 1];
+    if (threadIdx.x == 0) {
+        uint32_t p = 0;
+        s_pre[0] = 0;
 #pragma unroll
-    for (int c = 0; c < LPC_Q_CSHARDS; ++c) pre[c + 1] = pre[c] + min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-    const uint32_t stride = gridDim.x, iend = pre[LPC_Q_CSHARDS];
+        for (int c = 0; c < LPC_Q_CSHARDS; ++c) { p += min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap); s_pre[c + 1] = p; }
+    }
+    __syncthreads();
+    const uint32_t stride = gridDim.x, iend = s_pre[LPC_Q_CSHARDS];
     for (uint32_t i = blockIdx.x; i < iend; i += stride) {
         int c = 0;
-        while (i >= pre[c + 1]) ++c;
-        const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - pre[c])];
+        while (i >= s_pre[c + 1]) ++c;
+        const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - s_pre[c])];
         Piece P;
         memset(&P, 0, sizeof(P));
         P.root = (int32_t)q_node(it);
@@ -1104,8 +1110,10 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
             if (!any_lane(r0 || r1)) continue;
             const int32_t idx = bcasti(S.idx, k);
             const f3 V0 = mk3(v0x, v0y, v0z);
-            const f3 E1 = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
-            const f3 E2 = mk3(e2x, e2y, e2z);
+            // a thin triangle's filter edge is E1 (ax1): the exact record in its order
+            const f3 Ea = mk3(e2x, e2y, e2z), Eb = mk3(bcast(S.e1x, k), bcast(S.e1y, k), bcast(S.e1z, k));
+            const bool ax1 = bcasti(S.ax1, k) != 0;
+            const f3 E1 = ax1 ? Ea : Eb, E2 = ax1 ? Eb : Ea;
             if (r0) mt_accumulate(O0, D0, V0, E1, E2, idx, eps, t0, i0, c0);
             if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
             n_exact += (uint32_t)r0 + (uint32_t)r1;

@@ -453,11 +453,18 @@ typedef NodeW<8> Node8;
 // Moller-Trumbore is rounding noise that can accept rays anywhere along the line
 // through V0 with direction E2, so it gets a line filter instead (sliver_params).
 // Padding records have a = NaN (never pass).
+// A "thin" triangle (round 4, LPC_THIN) gets the same kind of record: one whose
+// bounding sphere is far wider than the triangle (the lens meshes' discs through
+// the optical axis: 10 mm long, 0.4 mm wide, every axial ray passes all their
+// spheres) is bounded better by the line filter about its longer edge.  The
+// filter's edge ("axis") sits in e2; ax1 = 1 says it is E1 (the v-test's line,
+// sliver_params_axis), and the exact test then takes E1 = e2, E2 = e1.
 struct SliverRec {
     float v0x, v0y, v0z, e2x, e2y, e2z, a, b;
     int32_t idx;
     float e1x, e1y, e1z;    // with v0, e2: the exact record (Moller-Trumbore input)
     float dmin;             // |DEN| >= 1e-6 needs |D| >= dmin (sliver_dmin)
+    int32_t ax1;            // 1: e2 holds E1 and e1 holds E2 (line filter about E1)
 };
 
 // Bound of one wave's packet of rays (k_packet): every origin lies within ro of
@@ -695,6 +702,60 @@ static inline float sliver_dmin(const float *V0, const float *V1, const float *V
     float f = (float)dmin;
     if ((double)f > dmin) f = nextafterf(f, 0.0f);
     return f;
+}
+
+// The same bound about E1 (the v-test): Moller-Trumbore accepts only if
+// 0 <= v and fl(u + v) <= 1 with u >= 0, so |fl(Q.D)| <= |fl(DEN)| (1 + 3eps) with
+// Q = T x E1, and |fl(Q.D) - D.(T x E1)| <= 10 eps |D||E1||T| as for P.T: acceptance
+// implies |D.(E1 x T)| <= |D| (|E1 x E2|(1+3eps) + 11 eps |E1||E2| + 10 eps |E1||T|),
+// i.e. sliver_params with the roles of |E1| and |E2| swapped in the |T| term.
+static inline void sliver_params_axis(const float *V0, const float *V1, const float *V2, int ax1, float *a_out,
+                                      float *b_out)
+{
+    const double eps = 1.0 / 16777216.0;
+    double e1[3], e2[3];
+    for (int k = 0; k < 3; ++k) { e1[k] = (double)(V1[k] - V0[k]); e2[k] = (double)(V2[k] - V0[k]); }
+    const double c[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                         e2[0] * e1[1] - e2[1] * e1[0]};
+    const double nc = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    const double n2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+    double a = 2.0 * (nc * (1.0 + 4.0 * eps) + 16.0 * eps * n2 * n1);
+    double b = 2.0 * sqrt(3.0) * 32.0 * eps * (ax1 ? n1 : n2);
+    float af = (float)a, bf = (float)b;
+    if ((double)af < a) af = nextafterf(af, INFINITY);
+    if ((double)bf < b) bf = nextafterf(bf, INFINITY);
+    *a_out = af; *b_out = bf;
+}
+
+// Thin-triangle rule (LPC_THIN = k percent): the line filter about the longer of
+// E1, E2 passes rays within h = |E1 x E2| / max(|E1|, |E2|) of a line, about 2 h S of
+// a scene-sized cross-section (S the scene's half diagonal, 4 h S), the sphere test
+// those within its radius rho (pi rho^2): the line filter is taken when
+// k/100 * 8 h S < pi rho^2.  Returns 0 (sphere), 1 (line about E2) or 2 (about E1).
+static inline int thin_axis(const float *V0, const float *V1, const float *V2, float cx, float cy, float cz,
+                            double S, double k)
+{
+    if (!(k > 0.0)) return 0;
+    double e1[3], e2[3], r2 = 0.0;
+    const float *Vs[3] = {V0, V1, V2};
+    const double fc[3] = {cx, cy, cz};
+    for (int v = 0; v < 3; ++v) {
+        double d2 = 0.0;
+        for (int q = 0; q < 3; ++q) { const double x = (double)Vs[v][q] - fc[q]; d2 += x * x; }
+        r2 = fmax(r2, d2);
+    }
+    for (int q = 0; q < 3; ++q) { e1[q] = (double)(V1[q] - V0[q]); e2[q] = (double)(V2[q] - V0[q]); }
+    const double c[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                         e2[0] * e1[1] - e2[1] * e1[0]};
+    const double nc = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    const double n2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+    const double el = fmax(n1, n2);
+    if (!(el > 0.0)) return 0;
+    const double hh = nc / el;
+    if (!(k * 8.0 * hh * S < 3.141592653589793 * r2)) return 0;
+    return n1 > n2 ? 2 : 1;
 }
 
 static inline void sliver_params(const float *V0, const float *V1, const float *V2, float *a_out,

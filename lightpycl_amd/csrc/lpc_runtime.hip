@@ -88,6 +88,8 @@ struct lpc_handle {
     double pop_dmax2 = INFINITY, init_dmax2 = INFINITY;   // max |D|^2 of the trace population / emitted rays
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
+    int64_t n_thin = 0;                              // of them thin triangles (LPC_THIN)
+    int thin_pct = 100;                              // LPC_THIN: thin-triangle rule, k percent (0: off)
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
     double scene_scale = 1.0;                        // half diagonal of the scene box (filter h)
     std::vector<int32_t> slot_run;
@@ -401,6 +403,7 @@ static int build_records(lpc_handle *h)
     h->run_slo.clear(); h->run_shi.clear();
     h->sliver_dmin_host.clear();
     h->n_slivers = 0;
+    h->n_thin = 0;
     const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 0.0f, INFINITY);
     auto vptr = [&](int32_t t, int v) -> const float * {
         return v == 0 ? &h->hv0[4 * (size_t)t] : v == 1 ? &h->hv1[4 * (size_t)t] : &h->hv2[4 * (size_t)t];
@@ -416,6 +419,12 @@ static int build_records(lpc_handle *h)
             const FiltRec f = filter_record(V0, V1, V2, t, h->dcap, h->scene_scale);
             if (f.negA == INFINITY) continue;                     // never a candidate
             if (f.negB < -1e29f) { sl.push_back(t); continue; }
+            // thin: the line filter about its longer edge (k_slivers) bounds it better
+            if (thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale, 0.01 * h->thin_pct)) {
+                sl.push_back(t);
+                ++h->n_thin;
+                continue;
+            }
             fr.push_back(f);
             for (int k = 0; k < 3; ++k) cen.push_back(((double)V0[k] + V1[k] + V2[k]) / 3.0);
         }
@@ -433,9 +442,17 @@ static int build_records(lpc_handle *h)
             SliverRec S;
             memset(&S, 0, sizeof(S));
             S.v0x = V0[0]; S.v0y = V0[1]; S.v0z = V0[2];
-            S.e2x = V2[0] - V0[0]; S.e2y = V2[1] - V0[1]; S.e2z = V2[2] - V0[2];
-            sliver_params(V0, V1, V2, &S.a, &S.b);
-            S.e1x = V1[0] - V0[0]; S.e1y = V1[1] - V0[1]; S.e1z = V1[2] - V0[2];
+            // a thin triangle whose longer edge is E1 filters about E1 (e2 holds it)
+            const FiltRec f = filter_record(V0, V1, V2, t32, h->dcap, h->scene_scale);
+            const int ax = f.negB < -1e29f ? 1 : thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale,
+                                                           0.01 * h->thin_pct);
+            S.ax1 = ax == 2 ? 1 : 0;
+            const float e1[3] = {V1[0] - V0[0], V1[1] - V0[1], V1[2] - V0[2]};
+            const float e2[3] = {V2[0] - V0[0], V2[1] - V0[1], V2[2] - V0[2]};
+            const float *ea = S.ax1 ? e1 : e2, *eb = S.ax1 ? e2 : e1;
+            S.e2x = ea[0]; S.e2y = ea[1]; S.e2z = ea[2];
+            S.e1x = eb[0]; S.e1y = eb[1]; S.e1z = eb[2];
+            sliver_params_axis(V0, V1, V2, S.ax1, &S.a, &S.b);
             S.idx = t32;
             S.dmin = sliver_dmin(V0, V1, V2);
             slivers.push_back(S);
@@ -1360,6 +1377,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
     h->half = (int)env_int("LPC_HALF", h->half);
     h->half_small = (int)env_int("LPC_HALF_SMALL", h->half_small);
+    h->thin_pct = (int)env_int("LPC_THIN", h->thin_pct);
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->resort_min = std::max<int64_t>(1, env_int("LPC_RESORT_MIN", h->resort_min));

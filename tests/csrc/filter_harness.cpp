@@ -123,6 +123,55 @@ extern "C" void sliver_eval(int n, const float *O, const float *D, const float *
     }
 }
 
+// The line filter about E2 (ax1 = 0) or E1 (ax1 = 1) as k_slivers evaluates a
+// SliverRec (sliver_params_axis; the filter edge in e2, the exact test in the
+// triangle's own E1/E2 order), plus the exact acceptance of the same pairs.
+extern "C" void sliver_eval_axis(int n, const float *O, const float *D, const float *V, float eps, int fused,
+                                 int ax1, float *d_out, int *hit_out)
+{
+    for (int i = 0; i < n; ++i) {
+        const float *o = O + 3 * i, *dd = D + 3 * i, *v = V + 9 * i;
+        float a, b;
+        sliver_params_axis(v, v + 3, v + 6, ax1, &a, &b);
+        const float *w = ax1 ? v + 3 : v + 6;
+        const float ex = w[0] - v[0], ey = w[1] - v[1], ez = w[2] - v[2];
+        const float tx = o[0] - v[0], ty = o[1] - v[1], tz = o[2] - v[2];
+        const float tm = fmaxf(fmaxf(fabsf(tx), fabsf(ty)), fabsf(tz));
+        const float dl = sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+        float d;
+        if (fused) {
+            const float cx = fmaf(ey, tz, -(ez * ty)), cy = fmaf(ez, tx, -(ex * tz)), cz = fmaf(ex, ty, -(ey * tx));
+            const float x = fmaf(dd[2], cz, fmaf(dd[1], cy, dd[0] * cx));
+            const float rhs = dl * fmaf(b, tm, a);
+            d = fmaf(x, x, -(rhs * rhs));
+        } else {
+            const float cx = ey * tz - ez * ty, cy = ez * tx - ex * tz, cz = ex * ty - ey * tx;
+            const float x = dd[0] * cx + dd[1] * cy + dd[2] * cz;
+            const float rhs = dl * (a + b * tm);
+            d = x * x - rhs * rhs;
+        }
+        d_out[i] = d;
+        float t = 0.0f;
+        const int h = mt_exact(mk3(o[0], o[1], o[2]), mk3(dd[0], dd[1], dd[2]), mk3(v[0], v[1], v[2]),
+                               mk3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), mk3(v[6] - v[0], v[7] - v[1], v[8] - v[2]),
+                               &t);
+        hit_out[i] = h && t > eps;
+    }
+}
+
+// The engine's thin-triangle rule (build_records: thin_axis on filter_record's
+// sphere): 0 sphere test, 1 line filter about E2, 2 about E1; -1 never / sliver.
+extern "C" void thin_class(int n, const float *V, double dcap, double S, double k, int *cls)
+{
+    for (int i = 0; i < n; ++i) {
+        const float *v = V + 9 * i;
+        float v0[4] = {v[0], v[1], v[2], 0}, v1[4] = {v[3], v[4], v[5], 0}, v2[4] = {v[6], v[7], v[8], 0};
+        FiltRec r = filter_record(v0, v1, v2, 0, dcap, S);
+        if (r.negA == INFINITY || r.negB < -1e29f) { cls[i] = -1; continue; }
+        cls[i] = thin_axis(v0, v1, v2, r.cx, r.cy, r.cz, S, k);
+    }
+}
+
 // filter_record's classification: 0 sphere test, 1 never, 2 always (-> sliver list)
 extern "C" void filt_class(int n, const float *V, double dcap, double S, int *cls)
 {

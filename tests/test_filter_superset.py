@@ -263,6 +263,115 @@ def test_sliver_line_filter_synthetic_thin(sliver_harness):
 
 
 @pytest.fixture(scope="module")
+def thin_harness(harness):
+    L = ctypes.CDLL(SO)
+    P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+    L.sliver_eval_axis.argtypes = [ctypes.c_int, P, P, P, ctypes.c_float, ctypes.c_int, ctypes.c_int, P, I]
+    L.sliver_eval_axis.restype = None
+    L.thin_class.argtypes = [ctypes.c_int, P, ctypes.c_double, ctypes.c_double, ctypes.c_double, I]
+    L.thin_class.restype = None
+
+    def run(O, D, V, eps, fused, ax1):
+        n = O.shape[0]
+        d = np.zeros(n, np.float32)
+        h = np.zeros(n, np.int32)
+        L.sliver_eval_axis(n, np.ascontiguousarray(O, np.float32), np.ascontiguousarray(D, np.float32),
+                           np.ascontiguousarray(V, np.float32), np.float32(eps), int(fused), int(ax1), d, h)
+        return d, h.astype(bool)
+
+    def classify(V, S, k=1.0, dcap=16.0):
+        c = np.zeros(V.shape[0], np.int32)
+        L.thin_class(V.shape[0], np.ascontiguousarray(V, np.float32), dcap, S, k, c)
+        return c
+    run.classify = classify
+    return run
+
+
+def _scene_box_half_diag(V):
+    P = V.reshape(-1, 3).astype(np.float64)
+    return 0.5 * float(np.linalg.norm(P.max(0) - P.min(0)))
+
+
+def test_thin_rule_picks_the_lens_discs_only(thin_harness):
+    """LPC_THIN: the eye's crystalline lens holds a disc of 144 long thin triangles
+    through the optical axis (its two arcs are joined across the axis), whose
+    bounding spheres every axial ray passes; those take the line filter.  The
+    sphere meshes of the synthetic, parabolic and lens scenes keep their sphere
+    tests."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    for name, lo, hi in (("eye", 144, 400), ("synthetic", 0, 0), ("parabolic", 0, 0), ("lens", 0, 0)):
+        sc = scenes.BUILDERS[name](n=8, seed=1)
+        v0, v1, v2, mid, *_ = flatten_meshes(sc.meshes)
+        V = np.concatenate([v0[:, :3], v1[:, :3], v2[:, :3]], 1).astype(np.float32)
+        c = thin_harness.classify(V, _scene_box_half_diag(V))
+        n_thin = int((c > 0).sum())
+        assert lo <= n_thin <= hi, (name, n_thin)
+        if name == "eye":
+            assert ((c > 0) & (mid == 2)).sum() >= 144
+
+
+def _rays_at_triangles(rng, V, n, dist, graze=0.0):
+    """Rays aimed at points inside / on the edges of the triangles V (rows), from
+    origins ~dist away, optionally tilted toward the triangle plane."""
+    j = rng.integers(0, V.shape[0], n)
+    v0, v1, v2 = (V[j, 3 * k:3 * k + 3].astype(np.float64) for k in range(3))
+    bu, bv = rng.random((2, n, 1))
+    f = bu + bv > 1
+    bu[f], bv[f] = 1 - bu[f], 1 - bv[f]
+    edge = rng.random((n, 1)) < 0.3
+    bv = np.where(edge, 0.0, bv)
+    tgt = v0 + bu * (v1 - v0) + bv * (v2 - v0)
+    nrm = np.cross(v1 - v0, v2 - v0)
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-300)
+    tang = (v1 - v0) / np.maximum(np.linalg.norm(v1 - v0, axis=1, keepdims=True), 1e-300)
+    o = tgt + (nrm * (1 - graze) + tang * graze * rng.normal(size=(n, 1)) +
+               rng.normal(size=(n, 3)) * 0.3) * dist[:, None]
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o.astype(np.float32), d.astype(np.float32), V[j]
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_thin_line_filter_is_superset(thin_harness, fused):
+    """Every pair Moller-Trumbore accepts passes the line filter about the edge the
+    thin rule picks (E1 via the v-test, E2 via the u-test): the eye's thin triangles
+    and random thin triangles (aspect 3 .. 1e4, long edge as E1 or E2), rays at their
+    interiors, edges and at grazing angles."""
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    rng = np.random.default_rng(21 + fused)
+    sc = scenes.eye(n=8, seed=1)
+    v0, v1, v2, *_ = flatten_meshes(sc.meshes)
+    Ve = np.concatenate([v0[:, :3], v1[:, :3], v2[:, :3]], 1).astype(np.float32)
+    ce = thin_harness.classify(Ve, _scene_box_half_diag(Ve))
+    m = 6000
+    p0 = rng.normal(size=(m, 3)) * 50
+    e = rng.normal(size=(m, 3))
+    e /= np.linalg.norm(e, axis=1, keepdims=True)
+    perp = np.cross(e, rng.normal(size=(m, 3)))
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True)
+    L = rng.uniform(0.01, 100, (m, 1))
+    w = L / 10.0 ** rng.uniform(0.5, 4, (m, 1))
+    pa, pb = p0 + L * e, p0 + L * e * rng.uniform(0, 1, (m, 1)) + w * perp
+    long1 = rng.random(m) < 0.5                 # long edge = E1 (v1 - v0) or E2 (v2 - v0)
+    Vr = np.where(long1[:, None], np.concatenate([p0, pa, pb], 1), np.concatenate([p0, pb, pa], 1))
+    for V, ax in ((Ve[ce > 0], ce[ce > 0]), (Vr.astype(np.float32), np.where(long1, 2, 1))):
+        for k in (1, 2):
+            Vk = V[ax == k]
+            if len(Vk) == 0:
+                continue
+            for graze in (0.0, 0.9, 0.999):
+                n = 200_000
+                dist = rng.choice([1e-2, 1.0, 30.0, 1e3], n)
+                O, D, Vj = _rays_at_triangles(rng, Vk, n, dist, graze)
+                d, hit = thin_harness(O, D, Vj, 1e-6, fused, k == 2)
+                assert hit.sum() > 1000
+                assert not (hit & ~(d <= 0)).any(), (k, graze)
+
+
+@pytest.fixture(scope="module")
 def packet_harness(harness):
     L = ctypes.CDLL(SO)
     P = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")

@@ -21,7 +21,9 @@ kname = sys.argv[3] if len(sys.argv) > 3 else "k_rootwalk"     # the bench roofl
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "profiles")
 os.makedirs(out, exist_ok=True)
-shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+kst = os.path.join(src, "kt", "kt_kernel_stats.csv")
+if os.path.exists(kst):                 # a kernel trace of the same run, when there is one
+    shutil.copy(kst, os.path.join(out, f"{tag}_kernel_stats.csv"))
 per = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in sorted(os.listdir(src)):
     f = os.path.join(src, d, "pmc_counter_collection.csv")
