@@ -1,4 +1,4 @@
-"""Per-dispatch counter rows of the pmc_probe.sh passes for kernels matching a
+"""Per-dispatch counter rows of the tools/gpu_round.sh pmc passes for kernels matching a
 regex (the last bench step's dispatches: grid size tells the iteration)."""
 import collections
 import csv

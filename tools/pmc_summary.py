@@ -1,4 +1,4 @@
-"""Summarise a tools/profile.sh run into profiles/ (committed evidence).
+"""Summarise a tools/gpu_round.sh profile/pmc run into profiles/ (committed evidence).
 
     python tools/pmc_summary.py gpurun_out/prof r01
 
