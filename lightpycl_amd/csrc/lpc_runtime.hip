@@ -112,6 +112,7 @@ struct lpc_handle {
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
+    int roots_pb3 = 1;                              // LPC_ROOTS_PB3: k_roots_s packets per block with >= 3 tasks per packet
     bool roots_gate = true;                         // LPC_ROOTS_GATE: k_roots_s tests the run roots first
     int walk_nb = 1;                                // LPC_WALK_NB: nodes per walk step (1 or LPC_NB, 8-wide only)
     int max_levels = 0;                             // deepest run hierarchy (stack bound of the batched walk)
@@ -939,7 +940,8 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     const int rs_S = (int)((pt->npieces + 63) / 64);
     const bool roots_s = h->roots_s > 0 && (rs_S <= 4 || (ds && rs_S <= LPC_ROOTS_TASKS));
     if (ds && !roots_s) return set_err(h, LPC_E_STATE, "internal: device-sized root tests need k_roots_s");
-    const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? 1 : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
+    const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? std::max(1, std::min(h->roots_pb3, LPC_ROOTS_TASKS / rs_S))
+                      : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
     const int64_t rs_blocks = roots_s ? (npk + rs_pb - 1) / rs_pb : 0;
     const int64_t rs_vblocks = !ds ? rs_blocks : (((ds->bound + 63) / 64) + rs_pb - 1) / rs_pb;
     // per shard: at most its blocks' packets x pieces items (k_roots* flag an
@@ -1385,6 +1387,7 @@ int lpc_open(int device, lpc_handle **out)
     h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
+    h->roots_pb3 = (int)std::max<int64_t>(1, env_int("LPC_ROOTS_PB3", h->roots_pb3));
     h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
     h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);
     h->spec = env_int("LPC_SPEC", h->spec) != 0;
