@@ -673,8 +673,11 @@ static inline FiltRec filter_record(
 // |fl(DEN)| <= |D||E2 x E1| + 10 eps |D||E2||E1|, acceptance implies
 //     |D.(E2 x T)| <= |D| (|E2 x E1|(1+3eps) + 11 eps |E2||E1| + 10 eps |E2||T|).
 // The kernel tests x^2 <= (|D|(a + b tmax))^2 with x = D.(E2 x T) in float and
-// tmax = max|T_i| (|T| <= sqrt(3) tmax); a, b carry a factor 2 of slack for the
-// float evaluation of the test itself.
+// tmax = max|T_i| (|T| <= sqrt(3) tmax).  Its own float evaluation adds at most
+// 10 eps |D||E2||T| to |x| and 5 eps relative to the right side, so
+// a = |E1 x E2| (1 + 16 eps) + 32 eps |E1||E2| and b = 64 sqrt(3) eps |E2| (b tmax >=
+// 64 eps |E2||T|) cover both.  (Round 3 doubled the |E1 x E2| term as well: harmless
+// for slivers, where it is ~0, but twice the width for a thin triangle's line.)
 // Smallest |D| for which Moller-Trumbore's DEN = E1 . (D x E2) (float, .cl:75-79)
 // can reach the 1e-6 threshold.  Per component P_i = (D x E2)_i is a difference
 // of two products: |P^_i - P_i| <= 2.01 u s_i with s_i = |d_j e2_k| + |d_k e2_j|
@@ -720,7 +723,11 @@ static inline void sliver_params_axis(const float *V0, const float *V1, const fl
     const double nc = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
     const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
     const double n2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+#ifdef LPC_LINE_A2                  // round 3's constant (A/B builds only)
     double a = 2.0 * (nc * (1.0 + 4.0 * eps) + 16.0 * eps * n2 * n1);
+#else
+    double a = nc * (1.0 + 16.0 * eps) + 32.0 * eps * n2 * n1;
+#endif
     double b = 2.0 * sqrt(3.0) * 32.0 * eps * (ax1 ? n1 : n2);
     float af = (float)a, bf = (float)b;
     if ((double)af < a) af = nextafterf(af, INFINITY);
@@ -769,7 +776,11 @@ static inline void sliver_params(const float *V0, const float *V1, const float *
     const double nc = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
     const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
     const double n2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+#ifdef LPC_LINE_A2                  // round 3's constant (A/B builds only)
     double a = 2.0 * (nc * (1.0 + 4.0 * eps) + 16.0 * eps * n2 * n1);
+#else
+    double a = nc * (1.0 + 16.0 * eps) + 32.0 * eps * n2 * n1;
+#endif
     double b = 2.0 * sqrt(3.0) * 32.0 * eps * n2;
     float af = (float)a, bf = (float)b;
     if ((double)af < a) af = nextafterf(af, INFINITY);

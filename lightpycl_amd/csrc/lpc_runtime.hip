@@ -190,6 +190,8 @@ struct lpc_handle {
     bool early_acc = true;                          // LPC_EARLY_ACC: read the counters before k_scatter ends
     bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
+    bool stream_prio = true;                        // LPC_STREAM_PRIO: main stream high, side stream low priority
+    int prio_lo = 0;
     // results export (lpc_trace_iterate_export): k_export packs a chunk's part of
     // the results tuple into xst[par] on the main stream, the export stream copies
     // it to the caller's host block while the next kernels run
@@ -1344,7 +1346,19 @@ int lpc_open(int device, lpc_handle **out)
     lpc_handle *h = new lpc_handle();
     h->device = device;
     e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    // LPC_STREAM_PRIO (default 1): the main stream at the highest priority, the
+    // sliver side stream at the lowest, so the hierarchy stage's launches (root
+    // tests, walk, hand-over levels) get the CUs first and the slivers' long-lived
+    // waves fill what is left instead of holding the GPU ahead of the walk
+    const char *prio_env = getenv("LPC_STREAM_PRIO");
+    h->stream_prio = prio_env ? atoi(prio_env) != 0 : true;
+    int prio_lo = 0, prio_hi = 0;
+    if (e == hipSuccess && h->stream_prio && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess)
+        prio_lo = prio_hi = 0;
+    h->prio_lo = prio_lo;
+    if (e == hipSuccess)
+        e = h->stream_prio ? hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi)
+                           : hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
         return set_err(nullptr, LPC_E_HIP, std::string("stream: ") + hipGetErrorString(e));
@@ -1427,7 +1441,9 @@ int lpc_open(int device, lpc_handle **out)
     h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
     if (env_int("LPC_SIDE_STREAM", 1) != 0) {
         const unsigned evf = hipEventDisableTiming;   // the side stream's fork / join events
-        if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+        const hipError_t es = h->stream_prio ? hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, h->prio_lo)
+                                             : hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking);
+        if (es != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
             h->stream2 = nullptr;       // all on the main stream

@@ -322,7 +322,14 @@ def _rays_at_triangles(rng, V, n, dist, graze=0.0):
     bu[f], bv[f] = 1 - bu[f], 1 - bv[f]
     edge = rng.random((n, 1)) < 0.3
     bv = np.where(edge, 0.0, bv)
+    # 20 %: a vertex (the far vertex lies exactly at the line filter's width),
+    # jittered by a few ulps of the coordinates
+    vert = rng.random((n, 1)) < 0.2
+    k = rng.integers(0, 3, (n, 1))
+    bu = np.where(vert, (k == 1).astype(float), bu)
+    bv = np.where(vert, (k == 2).astype(float), bv)
     tgt = v0 + bu * (v1 - v0) + bv * (v2 - v0)
+    tgt = tgt + np.where(vert, rng.normal(size=(n, 3)) * 1e-7 * np.abs(v0).max(1, keepdims=True), 0.0)
     nrm = np.cross(v1 - v0, v2 - v0)
     nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-300)
     tang = (v1 - v0) / np.maximum(np.linalg.norm(v1 - v0, axis=1, keepdims=True), 1e-300)
