@@ -112,7 +112,9 @@ struct lpc_handle {
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
-    int roots_pb3 = 1;                              // LPC_ROOTS_PB3: k_roots_s packets per block with >= 3 tasks per packet
+    int roots_pb3 = 1;
+    int64_t fork_roots_min = INT64_MAX;             // LPC_FORK_ROOTS_MIN: slivers after k_roots_s from this population
+    bool fork_pending = false;                      // run_intersect -> run_queue: record the side fork after the root tests                              // LPC_ROOTS_PB3: k_roots_s packets per block with >= 3 tasks per packet
     bool roots_gate = true;                         // LPC_ROOTS_GATE: k_roots_s tests the run roots first
     int walk_nb = 1;                                // LPC_WALK_NB: nodes per walk step (1 or LPC_NB, 8-wide only)
     int max_levels = 0;                             // deepest run hierarchy (stack bound of the batched walk)
@@ -190,8 +192,6 @@ struct lpc_handle {
     bool early_acc = true;                          // LPC_EARLY_ACC: read the counters before k_scatter ends
     bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
-    bool stream_prio = true;                        // LPC_STREAM_PRIO: main stream high, side stream low priority
-    int prio_lo = 0;
     // results export (lpc_trace_iterate_export): k_export packs a chunk's part of
     // the results tuple into xst[par] on the main stream, the export stream copies
     // it to the caller's host block while the next kernels run
@@ -983,6 +983,10 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     else
         hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
                            (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
+    if (h->fork_pending) {                  // the slivers start after the root tests (LPC_FORK_ROOTS_MIN)
+        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        h->fork_pending = false;
+    }
     RayBase ray;
     RETIF(ray_base(h, in, rs, n, &ray));
     SpillArgs SP;
@@ -1173,9 +1177,14 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // add to the slots with order-independent atomics); joined at the end
     hipStream_t ss = h->stream;
     const bool side = nsp > 0 && h->stream2 && h->ev_side[0];
+    // LPC_FORK_ROOTS_MIN: from this population size the slivers wait for the root
+    // tests too (fork recorded after k_roots_s in run_queue): a large population's
+    // long-lived sliver waves otherwise hold the CUs while k_roots_s, which the walk
+    // waits for, gets what is left
+    h->fork_pending = side && h->sliver_late && n >= h->fork_roots_min;
     if (side) {
         ss = h->stream2;
-        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        if (!h->fork_pending) HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
     }
     // on the side stream the sliver kernels are launched after the hierarchy
     // stage's (the host reaches k_roots / k_rootwalk sooner; the slivers still
@@ -1200,6 +1209,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     };
     const bool late = side && h->sliver_late;
     if (!late) RETIF(launch_slivers());
+    auto fork_now = [&]() -> int {            // the deferred fork, if run_queue did not record it
+        if (h->fork_pending) { HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream)); h->fork_pending = false; }
+        return 0;
+    };
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     // root items (default): the item encoding's bounds
@@ -1256,6 +1269,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         h->prof_launches += 1;
         h->prof_pairs += n * (int64_t)h->M;
     }
+    RETIF(fork_now());
     if (late) RETIF(launch_slivers());
     if (side) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
     if (st_user) {
@@ -1346,19 +1360,7 @@ int lpc_open(int device, lpc_handle **out)
     lpc_handle *h = new lpc_handle();
     h->device = device;
     e = hipSetDevice(device);
-    // LPC_STREAM_PRIO (default 1): the main stream at the highest priority, the
-    // sliver side stream at the lowest, so the hierarchy stage's launches (root
-    // tests, walk, hand-over levels) get the CUs first and the slivers' long-lived
-    // waves fill what is left instead of holding the GPU ahead of the walk
-    const char *prio_env = getenv("LPC_STREAM_PRIO");
-    h->stream_prio = prio_env ? atoi(prio_env) != 0 : true;
-    int prio_lo = 0, prio_hi = 0;
-    if (e == hipSuccess && h->stream_prio && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess)
-        prio_lo = prio_hi = 0;
-    h->prio_lo = prio_lo;
-    if (e == hipSuccess)
-        e = h->stream_prio ? hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi)
-                           : hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
         return set_err(nullptr, LPC_E_HIP, std::string("stream: ") + hipGetErrorString(e));
@@ -1402,6 +1404,7 @@ int lpc_open(int device, lpc_handle **out)
     h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
     h->roots_pb3 = (int)std::max<int64_t>(1, env_int("LPC_ROOTS_PB3", h->roots_pb3));
+    h->fork_roots_min = env_int("LPC_FORK_ROOTS_MIN", h->fork_roots_min);
     h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
     h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);
     h->spec = env_int("LPC_SPEC", h->spec) != 0;
@@ -1441,9 +1444,7 @@ int lpc_open(int device, lpc_handle **out)
     h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
     if (env_int("LPC_SIDE_STREAM", 1) != 0) {
         const unsigned evf = hipEventDisableTiming;   // the side stream's fork / join events
-        const hipError_t es = h->stream_prio ? hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, h->prio_lo)
-                                             : hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking);
-        if (es != hipSuccess ||
+        if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
             h->stream2 = nullptr;       // all on the main stream
