@@ -102,6 +102,28 @@ struct RaysOut {
     int32_t *pmid;
 };
 
+// The sliver-list tests of one launch (k_slivers, or k_rootwalk's tail when
+// merged: LPC_SLIVER_MERGE).  Device-sized launches (nd) read n and max |D|^2
+// (dm2d) on the device.  nsp = 0: no sliver work.
+struct SliverArgs {
+    RaysIn R;
+    const float *rs;
+    int64_t n;
+    const int32_t *perm;
+    const lpc::PacketRec *pk;
+    const lpc::SliverRec *srec;
+    const Piece *pieces;
+    int nsp;                          // sliver pieces of the launch (the prefix its rays can reach)
+    int ppw;                          // packets per (wave, piece) unit
+    float eps, max_ray_len, dmax;
+    unsigned long long *skey;
+    int32_t *scnt;
+    unsigned long long *stats;
+    const long long *nd;
+    const unsigned *dm2d;
+    uint32_t *tmask;
+};
+
 struct ShadeOutPtrs {                 // per-ray outputs of k_shade (SoA)
     float *destx, *desty, *destz, *pw;
     int32_t *imid, *meas;

@@ -968,6 +968,10 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
     }
 }
 
+static __device__ __forceinline__ void sliver_group(const SliverArgs &A, int64_t n, float dmax, int64_t w0,
+                                                    int64_t w1, int piece);
+static __device__ __forceinline__ void sliver_launch_size(const SliverArgs &A, int64_t &n, float &dmax);
+
 // k_rootwalk: the root items (k_roots), grid-stride, one item per wave at a
 // time -- k_intersect's (packet, piece) waves without the waves whose root test
 // fails.  A wave that exceeds the hand-over budget queues its remaining
@@ -982,7 +986,8 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
                                                      const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
                                                      unsigned long long *__restrict__ skey, int32_t *__restrict__ scnt,
                                                      unsigned long long *__restrict__ stats, QueueArgs Q,
-                                                     SpillArgs out, const long long *__restrict__ nd)
+                                                     SpillArgs out, const long long *__restrict__ nd,
+                                                     SliverArgs SA)
 {
     __shared__ WaveLds lds;
     if (nd) n = *nd;
@@ -1034,6 +1039,21 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
         trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot, eps,
                                                 max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
     }
+    // merged sliver tests (LPC_SLIVER_MERGE): (packet group, sliver piece) units
+    // grid-stride after the root items, so the waves whose items end early take
+    // them -- no second stream whose long-lived waves would hold the CUs
+    if (SA.nsp > 0) {
+        int64_t ns;
+        float dmax;
+        sliver_launch_size(SA, ns, dmax);
+        const int64_t npk = (ns + 127) / 128, ppw = SA.ppw;
+        const int64_t units = ((npk + ppw - 1) / ppw) * SA.nsp;
+        for (int64_t u = blockIdx.x; u < units; u += stride) {
+            const int64_t g = u / SA.nsp;
+            const int64_t w0 = g * ppw;
+            sliver_group(SA, ns, dmax, w0, min(w0 + ppw, npk), (int)(u - g * SA.nsp));
+        }
+    }
 }
 
 // k_slivers: the run's slivers (line filter) for packets of 128 rays (two per
@@ -1046,45 +1066,29 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
 // Device-sized launch (nd != NULL): the population size and its max |D|^2 (dm2d,
 // float bits) read on the device, ppw = the packets over the grid's waves, and
 // every sliver piece in grid.y (a piece whose slivers no ray can pass exits).
-__global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                 const int32_t *__restrict__ perm,
-                                                 const PacketRec *__restrict__ pk,
-                                                 const SliverRec *__restrict__ srec,
-                                                 const Piece *__restrict__ pieces, float eps, float max_ray_len,
-                                                 unsigned long long *__restrict__ skey,
-                                                 int32_t *__restrict__ scnt,
-                                                 unsigned long long *__restrict__ stats, int ppw,
-                                                 float dmax, const long long *__restrict__ nd,
-                                                 const unsigned *__restrict__ dm2d, uint32_t *__restrict__ tmask)
+// One wave: packets [w0, w1) of 128 rays against sliver piece `piece`.
+static __device__ __forceinline__ void sliver_group(const SliverArgs &A, int64_t n, float dmax, int64_t w0,
+                                                    int64_t w1, int piece)
 {
     const int lane = threadIdx.x & 63;
-    if (nd) {
-        n = *nd;
-        const double d2 = (double)__uint_as_float(*dm2d);
-        dmax = d2 >= 0.0 ? (float)fmin(sqrt(d2 * (1.0 + 1e-5)), (double)INFINITY) : INFINITY;   // as run_intersect
-        ppw = (int)max((int64_t)1, ((n + 127) / 128 + (int64_t)gridDim.x * 4 - 1) / ((int64_t)gridDim.x * 4));
-    }
-    const int64_t npk = (n + 127) / 128;
-    const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
-    if (w0 >= npk) return;
-    const int64_t w1 = min(w0 + (int64_t)ppw, npk);
-    const Piece P = pieces[blockIdx.y];
+    const Piece P = A.pieces[piece];
     const int32_t j = P.s_lo + lane;
     SliverRec S;
-    if (j < P.s_hi) S = srec[j];
+    if (j < P.s_hi) S = A.srec[j];
     else { memset(&S, 0, sizeof(S)); S.a = NAN; S.idx = -1; }
     if (!(S.dmin <= dmax)) S.a = NAN;             // no ray of the launch can pass its DEN test
     if (!any_lane(S.a == S.a)) return;            // the whole piece culled
     const int64_t o = (int64_t)P.slot * n;
+    const float eps = A.eps, max_ray_len = A.max_ray_len;
     uint32_t n_tests = 0, n_exact = 0;
     for (int64_t w = w0; w < w1; ++w) {
-        const PacketRec Q = pk[w];
+        const PacketRec Q = A.pk[w];
         uint64_t m = __builtin_amdgcn_ballot_w64(packet_sliver_test(Q, S));
         if (!m) continue;
         const int64_t s0 = w * 128 + lane, s1 = s0 + 64;
         f3 O0, O1, D0, D1;
-        load_ray(R, rs, n, s0 < n ? s0 : n - 1, O0, D0);
-        load_ray(R, rs, n, s1 < n ? s1 : n - 1, O1, D1);
+        load_ray(A.R, A.rs, n, s0 < n ? s0 : n - 1, O0, D0);
+        load_ray(A.R, A.rs, n, s1 < n ? s1 : n - 1, O1, D1);
         const f2 ox = {O0.x, O1.x}, oy = {O0.y, O1.y}, oz = {O0.z, O1.z};
         const f2 dx = {D0.x, D1.x}, dy = {D0.y, D1.y}, dz = {D0.z, D1.z};
         const f2 dl = {sqrtf(D0.x * D0.x + D0.y * D0.y + D0.z * D0.z), sqrtf(D1.x * D1.x + D1.y * D1.y + D1.z * D1.z)};
@@ -1118,16 +1122,42 @@ __global__ __launch_bounds__(256) void k_slivers(RaysIn R, const float *__restri
             if (r1) mt_accumulate(O1, D1, V0, E1, E2, idx, eps, t1, i1, c1);
             n_exact += (uint32_t)r0 + (uint32_t)r1;
         }
-        if (s0 < n) slot_flush(skey, scnt, o, perm ? perm[s0] : s0, t0, i0, c0, tmask, P.slot);
-        if (s1 < n) slot_flush(skey, scnt, o, perm ? perm[s1] : s1, t1, i1, c1, tmask, P.slot);
+        if (s0 < n) slot_flush(A.skey, A.scnt, o, A.perm ? A.perm[s0] : s0, t0, i0, c0, A.tmask, P.slot);
+        if (s1 < n) slot_flush(A.skey, A.scnt, o, A.perm ? A.perm[s1] : s1, t1, i1, c1, A.tmask, P.slot);
     }
-    if (stats) {
+    if (A.stats) {
         for (int q = 32; q >= 1; q >>= 1) n_exact += __shfl_xor(n_exact, q, 64);
         if (lane == 0) {
-            atomicAdd(&stats[1], (unsigned long long)n_tests);
-            atomicAdd(&stats[3], (unsigned long long)n_exact);
+            atomicAdd(&A.stats[1], (unsigned long long)n_tests);
+            atomicAdd(&A.stats[3], (unsigned long long)n_exact);
         }
     }
+}
+
+// The launch's n and max |D| (device-sized: from the device, as run_intersect
+// computes them on the host).
+static __device__ __forceinline__ void sliver_launch_size(const SliverArgs &A, int64_t &n, float &dmax)
+{
+    n = A.n;
+    dmax = A.dmax;
+    if (A.nd) {
+        n = *A.nd;
+        const double d2 = (double)__uint_as_float(*A.dm2d);
+        dmax = d2 >= 0.0 ? (float)fmin(sqrt(d2 * (1.0 + 1e-5)), (double)INFINITY) : INFINITY;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_slivers(SliverArgs A)
+{
+    int64_t n;
+    float dmax;
+    sliver_launch_size(A, n, dmax);
+    int64_t ppw = A.ppw;
+    if (A.nd) ppw = max((int64_t)1, ((n + 127) / 128 + (int64_t)gridDim.x * 4 - 1) / ((int64_t)gridDim.x * 4));
+    const int64_t npk = (n + 127) / 128;
+    const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ppw;
+    if (w0 >= npk) return;
+    sliver_group(A, n, dmax, w0, min(w0 + ppw, npk), (int)blockIdx.y);
 }
 
 // k_gather from the 32-byte rows k_raykey wrote: one cache line per ray instead

@@ -113,6 +113,8 @@ struct lpc_handle {
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     int roots_pb3 = 1;
+    int sliver_merge = 0;                           // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid
+    int64_t sliver_merge_ppw = 4;                   // LPC_SLIVER_MERGE_PPW: packets per merged unit
     int64_t fork_roots_min = INT64_MAX;             // LPC_FORK_ROOTS_MIN: slivers after k_roots_s from this population
     bool fork_pending = false;                      // run_intersect -> run_queue: record the side fork after the root tests                              // LPC_ROOTS_PB3: k_roots_s packets per block with >= 3 tasks per packet
     bool roots_gate = true;                         // LPC_ROOTS_GATE: k_roots_s tests the run roots first
@@ -933,7 +935,7 @@ static int check_qerr(lpc_handle *h)
 // and hands heavy subtrees to the k_spill levels.
 static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
                      const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
-                     unsigned long long *stats, const DevSize *ds = nullptr)
+                     unsigned long long *stats, const DevSize *ds = nullptr, const SliverArgs *merged = nullptr)
 {
     // device-sized (ds): n is the expected size (grids), the bound sizes the shards
     const int64_t npk = (n + 63) / 64;
@@ -987,6 +989,16 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
         h->fork_pending = false;
     }
+    // merged sliver tests (LPC_SLIVER_MERGE): the packet bounds before the walk,
+    // on this stream; the walk's waves take the (packet group, piece) units
+    SliverArgs SA;
+    memset(&SA, 0, sizeof(SA));
+    if (merged) {
+        SA = *merged;
+        const int64_t npkx = (n + 127) / 128;
+        hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, h->stream, in, rs, n,
+                           (PacketRec *)h->w_pk.p, ds ? ds->nd : nullptr);
+    }
     RayBase ray;
     RETIF(ray_base(h, in, rs, n, &ray));
     SpillArgs SP;
@@ -1002,7 +1014,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
 #define LPC_LAUNCH_WALK(WW, NT, PF, HF, B)                                                                       \
     hipExtLaunchKernelGGL((k_rootwalk<WW, PF, HF, B>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm, \
                           (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,   \
-                          stats, Q, SP, ds ? ds->nd : nullptr)
+                          stats, Q, SP, ds ? ds->nd : nullptr, SA)
     if (h->built_w == 8) {
         if (stats) LPC_LAUNCH_WALK(8, Node8, true, false, 1);
         else if (walk_batched(h)) {
@@ -1176,7 +1188,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // the slivers run beside the hierarchy stage on a second stream (both only
     // add to the slots with order-independent atomics); joined at the end
     hipStream_t ss = h->stream;
-    const bool side = nsp > 0 && h->stream2 && h->ev_side[0];
+    // LPC_SLIVER_MERGE: the sliver units run in the walk's own grid (k_rootwalk's
+    // tail) on this stream instead of k_slivers on the side stream
+    const bool merge_try = h->sliver_merge && nsp > 0 && h->queue == 2 && !h->prof_waves && !h->xcd_claim;
+    const bool side = !merge_try && nsp > 0 && h->stream2 && h->ev_side[0];
     // LPC_FORK_ROOTS_MIN: from this population size the slivers wait for the root
     // tests too (fork recorded after k_roots_s in run_queue): a large population's
     // long-lived sliver waves otherwise hold the CUs while k_roots_s, which the walk
@@ -1189,6 +1204,15 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // on the side stream the sliver kernels are launched after the hierarchy
     // stage's (the host reaches k_roots / k_rootwalk sooner; the slivers still
     // run beside k_rootwalk)
+    auto sliver_args = [&](int64_t ppw) {
+        SliverArgs A;
+        memset(&A, 0, sizeof(A));
+        A.R = in; A.rs = rs; A.n = n; A.perm = perm; A.pk = (const PacketRec *)h->w_pk.p;
+        A.srec = (const SliverRec *)h->d_srec.p; A.pieces = (const Piece *)pt->spieces.p; A.nsp = nsp;
+        A.ppw = (int)ppw; A.eps = eps; A.max_ray_len = max_ray_len; A.dmax = dmax_k;
+        A.skey = skey; A.scnt = scnt; A.stats = stats; A.nd = nd_dev; A.dm2d = dm2_dev; A.tmask = h->tm_cur;
+        return A;
+    };
     auto launch_slivers = [&]() -> int {
         if (side) HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_side[0], 0));
         if (nsp > 0) {
@@ -1199,16 +1223,14 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
             hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
                                (PacketRec *)h->w_pk.p, nd_dev);
-            hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, ss, in, rs, n, perm, (const PacketRec *)h->w_pk.p,
-                               (const SliverRec *)h->d_srec.p, (const Piece *)pt->spieces.p, eps, max_ray_len, skey,
-                               scnt, stats, (int)ppw, dmax_k, nd_dev, dm2_dev, h->tm_cur);
+            hipLaunchKernelGGL(k_slivers, sg, dim3(256), 0, ss, sliver_args(ppw));
             HIPCHK(h, hipGetLastError());
         }
         if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
         return 0;
     };
     const bool late = side && h->sliver_late;
-    if (!late) RETIF(launch_slivers());
+    if (!late && !merge_try) RETIF(launch_slivers());
     auto fork_now = [&]() -> int {            // the deferred fork, if run_queue did not record it
         if (h->fork_pending) { HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream)); h->fork_pending = false; }
         return 0;
@@ -1216,7 +1238,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
     // root items (default): the item encoding's bounds
-    bool qpath = false;
+    bool qpath = false, merged = false;
     if (h->queue == 2 && !h->prof_waves) {
         PieceTable *ptq;
         RETIF(piece_table(h, n, &ptq, q_level(h, n)));
@@ -1226,9 +1248,15 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                 h->K <= LPC_Q_MAX_SLOTS;
         if (qpath) {
             pt = ptq;                   // same sliver pieces at every level
-            if (pt->npieces > 0) RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds));
+            if (pt->npieces > 0) {
+                const SliverArgs SAm = sliver_args(std::max<int64_t>(1, h->sliver_merge_ppw));
+                RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds,
+                                merge_try ? &SAm : nullptr));
+                merged = merge_try;
+            }
         }
     }
+    if (merge_try && !merged) RETIF(launch_slivers());     // no walk to carry them: on this stream
     if (ds && !qpath) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the root-item path");
     if (pt->npieces > 0 && !qpath) {
         // k_intersect: one wave per (packet, piece) (LPC_QUEUE=0, per-wave records)
@@ -1405,6 +1433,8 @@ int lpc_open(int device, lpc_handle **out)
     h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
     h->roots_pb3 = (int)std::max<int64_t>(1, env_int("LPC_ROOTS_PB3", h->roots_pb3));
     h->fork_roots_min = env_int("LPC_FORK_ROOTS_MIN", h->fork_roots_min);
+    h->sliver_merge = (int)env_int("LPC_SLIVER_MERGE", h->sliver_merge);
+    h->sliver_merge_ppw = env_int("LPC_SLIVER_MERGE_PPW", h->sliver_merge_ppw);
     h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
     h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);
     h->spec = env_int("LPC_SPEC", h->spec) != 0;

@@ -110,6 +110,10 @@ _POLICIES = [
     dict(LPC_XCD_CLAIM="1"), dict(LPC_XCD_CLAIM="1", LPC_Q_TARGET="1000000"),
     dict(LPC_XCD_CLAIM="1", LPC_BUDGET="3"), dict(LPC_BUDGET_SMALL="0"), dict(LPC_BUDGET_SMALL="5"),
     dict(LPC_HALF_SMALL="1"), dict(LPC_DS_CAP="0"),
+    # slivers in the walk's grid (k_rootwalk's tail), or after the root tests
+    dict(LPC_SLIVER_MERGE="1"), dict(LPC_SLIVER_MERGE="1", LPC_SLIVER_MERGE_PPW="1"),
+    dict(LPC_SLIVER_MERGE="1", LPC_SLIVER_MERGE_PPW="33", LPC_SLIVER_CULL="0"),
+    dict(_OLD, LPC_SLIVER_MERGE="1"), dict(LPC_FORK_ROOTS_MIN="0"), dict(LPC_THIN="0"), dict(LPC_THIN="25"),
     # the k_intersect alternative and its knobs
     dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
     dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
@@ -649,3 +653,30 @@ def test_resorted_populations_keys(monkeypatch, env):
         r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
         return r[np.lexsort(r.T[::-1])]
     np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
+
+
+@pytest.mark.parametrize("cfg", [dict(LPC_SLIVER_MERGE="1"), dict(LPC_SLIVER_MERGE="1", LPC_SLIVER_MERGE_PPW="1"),
+                                 dict(LPC_THIN="0"), dict(LPC_THIN="25"), dict(LPC_FORK_ROOTS_MIN="0"),
+                                 dict(LPC_SLIVER_MERGE="1", LPC_RESORT_MIN="4096")])
+def test_eye_policies_identical(monkeypatch, cfg):
+    """The eye (the scene with thin triangles on the sliver path): whole traces in
+    results mode under the sliver placement policies equal the default's, every
+    results tuple element for element (the default itself equals the reference's
+    kernels: test_trace_results_match_reference)."""
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    sc = scenes.eye(n=3000, seed=6)
+
+    def trace():
+        tr = CL_Tracer(device=0)
+        res = tr.iterative_tracer(light_source=sc.sources, meshes=sc.meshes, trace_iterations=sc.iterations,
+                                  trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env)
+        return [tuple(np.array(a) for a in r) for r in res]
+
+    base = trace()
+    for k, v in cfg.items():
+        monkeypatch.setenv(k, v)
+    got = trace()
+    assert len(got) == len(base) >= 3
+    for it, (a, b) in enumerate(zip(got, base)):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y, err_msg=f"it{it} {cfg}")
