@@ -149,14 +149,14 @@ struct lpc_handle {
     uint32_t *tm_cur = nullptr;                     // this launch's masks (the walk writes, k_shade_stage reads)
     // launch policy (defaults; LPC_* environment overrides read at lpc_open)
     int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
-    int spill_budget = 24;                          // node visits before a wave hands over (0 off)
+    int spill_budget = 20;                          // node visits before a wave hands over (0 off)
     int spill_budget_small = -1;                    // ... for populations below spill_small_n rays (-1: spill_budget)
     int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
     int64_t spill_large_n = 0;                      // 0: spill_large_per_tri x triangles
     int64_t spill_large_per_tri = 16;
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
-    int spill_levels = 4;                           // k_spill launches (hand-over depth)
+    int spill_levels = 3;                           // k_spill launches (hand-over depth)
     int spill_levels_small = 1;                     // ... for populations below spill_small_n rays
     int64_t spill_small_n = 262144;
     int spill_shrink = 1;                           // level l grid = spill_blocks >> (shrink * l) ...
