@@ -29,6 +29,12 @@ atomics)
   # where the walk's writes go: memory-side atomic requests (64 B each) against
   # all write requests, per launch (one bench step: the primary and two secondaries)
   ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_ATOMIC_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum -d $R/$O/pmc_atomics -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu --no-configs > $R/$O/pmc_atomics.log 2>&1 ) || { echo "pmc atomics failed"; exit 1; } ;;
+eye)
+  # kernel trace of one eye trace (2 M rays, 16 iterations) after two warm-up traces
+  prof 300 kte --kernel-trace --stats -d $R/$O/kte -o kt --output-format csv -- python3 $R/tools/cfg_trace.py eye 2000000 16 1 > $O/kte.log 2>&1 || { echo kte failed; exit 1; } ;;
+all)
+  # the round's evidence: GPU tests, PMC passes, kernel traces, the bench line
+  for st in tests pmc profile eye bench; do bash $0 $st || exit 1; done ;;
 hostgap)
   LPC_HOSTPROF=1 run 120 host_gap.log python -u tools/host_gap.py 20 ;;
 results)
