@@ -80,6 +80,48 @@ class CL_Tracer:
         self.hist_data = None
 
     # ------------------------------------------------------------------------
+    def _flatten(self, meshes):
+        """flatten_meshes(meshes), reused when this tracer last flattened the same
+        mesh objects and their vertex / triangle tables and materials still hold
+        the same bits (compared with kept copies); meshes whose tables are not
+        numpy arrays are flattened every time."""
+        def bits(a):
+            a = np.ascontiguousarray(a)
+            return a.view(f"u{a.itemsize}") if a.dtype.kind in "fiu" and a.itemsize in (1, 2, 4, 8) else None
+
+        def mat(m):
+            b = m.getMaterialBuf()
+            return tuple(float(np.float32(b.get(k))) for k in ("type", "IOR", "R", "dissipation"))
+
+        cache = getattr(self, "_flat_cache", None)
+        if cache is not None and len(cache[0]) == len(meshes):
+            same = True
+            for m, (mid, v, t, mt) in zip(meshes, cache[0]):
+                V, T = getattr(m, "vertices", None), getattr(m, "triangles", None)
+                if (id(m) != mid or type(V) is not np.ndarray or type(T) is not np.ndarray or
+                        V.shape != v.shape or T.shape != t.shape or mat(m) != mt):
+                    same = False
+                    break
+                bv, bt = bits(V), bits(T)
+                if bv is None or bt is None or bv.dtype != v.dtype or bt.dtype != t.dtype or \
+                        not np.array_equal(bv, v) or not np.array_equal(bt, t):
+                    same = False
+                    break
+            if same:
+                return cache[1]
+        arrs = flatten_meshes(meshes)
+        keep = []
+        for m in meshes:
+            V, T = getattr(m, "vertices", None), getattr(m, "triangles", None)
+            bv = bits(V) if type(V) is np.ndarray else None
+            bt = bits(T) if type(T) is np.ndarray else None
+            if bv is None or bt is None:
+                keep = None
+                break
+            keep.append((id(m), bv.copy(), bt.copy(), mat(m)))
+        self._flat_cache = (keep, arrs) if keep is not None else None
+        return arrs
+
     def iterative_tracer(self, light_source, meshes, trace_iterations=100, trace_until_dissipated=0.99,
                          max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True):
         """Trace until ``trace_iterations`` bounces, until less than
@@ -106,7 +148,7 @@ class CL_Tracer:
         input_power = f32_sorted_sum(power)                            # :115
         pow_shape0 = power.shape
 
-        arrs = flatten_meshes(meshes)                                  # :121-151
+        arrs = self._flatten(meshes)                                   # :121-151
         ph["flatten"] = clk() - t_ph
         t_ph = clk()
         self.engine.upload_arrays(*arrs)                                # skipped for an unchanged scene

@@ -327,3 +327,33 @@ def test_pinned_pool_recycles_blocks(monkeypatch):
         assert res[1][0].shape == (1000, 4) and res[1][1].dtype == np.int32
     finally:
         gc.enable()
+
+
+def test_tracer_flatten_cache_follows_the_meshes():
+    """CL_Tracer reuses its last flatten only while the same mesh objects hold the
+    same vertex / triangle bits and materials; any change flattens again."""
+    import numpy as np
+    from lightpycl_amd import scenes
+    from lightpycl_amd.engine import flatten_meshes
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    sc = scenes.parabolic(n=10)
+    tr = CL_Tracer.__new__(CL_Tracer)
+    a = tr._flatten(sc.meshes)
+    assert tr._flatten(sc.meshes) is a
+
+    def fresh_equal(x):
+        return all(np.array_equal(p, q) and p.dtype == q.dtype for p, q in zip(x, flatten_meshes(sc.meshes)))
+    sc.meshes[1].translate([0, 0, 1e-3, 0])                 # new vertex table
+    b = tr._flatten(sc.meshes)
+    assert b is not a and fresh_equal(b)
+    v = sc.meshes[1].vertices
+    v[0, 0] = np.nextafter(v[0, 0], np.inf)                 # in place, one ulp
+    c = tr._flatten(sc.meshes)
+    assert c is not b and fresh_equal(c)
+    sc.meshes[1].setMaterial(mat_type="refractive", IOR=1.7)   # (a mirror keeps its reflectivity: the quirk)
+    d = tr._flatten(sc.meshes)
+    assert d is not c and fresh_equal(d)
+    e = tr._flatten(sc.meshes[::-1])                        # other order
+    assert e is not d
+    assert all(np.array_equal(p, q) for p, q in zip(e, flatten_meshes(sc.meshes[::-1])))
+
