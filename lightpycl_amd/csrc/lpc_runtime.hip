@@ -113,8 +113,8 @@ struct lpc_handle {
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     int roots_pb3 = 1;
-    int64_t sliver_merge = 4000001;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid for
-                                                    // populations >= this - 1 (0: never; 1: always)
+    int64_t sliver_merge = 4000000;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
+                                                    // this population size (0: always; -1: never)
     int64_t sliver_merge_ppw = 4;                   // LPC_SLIVER_MERGE_PPW: packets per merged unit
     int64_t fork_roots_min = INT64_MAX;             // LPC_FORK_ROOTS_MIN: slivers after k_roots_s from this population
     bool fork_pending = false;                      // run_intersect -> run_queue: record the side fork after the root tests                              // LPC_ROOTS_PB3: k_roots_s packets per block with >= 3 tasks per packet
@@ -1191,7 +1191,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     hipStream_t ss = h->stream;
     // LPC_SLIVER_MERGE: the sliver units run in the walk's own grid (k_rootwalk's
     // tail) on this stream instead of k_slivers on the side stream
-    const bool merge_try = h->sliver_merge > 0 && n >= (int64_t)h->sliver_merge - 1 && nsp > 0 && h->queue == 2 &&
+    const bool merge_try = h->sliver_merge >= 0 && n >= h->sliver_merge && nsp > 0 && h->queue == 2 &&
                            !h->prof_waves && !h->xcd_claim;
     const bool side = !merge_try && nsp > 0 && h->stream2 && h->ev_side[0];
     // LPC_FORK_ROOTS_MIN: from this population size the slivers wait for the root

@@ -111,9 +111,9 @@ _POLICIES = [
     dict(LPC_XCD_CLAIM="1", LPC_BUDGET="3"), dict(LPC_BUDGET_SMALL="0"), dict(LPC_BUDGET_SMALL="5"),
     dict(LPC_HALF_SMALL="1"), dict(LPC_DS_CAP="0"),
     # slivers in the walk's grid (k_rootwalk's tail), or after the root tests
-    dict(LPC_SLIVER_MERGE="1"), dict(LPC_SLIVER_MERGE="1", LPC_SLIVER_MERGE_PPW="1"),
-    dict(LPC_SLIVER_MERGE="1", LPC_SLIVER_MERGE_PPW="33", LPC_SLIVER_CULL="0"),
-    dict(_OLD, LPC_SLIVER_MERGE="1"), dict(LPC_FORK_ROOTS_MIN="0"), dict(LPC_THIN="0"), dict(LPC_THIN="25"),
+    dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="1"),
+    dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="33", LPC_SLIVER_CULL="0"),
+    dict(_OLD, LPC_SLIVER_MERGE="0"), dict(LPC_FORK_ROOTS_MIN="0"), dict(LPC_THIN="0"), dict(LPC_THIN="25"),
     # the k_intersect alternative and its knobs
     dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
     dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
@@ -655,9 +655,9 @@ def test_resorted_populations_keys(monkeypatch, env):
     np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
 
 
-@pytest.mark.parametrize("cfg", [dict(LPC_SLIVER_MERGE="1"), dict(LPC_SLIVER_MERGE="1", LPC_SLIVER_MERGE_PPW="1"),
+@pytest.mark.parametrize("cfg", [dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="1"),
                                  dict(LPC_THIN="0"), dict(LPC_THIN="25"), dict(LPC_FORK_ROOTS_MIN="0"),
-                                 dict(LPC_SLIVER_MERGE="1", LPC_RESORT_MIN="4096")])
+                                 dict(LPC_SLIVER_MERGE="0", LPC_RESORT_MIN="4096")])
 def test_eye_policies_identical(monkeypatch, cfg):
     """The eye (the scene with thin triangles on the sliver path): whole traces in
     results mode under the sliver placement policies equal the default's, every
