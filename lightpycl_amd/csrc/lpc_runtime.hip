@@ -111,7 +111,7 @@ struct lpc_handle {
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
-    int roots_s = 8;                                // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
+    int roots_s = 16;                               // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     int roots_pb3 = 1;
     int64_t sliver_merge = 4000000;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
                                                     // this population size (0: always; -1: never)
