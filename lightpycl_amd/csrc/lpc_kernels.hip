@@ -1176,6 +1176,82 @@ __global__ __launch_bounds__(256) void k_gather_aos(const float4 *__restrict__ a
     if (full) { rs[6 * n + s] = b.z; rs[7 * n + s] = b.w; }
 }
 
+// k_gather_aos with the root tests of k_roots_s fused in (one task per packet:
+// at most 64 pieces, no run gate): 16 packets per 1024-thread block, each wave
+// gathers its packet's 64 rays and tests them against the pieces from the rows
+// it just read (the values k_roots_s would load from the gathered copy), then the
+// block reserves its items with one atomic, as k_roots_s does.  Lanes past n add
+// nothing (k_roots_s tests ray n - 1 there, which its own lane already covers).
+template <bool HALF>
+__global__ __launch_bounds__(1024) void k_gather_roots(const float4 *__restrict__ aos, int64_t n,
+                                                       const int32_t *__restrict__ perm, float *__restrict__ rs,
+                                                       int full, const Piece *__restrict__ pieces, int npieces,
+                                                       QueueArgs Q)
+{
+    __shared__ float4 s_pc[64];
+    __shared__ float s_pa[64];
+    __shared__ unsigned long long s_m[16];
+    __shared__ uint32_t s_off[17];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((int)threadIdx.x < npieces) {
+        const Piece &P = pieces[threadIdx.x];
+        s_pc[threadIdx.x] = make_float4(P.cx, P.cy, P.cz, P.negB);
+        s_pa[threadIdx.x] = P.negA;
+    }
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = s < n;
+    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
+    if (in) {
+        const int64_t q = perm[s];
+        a = aos[2 * q];
+        b = aos[2 * q + 1];
+        rs[s] = a.x; rs[n + s] = a.y; rs[2 * n + s] = a.z;
+        rs[3 * n + s] = a.w; rs[4 * n + s] = b.x; rs[5 * n + s] = b.y;
+        if (full) { rs[6 * n + s] = b.z; rs[7 * n + s] = b.w; }
+    }
+    __syncthreads();
+    const int64_t w = (int64_t)blockIdx.x * nw + wv;       // this wave's packet
+    uint64_t ml = 0;
+    if (in) {
+        const f3 O = mk3(a.x, a.y, a.z), D = mk3(a.w, b.x, b.y);
+        float nx, ny, nz;
+        unit_dir(D, nx, ny, nz);
+        int p = 0;
+        for (; p + 1 < npieces; p += 2) {
+            const float4 c0 = s_pc[p], c1 = s_pc[p + 1];
+            const lpc_f2 cx = {c0.x, c1.x}, cy = {c0.y, c1.y}, cz = {c0.z, c1.z}, nb = {c0.w, c1.w};
+            const lpc_f2 na = {s_pa[p], s_pa[p + 1]};
+            const lpc_f2 d = HALF ? filter_test2h(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz)
+                                  : filter_test2(cx, cy, cz, nb, na, O.x, O.y, O.z, nx, ny, nz);
+            ml |= ((uint64_t)(d.x <= 0.0f) << p) | ((uint64_t)(d.y <= 0.0f) << (p + 1));
+        }
+        if (p < npieces) {
+            const float4 c = s_pc[p];
+            const float d = HALF ? filter_testh(c.x, c.y, c.z, c.w, s_pa[p], O.x, O.y, O.z, nx, ny, nz)
+                                 : filter_test(c.x, c.y, c.z, c.w, s_pa[p], O.x, O.y, O.z, nx, ny, nz);
+            ml |= (uint64_t)(d <= 0.0f) << p;
+        }
+    }
+    const uint64_t m = wave_or64(ml);
+    if (lane == 0) s_m[wv] = m;
+    __syncthreads();
+    const int c = q_shard((uint32_t)blockIdx.x);
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int k = 0; k < nw; ++k) { s_off[k] = tot; tot += (uint32_t)__builtin_popcountll(s_m[k]); }
+        s_off[nw] = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(c), tot) : 0u;
+    }
+    __syncthreads();
+    if ((m >> lane) & 1ull) {
+        const uint32_t pos = s_off[nw] + s_off[wv] + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (pos < Q.rcap)
+            Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)pieces[lane].root,
+                                                       (uint32_t)pieces[lane].slot);
+        else
+            atomicOr(Q.err, 2u);
+    }
+}
+
 // Slot initial state: slots a run flushes into start at (max_ray_len, idx -1,
 // count 0); slots no run writes keep the reference's initial scratch
 // (max_ray_len, idx 0, count 0).  Also empties the launch's origin box (misc).

@@ -113,6 +113,7 @@ struct lpc_handle {
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 16;                               // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     int roots_pb3 = 1;
+    bool gather_roots = false;                      // LPC_GATHER_ROOTS: k_gather_roots (gather + root tests)
     int64_t sliver_merge = 4000000;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
                                                     // this population size (0: always; -1: never)
     int64_t sliver_merge_ppw = 4;                   // LPC_SLIVER_MERGE_PPW: packets per merged unit
@@ -931,12 +932,14 @@ static int check_qerr(lpc_handle *h)
     return e ? q_failed(h) : 0;
 }
 
-// The root-item form of the hierarchy stage (default): k_roots* write the
-// (packet, piece) items whose root test passes, k_rootwalk walks them grid-stride
-// and hands heavy subtrees to the k_spill levels (DESIGN.md section 5).
-static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
-                     const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
-                     unsigned long long *stats, const DevSize *ds = nullptr, const SliverArgs *merged = nullptr)
+// The root-item queue of a launch of n rays: shard capacity, buffer, arguments.
+struct QueueShape {
+    int64_t npk, rblocks, rs_blocks;
+    int rs_S, rs_pb;
+    bool roots_s;
+};
+static int queue_args(lpc_handle *h, int64_t n, const PieceTable *pt, const DevSize *ds, QueueArgs *Qo,
+                      QueueShape *sh)
 {
     // device-sized (ds): n is the expected size (grids), the bound sizes the shards
     const int64_t npk = (n + 63) / 64;
@@ -953,6 +956,9 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     // overflow through Q.err instead of dropping items silently)
     int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
                             ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+    // k_gather_roots: 16 packets per block
+    rcap = std::max<int64_t>(rcap, ((((npk + 15) / 16) + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 16 *
+                                       (int64_t)pt->npieces);
     const bool xpiece = h->xcd_claim && roots_s;
     if (xpiece)                         // a shard takes every packet's items of its pieces (piece % 8)
         rcap = std::max<int64_t>(rcap, rs_vblocks * rs_pb *
@@ -966,11 +972,35 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     Q.rcap = (uint32_t)rcap;
     Q.xpiece = xpiece ? 1 : 0;
     Q.claim = h->xcd_claim ? 1 : 0;
+    *Qo = Q;
+    sh->npk = npk; sh->rblocks = rblocks; sh->rs_blocks = rs_blocks; sh->rs_S = rs_S; sh->rs_pb = rs_pb;
+    sh->roots_s = roots_s;
+    return 0;
+}
+
+// The root-item form of the hierarchy stage (default): k_roots* write the
+// (packet, piece) items whose root test passes, k_rootwalk walks them grid-stride
+// and hands heavy subtrees to the k_spill levels (DESIGN.md section 5).
+// roots_done: k_gather_roots already wrote the items (same queue arguments).
+static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
+                     const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
+                     unsigned long long *stats, const DevSize *ds = nullptr, const SliverArgs *merged = nullptr,
+                     bool roots_done = false)
+{
+    QueueArgs Q;
+    QueueShape sh;
+    RETIF(queue_args(h, n, pt, ds, &Q, &sh));
+    const int64_t npk = sh.npk, rblocks = sh.rblocks, rs_blocks = sh.rs_blocks;
+    const int rs_S = sh.rs_S, rs_pb = sh.rs_pb;
+    const bool roots_s = sh.roots_s;
+    const int64_t rcap = (int64_t)Q.rcap;
     if (h->host_prof)
         fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d groups %d S %d pb %d blocks %lld rcap %lld\n",
                 (long long)n, (long long)npk, (int)pt->npieces, (int)pt->ngroups, rs_S, rs_pb, (long long)rs_blocks,
                 (long long)rcap);
-    if (roots_s) {
+    if (roots_done) {
+        // k_gather_roots wrote the items
+    } else if (roots_s) {
         if (h->half_roots)
             hipLaunchKernelGGL(k_roots_s<true>, dim3((unsigned)std::max<int64_t>(rs_blocks, 1)), dim3(256), 0,
                                h->stream, in, rs, n, (const Piece *)pt->pieces.p, (int)pt->npieces,
@@ -1114,6 +1144,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     }
     const int32_t *perm = nullptr;
     const float *rs = nullptr;
+    bool roots_done = false;                    // k_gather_roots wrote the root items
     if (sorted) {
         // coherence order: rays of one wave share origin cell and direction
         // (key [scene-box origin cell | direction], k_raykey), gathered from the
@@ -1158,8 +1189,32 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                                                 b0, b1, h->stream));
         }
         perm = vout;
-        hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
-                           perm, (float *)h->w_rs.p, traced ? 1 : 0);
+        // LPC_GATHER_ROOTS: the gather with the root tests fused in, when the launch
+        // takes the root-item path with one task per packet and no run gate
+        if (h->gather_roots && h->queue == 2 && !h->prof_waves && !ds && !h->xcd_claim && h->roots_s > 0 &&
+            (nb + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS && (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES &&
+            h->K <= LPC_Q_MAX_SLOTS) {
+            PieceTable *ptf;
+            RETIF(piece_table(h, n, &ptf, q_level(h, n)));
+            if (ptf->npieces > 0 && ptf->npieces <= 64 && ptf->ngroups == 0) {
+                QueueArgs Qf;
+                QueueShape shf;
+                RETIF(queue_args(h, n, ptf, nullptr, &Qf, &shf));
+                const dim3 gg((unsigned)((n + 1023) / 1024));
+                if (h->half_roots)
+                    hipLaunchKernelGGL(k_gather_roots<true>, gg, dim3(1024), 0, h->stream, (const float4 *)h->w_aos.p,
+                                       n, perm, (float *)h->w_rs.p, traced ? 1 : 0, (const Piece *)ptf->pieces.p,
+                                       (int)ptf->npieces, Qf);
+                else
+                    hipLaunchKernelGGL(k_gather_roots<false>, gg, dim3(1024), 0, h->stream, (const float4 *)h->w_aos.p,
+                                       n, perm, (float *)h->w_rs.p, traced ? 1 : 0, (const Piece *)ptf->pieces.p,
+                                       (int)ptf->npieces, Qf);
+                roots_done = true;
+            }
+        }
+        if (!roots_done)
+            hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
+                               perm, (float *)h->w_rs.p, traced ? 1 : 0);
         rs = (const float *)h->w_rs.p;
     }
     if (traced) {
@@ -1253,7 +1308,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             if (pt->npieces > 0) {
                 const SliverArgs SAm = sliver_args(std::max<int64_t>(1, h->sliver_merge_ppw));
                 RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds,
-                                merge_try ? &SAm : nullptr));
+                                merge_try ? &SAm : nullptr, roots_done));
                 merged = merge_try;
             }
         }
@@ -1436,6 +1491,7 @@ int lpc_open(int device, lpc_handle **out)
     h->roots_pb3 = (int)std::max<int64_t>(1, env_int("LPC_ROOTS_PB3", h->roots_pb3));
     h->fork_roots_min = env_int("LPC_FORK_ROOTS_MIN", h->fork_roots_min);
     h->sliver_merge = env_int("LPC_SLIVER_MERGE", h->sliver_merge);
+    h->gather_roots = env_int("LPC_GATHER_ROOTS", h->gather_roots ? 1 : 0) != 0;
     h->sliver_merge_ppw = env_int("LPC_SLIVER_MERGE_PPW", h->sliver_merge_ppw);
     h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
     h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);

@@ -114,6 +114,8 @@ _POLICIES = [
     dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="1"),
     dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="33", LPC_SLIVER_CULL="0"),
     dict(_OLD, LPC_SLIVER_MERGE="0"), dict(LPC_FORK_ROOTS_MIN="0"), dict(LPC_THIN="0"), dict(LPC_THIN="25"),
+    # the gather with the root tests fused in
+    dict(LPC_GATHER_ROOTS="1"), dict(LPC_GATHER_ROOTS="1", LPC_HALF="4"), dict(LPC_GATHER_ROOTS="1", LPC_Q_TARGET="1"),
     # the k_intersect alternative and its knobs
     dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
     dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
@@ -657,7 +659,8 @@ def test_resorted_populations_keys(monkeypatch, env):
 
 @pytest.mark.parametrize("cfg", [dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="1"),
                                  dict(LPC_THIN="0"), dict(LPC_THIN="25"), dict(LPC_FORK_ROOTS_MIN="0"),
-                                 dict(LPC_SLIVER_MERGE="0", LPC_RESORT_MIN="4096")])
+                                 dict(LPC_SLIVER_MERGE="0", LPC_RESORT_MIN="4096"), dict(LPC_GATHER_ROOTS="1"),
+                                 dict(LPC_GATHER_ROOTS="1", LPC_RESORT_MIN="4096")])
 def test_eye_policies_identical(monkeypatch, cfg):
     """The eye (the scene with thin triangles on the sliver path): whole traces in
     results mode under the sliver placement policies equal the default's, every
@@ -680,3 +683,36 @@ def test_eye_policies_identical(monkeypatch, cfg):
     for it, (a, b) in enumerate(zip(got, base)):
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y, err_msg=f"it{it} {cfg}")
+
+
+@pytest.mark.parametrize("name,n", [("synthetic", 200000), ("eye", 30000), ("synthetic_dense", 60000)])
+def test_gather_roots_equals_separate_kernels(monkeypatch, name, n):
+    """k_gather_roots (the coherence gather with the root tests fused in) writes
+    the same root items as k_gather_aos + k_roots_s (their order inside a shard
+    differs; results do not depend on it): identical traces -- counts, per-mesh
+    power and the measured record element for element, in traced order -- with
+    re-sorted chained populations too (LPC_RESORT_MIN)."""
+    from lightpycl_amd.engine import Engine
+    sc = scenes.BUILDERS[name](n=n, seed=31)
+    o4, d4, pw = rays_of(sc)
+    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
+    out = []
+    for gr in ("1", "0"):
+        monkeypatch.setenv("LPC_GATHER_ROOTS", gr)
+        monkeypatch.setenv("LPC_RESORT_MIN", "20000")
+        e = Engine(0)
+        try:
+            e.upload_meshes(sc.meshes)
+            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+            for rep in range(2):
+                e.reset()
+                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
+            pos, p, mm = e.fetch_measured()
+            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, list(mp),
+                        pos, p, mm))
+        finally:
+            e.close()
+    a, b = out
+    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
+    for x, y in zip(a[3:], b[3:]):
+        np.testing.assert_array_equal(x, y)
