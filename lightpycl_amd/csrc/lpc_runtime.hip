@@ -113,7 +113,7 @@ struct lpc_handle {
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
     int roots_s = 16;                               // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
     int roots_pb3 = 1;
-    bool gather_roots = false;                      // LPC_GATHER_ROOTS: k_gather_roots (gather + root tests)
+    bool gather_roots = true;                       // LPC_GATHER_ROOTS: k_gather_roots (gather + root tests)
     int64_t sliver_merge = 4000000;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
                                                     // this population size (0: always; -1: never)
     int64_t sliver_merge_ppw = 4;                   // LPC_SLIVER_MERGE_PPW: packets per merged unit

@@ -115,7 +115,7 @@ _POLICIES = [
     dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="33", LPC_SLIVER_CULL="0"),
     dict(_OLD, LPC_SLIVER_MERGE="0"), dict(LPC_FORK_ROOTS_MIN="0"), dict(LPC_THIN="0"), dict(LPC_THIN="25"),
     # the gather with the root tests fused in
-    dict(LPC_GATHER_ROOTS="1"), dict(LPC_GATHER_ROOTS="1", LPC_HALF="4"), dict(LPC_GATHER_ROOTS="1", LPC_Q_TARGET="1"),
+    dict(LPC_GATHER_ROOTS="0"), dict(LPC_GATHER_ROOTS="1", LPC_HALF="4"), dict(LPC_GATHER_ROOTS="1", LPC_Q_TARGET="1"),
     # the k_intersect alternative and its knobs
     dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
     dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
