@@ -20,6 +20,13 @@ shared-memory hook (lpc_set_allreduce + lpc_shm_allreduce); the trace-end
 histogram and the timing go over RCCL (torch.distributed "nccl").
 
 The line also carries:
+  strong        strong scaling: ONE fixed global set of --rays rays (seed 7, the
+                N=1 headline's rays) split over the ranks with shard_bounds, traced
+                to the global termination; per-rank ms, global counts;
+  config5       BASELINE.json config 5: 100 M rays over the ranks (8 fixed blocks
+                of 12.5 M rays, seeds 7..14, rank r of N takes blocks [8r/N, 8(r+1)/N));
+  cold          N=1: a fresh CL_Tracer's first call (scene upload, new rays, no
+                speculation prediction), and new rays on a warm engine;
   parity        the timed workload checked against the oracle: the first bounce
                 of the rank's first --cpu-rays rays (the same oracle outputs the
                 cpu_baseline leg times; decisions and destinations bit for bit,
@@ -96,6 +103,10 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=1 << 20, help="CPU baseline sample (rays, one bounce)")
     ap.add_argument("--no-configs", action="store_true", help="skip BASELINE configs 2-4")
     ap.add_argument("--no-prof", action="store_true", help="no HIP events in the timed region (A/B of their cost)")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling and config-5 blocks")
+    ap.add_argument("--strong-steps", type=int, default=100, help="timed steps of the strong-scaling block")
+    ap.add_argument("--c5-steps", type=int, default=5, help="timed traces of the config-5 block")
+    ap.add_argument("--c5-rays", type=int, default=100_000_000, help="config 5: global rays (8 blocks)")
     return ap.parse_args()
 
 
@@ -144,6 +155,10 @@ def cpu_leg(sc, eng, o, d, p, nrays, first_stats, timed):
     S = oracle.Scene(sc.meshes)
     z = np.zeros(n, np.int32)
     pm = np.full(n, -2, np.int32)
+    model, affinity = cpu_info()
+    # the oracle's OpenMP team set explicitly to every core of the affinity mask
+    # (all host cores), not the inherited OMP_NUM_THREADS
+    threads = oracle.set_threads(affinity if timed else 0)
     t = time.perf_counter()
     ref = oracle.bounce(S, o, d, p, z, pm, sc.max_ray_len, sc.ior_env)
     dt = time.perf_counter() - t
@@ -218,14 +233,20 @@ def cpu_leg(sc, eng, o, d, p, nrays, first_stats, timed):
                           and abs(st.power_next - pw) <= 1e-6 * max(abs(pw), 1e-300))}
     base = None
     if timed:
-        model, affinity = cpu_info()
-        # the oracle's OpenMP team: OMP_NUM_THREADS when set, else the affinity mask
-        cores = min(int(os.environ.get("OMP_NUM_THREADS", affinity)), affinity)
-        base = dict(value=n / dt, unit="ray-bounces/s", cores=cores, kind="port",
-                    cpu_model=model, cores_in_affinity_mask=affinity,
+        base = dict(value=n / dt, unit="ray-bounces/s", cores=threads, kind="port",
+                    cpu_model=model, cores_in_affinity_mask=affinity, cgroup_cpu_max=cgroup_cpu_max(),
                     sample=f"first {n} rays of the workload, 1 bounce (intersect+postproc+Fresnel) over "
-                           f"{S.tri_count} triangles, {dt:.2f} s",
+                           f"{S.tri_count} triangles, {dt:.2f} s, {threads} OpenMP threads",
                     ri_per_s=n * S.tri_count / dt)
+        # beside it: the same kernels on 16 threads (the box's OMP_NUM_THREADS,
+        # rounds 1-4's figure), on a quarter of the sample
+        n16 = min(n, 1 << 18)
+        oracle.set_threads(16)
+        t = time.perf_counter()
+        oracle.bounce(S, o[:n16], d[:n16], p[:n16], z[:n16], pm[:n16], sc.max_ray_len, sc.ior_env)
+        d16 = time.perf_counter() - t
+        base["at_16_threads"] = {"value": n16 / d16, "rays": n16, "seconds": d16}
+        oracle.set_threads(threads)
     return parity, base
 
 
@@ -280,7 +301,9 @@ def run_results_mode():
     sc = scenes.BUILDERS[name](n=n, seed=7, iterations=depth)
     tr = CL_Tracer(device=0)
     kw = dict(trace_iterations=depth, trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env)
+    t_first = time.perf_counter()
     tr.iterative_tracer(sc.sources, sc.meshes, **kw)                 # warm-up (allocations, pinned blocks)
+    t_first = time.perf_counter() - t_first
     times = []
     for _ in range(5):
         t = time.perf_counter()
@@ -290,6 +313,7 @@ def run_results_mode():
     dt = sorted(times)[len(times) // 2]
     out = {"scene": name, "rays": n, "depth": depth, "iterations": len(res), "ray_bounces": b,
            "ms_per_trace_median": dt * 1e3, "ms_per_trace_all": [x * 1e3 for x in times],
+           "first_call_ms": t_first * 1e3, "first_timed_over_median": times[0] / dt,
            "ray_bounces_per_s": b / dt, "exact_power_sums": int(getattr(tr, "exact_sums", 0)),
            "host_bytes_per_trace": int(sum(sum(a.nbytes for a in r) for r in res)),
            "note": "CL_Tracer(...).iterative_tracer(keep_results=True) end to end: the results tuples "
@@ -315,6 +339,131 @@ def cpu_info():
     except (AttributeError, OSError):
         affinity = os.cpu_count() or 1
     return model, affinity
+
+
+def timed_block(eng, runner, comm, o, d, p, sc, steps, warmup, sync, dist, dev):
+    """Trace fixed rays `steps` times (after `warmup` untimed traces) through the
+    rank's engine and runner (global termination over the ranks), bracketed by
+    barrier + sync.  Returns the rank-0 view: max-over-ranks time, all ranks'
+    ray-bounces, per-rank ms, the global per-iteration counts, identical steps."""
+    eng.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+    in_pow = float(np.sum(p, dtype=np.float64))
+    in_all = float(comm.allreduce_sum([in_pow])[0]) if comm else in_pow
+
+    def step():
+        eng.reset()
+        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_all)
+    for _ in range(warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    res = [step() for _ in range(steps)]
+    sync()
+    dt = time.perf_counter() - t0
+    bounces = float(sum(r["bounces"] for r in res))
+    same = all(r["global_counts"] == res[0]["global_counts"] for r in res)
+    rank_ms = [dt / steps * 1e3]
+    if dist:
+        import torch
+        t = torch.tensor([dt, bounces, 0.0 if same else 1.0], dtype=torch.float64, device=dev)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        per = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(dist.get_world_size())]
+        dist.all_gather(per, torch.tensor([dt / steps * 1e3], dtype=torch.float64, device=dev))
+        rank_ms = [float(x.item()) for x in per]
+        dt, bounces, same = float(mx[0]), float(t[1]), float(mx[2]) == 0.0
+    g = res[-1]["global_counts"]
+    return {"ms_per_step": dt / steps * 1e3, "ray_bounces_per_s": bounces / dt, "steps": steps,
+            "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
+            "global_counts": [int(x) for x in g], "global_ray_bounces": int(sum(g)),
+            "steps_identical": bool(same), "mesh_power": [float(x) for x in res[-1]["mesh_power"]]}
+
+
+C5_BLOCKS = 8
+
+
+def config5_rays(scenes, rank, world, total):
+    """BASELINE config 5's fixed global ray set: 8 blocks of total/8 synthetic
+    rays (seeds 7..14); rank r of `world` takes the contiguous blocks
+    shard_bounds(8, r, world) (world <= 8; above, the block list is split by rays)."""
+    from lightpycl_amd.distributed import shard_bounds
+    per = total // C5_BLOCKS
+
+    def block(b):
+        ls = scenes.synthetic_rays(n=per, seed=7 + b)
+        return (np.asarray(ls.rays_origin, np.float32), np.asarray(ls.rays_dir, np.float32),
+                np.asarray(ls.rays_power, np.float32).reshape(-1))
+    if world <= C5_BLOCKS:
+        lo, hi = shard_bounds(C5_BLOCKS, rank, world)
+        parts = [block(b) for b in range(lo, hi)]
+        return tuple(np.concatenate([q[k] for q in parts]) for k in range(3))
+    b = rank * C5_BLOCKS // world
+    lo, hi = shard_bounds(per, rank - b * world // C5_BLOCKS, world // C5_BLOCKS)
+    o, d, p = block(b)
+    return o[lo:hi], d[lo:hi], p[lo:hi]
+
+
+def cold_block(scenes, Engine, ShardedTrace, n):
+    """The reference examples' measurement (example_directivity_parabolic_mirror.py:
+    88-102: time() around one iterative_tracer call) on the headline scene: a
+    fresh CL_Tracer's first call (mesh flatten, scene upload and record build,
+    new rays, no speculation prediction), aggregate and results mode; then new
+    rays on the warm engine (set_rays + one trace, a prediction from other rays)."""
+    from lightpycl_amd.iterative_tracer import CL_Tracer
+    out = {}
+    sc = scenes.synthetic(n=64, seed=7)                  # the scene objects (meshes, trace parameters)
+    for mode, keep, seed in (("aggregate", False, 1007), ("results", True, 1009)):
+        src = [scenes.synthetic_rays(n=n, seed=seed)]
+        t = time.perf_counter()
+        tr = CL_Tracer(device=0)
+        t_open = time.perf_counter() - t
+        res = tr.iterative_tracer(src, sc.meshes, trace_iterations=sc.iterations, trace_until_dissipated=sc.tau,
+                                  max_ray_len=sc.max_ray_len, ior_env=sc.ior_env, keep_results=keep)
+        dt = time.perf_counter() - t
+        b = tr.ray_bounces()
+        out[f"fresh_tracer_{mode}"] = {"ms": dt * 1e3, "open_ms": t_open * 1e3, "ray_bounces": b,
+                                       "ray_bounces_per_s": b / dt,
+                                       "phases_ms": {k: (v * 1e3 if not isinstance(v, list) else sum(v) * 1e3)
+                                                     for k, v in getattr(tr, "phase_s", {}).items()}}
+        del res
+        tr.engine.close()
+
+    def arrays(ls):
+        return (np.asarray(ls.rays_origin, np.float32), np.asarray(ls.rays_dir, np.float32),
+                np.asarray(ls.rays_power, np.float32).reshape(-1))
+    e = Engine(0)
+    e.upload_meshes(sc.meshes)
+    run = ShardedTrace(e)
+    o, d, p = arrays(scenes.synthetic_rays(n=n, seed=7))
+    e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+    for _ in range(3):                                  # warm: allocations, the prediction of these rays
+        e.reset()
+        run.run(sc.iterations, sc.tau, float(np.sum(p, dtype=np.float64)))
+    e.sync()
+    times = []
+    for seed in (2001, 2002, 2003):
+        o, d, p = arrays(scenes.synthetic_rays(n=n, seed=seed))
+        t = time.perf_counter()
+        e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+        r = run.run(sc.iterations, sc.tau, float(np.sum(p, dtype=np.float64)))
+        times.append((time.perf_counter() - t, r["bounces"]))
+    out["new_rays_warm_engine"] = {"ms": [x[0] * 1e3 for x in times],
+                                   "ray_bounces_per_s": [x[1] / x[0] for x in times],
+                                   "note": "set_rays (host->device rays, analysis) + one synchronous trace"}
+    e.close()
+    return out
+
+
+def cgroup_cpu_max():
+    """The container's CPU bandwidth limit (cgroup v2 cpu.max: "quota period" or
+    "max period"), so a thread count above the quota reads as what it is."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        return {"raw": f"{q} {per}", "cpus": None if q == "max" else int(q) / int(per)}
+    except (OSError, ValueError):
+        return None
 
 
 def free_port():
@@ -438,6 +587,27 @@ def main():
     hr = runner.run(sc.iterations, sc.tau, in_pow, hist=(sc.hist_limits, sc.hist_points),
                     input_power_global=in_pow_all)
     hist_total = float(np.sum(hr["hist"][0]) * ((sc.hist_limits[0][1] - sc.hist_limits[0][0]) / sc.hist_points) ** 2)
+    dev = ("cpu" if rehearse else f"cuda:{local}") if dist else None
+    blocks = {}
+    if not a.no_strong:
+        from lightpycl_amd.distributed import shard_bounds
+        # strong scaling: the N=1 headline's global rays (seed 7), one shard per rank
+        # (sc: the same scene and trace parameters as the weak block)
+        g = scenes.synthetic_rays(n=a.rays, seed=7)
+        go = np.asarray(g.rays_origin, np.float32)
+        gd = np.asarray(g.rays_dir, np.float32)
+        gp = np.asarray(g.rays_power, np.float32).reshape(-1)
+        lo, hi = shard_bounds(a.rays, rank, world)
+        blocks["strong"] = timed_block(eng, runner, comm, go[lo:hi], gd[lo:hi], gp[lo:hi], sc, a.strong_steps, 3,
+                                       sync, dist, dev)
+        blocks["strong"]["rays_global"] = a.rays
+        del g, go, gd, gp
+        # BASELINE config 5: 100 M rays over the ranks (8 fixed blocks)
+        co, cd, cp = config5_rays(scenes, rank, world, a.c5_rays)
+        blocks["config5"] = timed_block(eng, runner, comm, co, cd, cp, sc, a.c5_steps, 1, sync, dist, dev)
+        blocks["config5"]["rays_global"] = a.c5_rays
+        blocks["config5"]["rays_per_rank"] = int(len(cp))
+        del co, cd, cp
     rank_ms = [dt / a.steps * 1e3]
     if dist:
         import torch
@@ -538,10 +708,19 @@ def main():
         par.update(pp)
         out["cpu_baseline"] = base
     out["parity"] = par
+    if blocks:
+        out["strong"] = dict(blocks["strong"], scaling="strong",
+                             workload=f"one fixed set of {a.rays} rays (seed 7) split with shard_bounds over "
+                                      f"{world} rank(s); value = global ray-bounces / max-over-ranks time")
+        out["config5"] = dict(blocks["config5"], scaling="strong",
+                              workload=f"BASELINE config 5: {a.c5_rays} synthetic rays as {C5_BLOCKS} blocks "
+                                       f"(seeds 7..{6 + C5_BLOCKS}) over {world} rank(s)")
+    out["weak_global_counts"] = [int(x) for x in hr["global_counts"]]
     if world == 1 and not a.no_configs:
         runner.close()
         eng.close()
         out["configs"] = run_configs(Engine, ShardedTrace, scenes)
+        out["cold"] = cold_block(scenes, Engine, ShardedTrace, a.rays)
     print(json.dumps(out))
     if world > 1:
         finish()

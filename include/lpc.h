@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LPC_ABI_VERSION 1
+#define LPC_ABI_VERSION 2
 
 enum {
     LPC_OK = 0,
@@ -165,6 +165,11 @@ int lpc_trace_population_power(lpc_handle *h, float *out);
 /* Page-locked host memory for lpc_trace_iterate_export (hipHostMalloc). */
 int lpc_host_alloc(size_t bytes, void **out);
 int lpc_host_free(void *p);
+/* The reference's input-power sum `sum(np.sort(rays_power))` (iterative_tracer.py
+ * :115, :372) after the sort: a sequential float32 accumulation of x[0..n) left to
+ * right, as Python's builtin sum over float32 scalars evaluates it (n = 0: 0).
+ * Host code, no device; the drop-in runs it on a thread beside the upload. */
+int lpc_host_seq_sum_f32(const float *x, int64_t n, float *out);
 /* The reference's iteration loop on one device (iterative_tracer.py:241-391):
  * lpc_trace_iterate until the next population's power is below
  * power_threshold (= (1 - trace_until_dissipated) * input power, :383) or no
@@ -268,27 +273,21 @@ typedef struct {
     int64_t heavy_piece;     /* piece with the largest summed wave time (last launch) */
     int64_t heavy_piece_ticks;
     int64_t piece_ticks;     /* summed wave ticks over all pieces (last launch)  */
-    int64_t tail_waves;      /* k_intersect waves that ran >= 2^16 ticks (655 us) */
+    int64_t tail_waves;      /* walk waves that ran >= 2^16 ticks (655 us)   */
     int64_t tail_nodes;      /* their node visits                               */
     int64_t tail_spread_urad;/* their summed direction spread (micro-radians)   */
     int64_t tail_exact;      /* their exact tests                               */
-    double kernel_ms;        /* k_intersect launches alone (HIP events around each
-                                launch; intersect_ms adds k_spill, k_packet, k_slivers) */
+    double kernel_ms;        /* k_rootwalk launches alone (their own start/stop
+                                timestamps; intersect_ms adds k_spill, k_packet, k_slivers) */
     double xchg_us;          /* host time spent in the all-reduce hook (lpc_set_allreduce) */
     int64_t xchg_calls;      /* its calls (per-iteration stats + trace-end aggregates)  */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
- * traversal counters (2, diagnostic: adds atomics), timing plus per-wave
- * records of the k_intersect grid (3, diagnostic; LPC_QUEUE=0's walk), only the
- * walk kernel's launches (4: kernel_ms, launches and pairs; the lightest, for
- * timed runs), or disable (0). */
+ * traversal counters (2, diagnostic: adds atomics), only the walk kernel's
+ * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs), or
+ * disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
-/* Level 3: the last k_intersect launch's per-(piece, packet) records, 4 uint32
- * each {wall-clock ticks (100 MHz), hierarchy nodes visited, exact tests,
- * piece}, ordered [piece][packet]; *count = records available, at most `cap`
- * are copied into rec4 (may be NULL to query the count). */
-int lpc_prof_waves(lpc_handle *h, uint32_t *rec4, int64_t cap, int64_t *count);
 
 #ifdef __cplusplus
 }

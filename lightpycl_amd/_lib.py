@@ -71,6 +71,7 @@ _PROTOS = {
     "lpc_trace_population_power": [_P, _P],
     "lpc_host_alloc": [ctypes.c_size_t, _P],
     "lpc_host_free": [_P],
+    "lpc_host_seq_sum_f32": [_P, _I64, _P],
     "lpc_trace_population": [_P, _P],
     "lpc_trace_measured": [_P, _P, _P],
     "lpc_trace_fetch_measured": [_P, _P, _P, _P],
@@ -79,7 +80,6 @@ _PROTOS = {
                          _P],
     "lpc_prof_enable": [_P, _INT],
     "lpc_prof_read": [_P, _P, _INT],
-    "lpc_prof_waves": [_P, _P, _I64, _P],
     "lpc_filter_eval": [_P, _I64, _P, _P, _P, _INT, _P],
     "lpc_set_allreduce": [_P, _P, _P],
     "lpc_trace_global_stats": [_P, _P, _I32, _P],
@@ -135,7 +135,7 @@ def load(path: str = LIB_PATH):
         fn.restype = ctypes.c_int
     L.lpc_last_error.argtypes = [_P]
     L.lpc_last_error.restype = ctypes.c_char_p
-    if L.lpc_abi_version() != 1:
+    if L.lpc_abi_version() != 2:
         raise LpcError("liblpc ABI version mismatch")
     _lib = L
     return L

@@ -130,7 +130,9 @@ inline int shm_open_comm(const char *name, int32_t rank, int32_t world, int crea
 }
 
 // Give up on the comm: every later exchange on it fails, and so do the peers'
-// waits (they see this rank's abort word instead of spinning to the timeout).
+// waits (they see this rank's abort word instead of spinning to the timeout) and
+// the peers' current exchange if they were past their wait (the abort words are
+// checked again before the sum).
 inline void shm_abort(ShmComm *c, const std::string &why)
 {
     if (!c) return;
@@ -177,6 +179,14 @@ inline int shm_allreduce(ShmComm *c, double *vals, int32_t n)
                 __builtin_ia32_pause();
             }
         }
+        // a peer that published this exchange and then gave up (its own wait
+        // timed out): its values may be from an exchange the others never paired
+        // with it, so no rank sums them
+        for (int r = 0; r < c->world; ++r)
+            if (__atomic_load_n(&c->slot(r)->abort, __ATOMIC_ACQUIRE) != 0) {
+                shm_abort(c, "shm comm: rank " + std::to_string(r) + " aborted during exchange " + std::to_string(s));
+                return -1;
+            }
         for (int32_t i = 0; i < m; ++i) {
             double acc = 0.0;
             for (int r = 0; r < c->world; ++r) acc += c->slot(r)->v[b][i];

@@ -70,10 +70,7 @@ struct QueueArgs {
     uint32_t *err;                    // DevAcc::qerr: set if a shard overflows rcap (never expected; the
                                       //   host then reports the launch as incomplete instead of losing hits)
     uint32_t rcap;
-    int xpiece;                       // k_roots_s: an item's shard = its piece % 8 (else the block's)
-    int claim;                        // k_rootwalk: waves claim items (LPC_Q_HEAD), their XCD's shard first
 };
-#define LPC_Q_HEAD(c) (32 * (1 + (c)) + 16)   // claim head of shard c (k_rootwalk claim mode)
 // root shard of a k_roots* block
 __host__ __device__ inline int q_shard(uint32_t block) { return (int)(block % LPC_Q_CSHARDS); }
 
@@ -323,6 +320,15 @@ struct ProjArgs {
     int nx, ny;
     double div;                       // H += pc / div  (dx*dy, float64)
     double *H;
+};
+
+// set_rays' analysis of the emitted rays (k_ray_scan), read back once.
+struct RayScan {
+    unsigned long long dmax2_bits;    // max |D|^2 (float64, NaN as +inf): the bits of a non-negative double
+    uint32_t diff_o, diff_d;          // != 0: some origin / direction differs from ray 0's
+    uint32_t neg_pow;                 // != 0: some power is negative or NaN
+    uint32_t pad;
+    uint32_t hist[2][256];            // counting-sort hi digits: key bits [8, 16) and [23, 31)
 };
 
 }  // namespace lpck

@@ -8,8 +8,7 @@
 //                    at once, per-ray conservative tests, exact Moller-Trumbore
 //                    only for candidates -> per-slot nearest hit (64-bit
 //                    atomicMin) and hit count; heavy items hand subtrees over
-//                    to k_spill levels.  k_intersect: the same walk, one wave
-//                    per (packet, piece) (alternative launch, LPC_QUEUE=0).
+//                    to k_spill levels.
 //   k_packet, k_slivers
 //                    degenerate "sliver" triangles by a line filter.
 //   k_raykey, k_gather_aos
@@ -39,22 +38,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 namespace lpck {
 
-// Debug/timing switches (LPC_DBG, read at lpc_open; never set by tests; every
-// one makes results WRONG, timing experiments only): bit 0 = skip trav_packet's
-// per-ray result flush, bit 1 = cull children behind the ray origin, bit 2 =
-// skip the exact tests (drains).
-__constant__ int lpc_dbg = 0;
 // Drain entries whose ray mask has at least this many rays are tested
 // triangle-uniform (the record by scalar loads, each lane its own ray, results
-// in registers); sparser ones are expanded into packed (triangle, ray) pairs.
-// 65 = packed only (LPC_DRAIN_U, read at lpc_open).
-__constant__ int lpc_drain_u = 24;
-// Compile-time variants (A/B builds, tools/build_variant.sh): the packed drain
-// with the next step's records requested ahead (LPC_DRAIN_PIPE), and the
-// hierarchy kernels' launch bounds in waves per SIMD (LPC_WALK_MINB).
-#ifndef LPC_DRAIN_PIPE
-#define LPC_DRAIN_PIPE 0
-#endif
+// in registers); sparser ones are expanded into packed (triangle, ray) pairs
+// (round 3 A/B: 8 and 16 cost the synthetic scene 2-15 %).
+#define LPC_DRAIN_U 24
+// The hierarchy kernels' launch bounds in waves per SIMD (compile-time A/B
+// builds, tools/build_variant.py; 5 and 7 measured equal or slower).
 #ifndef LPC_WALK_MINB
 #define LPC_WALK_MINB 6
 #endif
@@ -185,15 +175,9 @@ static __device__ __forceinline__ void load_ray(const RaysIn &R, const float *__
     }
 }
 
-// Ray loaders of the traversal: a population as RaysIn or the coherence copy
-// (RayPair, the general form), or as one base of 8 equally spaced arrays
-// (RayBase: fewer kernel arguments and live registers in k_rootwalk / k_spill).
-struct RayPair {
-    RaysIn R;
-    const float *rs;
-    int64_t n;
-    __device__ __forceinline__ void load(int64_t q, f3 &O, f3 &D) const { load_ray(R, rs, n, q, O, D); }
-};
+// The traversal's rays: one base of 8 equally spaced arrays (a population or
+// the coherence copy; fewer kernel arguments and live registers in k_rootwalk /
+// k_spill than separate pointers).
 struct RayBase {
     const float *b;                   // ox at b, oy at b + s, ... dz at b + 5 s
     int64_t s;
@@ -212,12 +196,9 @@ static __device__ __forceinline__ void unit_dir(const f3 &D, float &nx, float &n
     nx = D.x * u; ny = D.y * u; nz = D.z * u;
 }
 
-// Stack depth per wave (node refs); the host checks every hierarchy fits (one
-// node per step: (W - 1) levels + 1; NB nodes per step: NB W levels).
-#define LPC_STACK 256
-#define LPC_STACK1 64
-// Nodes per step of the batched walk (trav_packet NB > 1)
-#define LPC_NB 4
+// Stack depth per wave (node refs); the host checks every hierarchy fits:
+// (W - 1) per level + 1.
+#define LPC_STACK 64
 
 // k-th set bit (0-based) of m.
 static __device__ __forceinline__ int select_bit(uint64_t m, int k)
@@ -234,7 +215,6 @@ static __device__ __forceinline__ int select_bit(uint64_t m, int k)
 // LDS of one wave's traversal.
 struct WaveLds {
     int32_t stack[LPC_STACK];
-    uint32_t nbuf[LPC_NB][48];         // batched walk: the step's node records (cx cy cz negB negA ref, W = 8)
     int32_t qidx[64], qscan[64];
     uint64_t qmask[64];
     float ray[6][64];                  // the packet's rays (O, D) for the drain
@@ -256,14 +236,13 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, cons
                                                    const f3 &O, const f3 &D, uint32_t &n_pairs, uint32_t &n_exact)
 {
     if (nq == 0) return;
-    if (PROF && (lpc_dbg & 4)) { nq = 0; return; }   // TIMING EXPERIMENT ONLY (results wrong): no exact tests
     {   // dense entries: one triangle for all its rays at once (its record by
         // scalar loads); the sparse entries move to the front of the queue for
         // the packed pairs below
         const bool ve = lane < nq;
         const int32_t my_idx = ve ? L.qidx[lane] : 0;
         const uint64_t my_mask = ve ? L.qmask[lane] : 0ull;
-        const uint64_t dense = __builtin_amdgcn_ballot_w64(ve && __builtin_popcountll(my_mask) >= lpc_drain_u);
+        const uint64_t dense = __builtin_amdgcn_ballot_w64(ve && __builtin_popcountll(my_mask) >= LPC_DRAIN_U);
         if (dense) {
             const bool keep = ve && !((dense >> lane) & 1ull);
             const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
@@ -325,44 +304,6 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, cons
     L.qscan[lane] = incl;
     const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
     n_pairs += (uint32_t)total;
-#if LPC_DRAIN_PIPE
-    // 64 pairs per step, one per lane; the next step's pair is located and its
-    // record requested before this step's tests (two gathers in flight)
-    auto locate = [&](int q, int &r, int32_t &idx) {
-        int e = 0;                             // first entry with qscan[e] > q
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-            if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
-        const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
-        r = select_bit(L.qmask[e], k);
-        idx = L.qidx[e];
-    };
-    int r0 = 0;
-    int32_t i0 = ~0;
-    if (lane < total) locate(lane, r0, i0);
-    ExactRec x0 = xrec[i0 >= 0 ? i0 : 0];
-    for (int base = 0; base < total; base += 64) {
-        const int q1 = base + 64 + lane;
-        int r1 = 0;
-        int32_t i1 = ~0;
-        if (q1 < total) locate(q1, r1, i1);
-        const ExactRec x1 = xrec[i1 >= 0 ? i1 : 0];
-        if (i0 >= 0) {
-            const f3 Or = mk3(L.ray[0][r0], L.ray[1][r0], L.ray[2][r0]);
-            const f3 Dr = mk3(L.ray[3][r0], L.ray[4][r0], L.ray[5][r0]);
-            float t;
-            if (mt_exact(Or, Dr, mk3(x0.v0x, x0.v0y, x0.v0z), mk3(x0.e1x, x0.e1y, x0.e1z),
-                         mk3(x0.e2x, x0.e2y, x0.e2z), &t) && t > eps) {
-                atomicAdd(&L.lcnt[r0], 1);
-                if (t < max_ray_len) atomicMin(&L.lkey[r0], slot_key(t, i0));
-            }
-            if (PROF) ++n_exact;
-        }
-        r0 = r1;
-        i0 = i1;
-        x0 = x1;
-    }
-#else
     for (int base = 0; base < total; base += 64) {
         const int q = base + lane;
         if (q < total) {
@@ -385,7 +326,6 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, cons
             if (PROF) ++n_exact;
         }
     }
-#endif
     nq = 0;
 }
 
@@ -395,26 +335,20 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, cons
 // rays (filter form d <= 0, see filter_record; node data wave-uniform through
 // the scalar cache); a child node is pushed when any ray passes it, a child
 // triangle's (index, lane mask) is queued for the exact test.
-// PROF: the profiling counters / records and the LPC_DBG timing switches
-// (compiled out of the default launches: fewer live registers in the hot loop).
-// NB > 1 (W = 8): the walk takes up to NB nodes off the stack per step, the
-// wave fetches their records at once (16 lanes x 12 bytes per node, vector loads
-// into LDS) and tests them one after the other: NB node fetches in flight
-// instead of one scalar-load round trip per node (the walk's critical path).  The
-// visit order changes, the results do not (order-independent flushes).
-template <int W, bool PROF = true, class RL = RayPair, bool HALF = false, int NB = 1>
-static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
+// PROF: the profiling counters (compiled out of the default launches: fewer
+// live registers in the hot loop).  start: the subtree root (a root item's
+// piece, or a k_spill item whose parent passed).
+template <int W, bool PROF = false>
+static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ray,
                                                    int64_t n, const int32_t *__restrict__ perm,
                                                    const NodeW<W> *__restrict__ nodes,
                                                    const ExactRec *__restrict__ xrec,
-                                                   const Piece &P, int64_t w, int piece_id, float eps,
+                                                   const int32_t slot, int64_t w, int piece_id, float eps,
                                                    float max_ray_len,
                                                    unsigned long long *__restrict__ skey,
                                                    int32_t *__restrict__ scnt,
                                                    unsigned long long *__restrict__ stats,
-                                                   uint32_t *__restrict__ wrec = nullptr, int64_t ridx = 0,
-                                                   SpillArgs SP = SpillArgs{nullptr, nullptr, 0u, 0, 31},
-                                                   int32_t start = -1)
+                                                   SpillArgs SP, int32_t start)
 {
     const int lane = threadIdx.x & 63;
     const int64_t s = w * 64 + lane;
@@ -422,17 +356,13 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
     ray.load(s < n ? s : n - 1, O, D);
     float nx, ny, nz;
     unit_dir(D, nx, ny, nz);
-    // start >= 0: a k_spill item (subtree root `start`, its parent passed)
-    if (start < 0 &&
-        !(P.root >= 0 && any_lane(filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, O.x, O.y, O.z, nx, ny, nz) <= 0.0f)))
-        return;
     L.ray[0][lane] = O.x; L.ray[1][lane] = O.y; L.ray[2][lane] = O.z;
     L.ray[3][lane] = D.x; L.ray[4][lane] = D.y; L.ray[5][lane] = D.z;
     const unsigned long long key0 = slot_key(max_ray_len, -1);
     L.lkey[lane] = key0;
     L.lcnt[lane] = 0;
 
-    const uint64_t clk0 = (PROF && (stats || wrec)) ? wall_clock64() : 0;
+    const uint64_t clk0 = (PROF && stats) ? wall_clock64() : 0;
     int32_t top = 0, nq = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
     uint32_t n_pairs = 0;                           // exact pairs drained (wave-uniform; hand-over cost)
@@ -444,7 +374,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
     auto drain = [&]() { drain_queue<PROF>(L, nq, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact); };
     int budget = SP.budget;
-    L.stack[top++] = start >= 0 ? start : P.root;
+    L.stack[top++] = start;
     while (top > 0) {
         // work hand-over: after `budget` nodes the subtrees left on the stack go
         // to k_spill, one wave each (a wave stuck in a dense region would
@@ -454,72 +384,19 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(SP.ctr, (uint32_t)top);
             base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0);
-            // one node per step: top <= 64 (the host's depth check, LPC_STACK1)
-            constexpr int kSpan = NB > 1 ? LPC_STACK : 64;
+            // top <= LPC_STACK = 64 (the host's depth check): one entry per lane
             if (base + (uint32_t)top <= SP.cap) {
-#pragma unroll
-                for (int j0 = 0; j0 < kSpan; j0 += 64) {
-                    const int j = j0 + lane;
-                    if (j < top) {
-                        SpillItem it;
-                        it.w = (int32_t)w; it.node = L.stack[j]; it.slot = P.slot; it.piece = piece_id;
-                        SP.items[base + j] = it;
-                    }
+                if (lane < top) {
+                    SpillItem it;
+                    it.w = (int32_t)w; it.node = L.stack[lane]; it.slot = slot; it.piece = piece_id;
+                    SP.items[base + lane] = it;
                 }
                 top = 0;
                 break;
             }
             // queue full: void the part of the range inside it, carry on here
-#pragma unroll
-            for (int j0 = 0; j0 < kSpan; j0 += 64) {
-                const int j = j0 + lane;
-                if (j < top && base + (uint32_t)j < SP.cap) SP.items[base + j].node = -1;
-            }
+            if (lane < top && base + (uint32_t)lane < SP.cap) SP.items[base + lane].node = -1;
             budget = 0;
-        }
-        if constexpr (NB > 1) {
-            static_assert(W == 8, "batched walk: 8-wide nodes");
-            const int k = min(top, NB);
-            {   // lanes 16 i + j fetch dwords 3 j .. 3 j + 2 of the i-th node from the top
-                const int i = lane >> 4, j = lane & 15;
-                if (i < k) {
-                    const uint32_t *src = (const uint32_t *)(nodes + L.stack[top - 1 - i]) + 3 * j;
-                    const uint32_t a = src[0], b = src[1], c = src[2];
-                    L.nbuf[i][3 * j] = a; L.nbuf[i][3 * j + 1] = b; L.nbuf[i][3 * j + 2] = c;
-                }
-            }
-            top -= k;
-            for (int b = 0; b < k; ++b) {
-                const float *nf = (const float *)L.nbuf[b];
-                const int32_t *nr = (const int32_t *)L.nbuf[b] + 5 * W;
-                ++n_nodes;
-                float d[W];
-#pragma unroll
-                for (int q = 0; q < W; q += 2) {
-                    const lpc_f2 cx = {nf[q], nf[q + 1]}, cy = {nf[W + q], nf[W + q + 1]};
-                    const lpc_f2 cz = {nf[2 * W + q], nf[2 * W + q + 1]}, nB = {nf[3 * W + q], nf[3 * W + q + 1]};
-                    const lpc_f2 nA = {nf[4 * W + q], nf[4 * W + q + 1]};
-                    const lpc_f2 r = HALF ? filter_test2h(cx, cy, cz, nB, nA, O.x, O.y, O.z, nx, ny, nz)
-                                          : filter_test2(cx, cy, cz, nB, nA, O.x, O.y, O.z, nx, ny, nz);
-                    d[q] = r.x;
-                    d[q + 1] = r.y;
-                }
-                if (__builtin_amdgcn_readfirstlane(nr[0]) >= 0) {     // internal node: children are nodes
-#pragma unroll
-                    for (int q = 0; q < W; ++q)
-                        if (any_lane(d[q] <= 0.0f)) L.stack[top++] = __builtin_amdgcn_readfirstlane(nr[q]);
-                } else {                                                 // leaf: triangles -> exact-test queue
-                    if (nq > 64 - W) drain();                            // room for the leaf's W entries
-#pragma unroll
-                    for (int q = 0; q < W; ++q) {
-                        const uint64_t m = __builtin_amdgcn_ballot_w64(d[q] <= 0.0f);
-                        if (!m) continue;
-                        if (lane == 0) { L.qidx[nq] = ~nr[q]; L.qmask[nq] = m; }
-                        ++nq;
-                    }
-                }
-            }
-            continue;
         }
         const int32_t node = __builtin_amdgcn_readfirstlane(L.stack[--top]);
         const NodeW<W> N = nodes[node];
@@ -528,23 +405,11 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
         float d[W];
 #pragma unroll
         for (int k = 0; k < W; k += 2) {
-            const lpc_f2 r = HALF ? filter_test2h(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
-                                                  lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
-                                                  lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz)
-                                  : filter_test2(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
-                                                 lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
-                                                 lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz);
+            const lpc_f2 r = filter_test2(lpc_f2{N.cx[k], N.cx[k + 1]}, lpc_f2{N.cy[k], N.cy[k + 1]},
+                                          lpc_f2{N.cz[k], N.cz[k + 1]}, lpc_f2{N.negB[k], N.negB[k + 1]},
+                                          lpc_f2{N.negA[k], N.negA[k + 1]}, O.x, O.y, O.z, nx, ny, nz);
             d[k] = r.x;
             d[k + 1] = r.y;
-        }
-        if (PROF && (lpc_dbg & 2)) {   // TIMING EXPERIMENT ONLY (results wrong): cull children behind the origin
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-                const float wx = N.cx[k] - O.x, wy = N.cy[k] - O.y, wz = N.cz[k] - O.z;
-                const float wn = wx * nx + wy * ny + wz * nz, ww = wx * wx + wy * wy + wz * wz;
-                const float R2 = fmaxf(0.0f, -(N.negA[k] + N.negB[k] * ww));
-                if (wn < 0.0f && wn * wn > R2 * 1.02f + 1e-6f) d[k] = 1.0f;
-            }
         }
         if (N.ref[0] >= 0) {                       // internal node: children are nodes
 #pragma unroll
@@ -583,53 +448,13 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RL &ray,
             if (piece_id < LPC_STATS_PIECES) atomicAdd(&stats[LPC_STATS_PIECE + piece_id], (unsigned long long)dt);
         }
     }
-    if (PROF && wrec) {                        // per-wave record (diagnostic, no contention)
-        for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
-        if (lane == 0) {
-            uint32_t *r = wrec + 4 * ridx;
-            r[0] = (uint32_t)(wall_clock64() - clk0); r[1] = n_nodes; r[2] = n_exact; r[3] = (uint32_t)piece_id;
-        }
-    }
-    if (s < n && !(PROF && (lpc_dbg & 1))) {
+    if (s < n) {
         const unsigned long long k = L.lkey[lane];
         const int32_t c = L.lcnt[lane];
-        const int64_t o = (int64_t)P.slot * n, q = perm ? perm[s] : s;
+        const int64_t o = (int64_t)slot * n, q = perm ? perm[s] : s;
         if (c) atomicAdd(&scnt[o + q], c);
         if (k != key0) atomicMin(&skey[o + q], k);
-        if (SP.tmask && (c || k != key0)) atomicOr(&SP.tmask[q], 1u << P.slot);
-    }
-}
-
-// k_intersect: grid = (ceil(n/256), pieces), block = 4 waves, one (packet,
-// piece) per wave.
-template <int W>
-__global__ __launch_bounds__(256, 6) void k_intersect(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                   const int32_t *__restrict__ perm,
-                                                   const NodeW<W> *__restrict__ nodes,
-                                                   const ExactRec *__restrict__ xrec,
-                                                   const Piece *__restrict__ pieces, float eps,
-                                                   float max_ray_len,
-                                                   unsigned long long *__restrict__ skey,
-                                                   int32_t *__restrict__ scnt,
-                                                   unsigned long long *__restrict__ stats,
-                                                   uint32_t *__restrict__ wrec, SpillArgs SP, int pgroup,
-                                                   int npieces)
-{
-    __shared__ WaveLds lds[4];
-    const int wv = threadIdx.x >> 6;
-    const unsigned bx = blockIdx.x, by = blockIdx.y;
-    const int64_t w = (int64_t)bx * 4 + wv;
-    if (w * 64 >= n) return;                       // whole wave past the end
-    // grid.y = ceil(npieces / pgroup): the wave takes pgroup pieces in turn
-    // (fewer waves launched only to fail a piece's root test; wave launch
-    // rate, ~1 per ns over the chip, bounds a launch of mostly empty waves)
-    const int p0 = (int)by * pgroup;
-    const int p1 = min(p0 + pgroup, npieces);
-    for (int p = p0; p < p1; ++p) {
-        const Piece P = pieces[p];
-        const int64_t slot = (int64_t)p * ((n + 63) / 64) + w;
-        trav_packet<W>(lds[wv], RayPair{R, rs, n}, n, perm, nodes, xrec, P, w, p, eps, max_ray_len,
-                       skey, scnt, stats, wrec, slot, SP);
+        if (SP.tmask && (c || k != key0)) atomicOr(&SP.tmask[q], 1u << slot);
     }
 }
 
@@ -638,7 +463,7 @@ __global__ __launch_bounds__(256, 6) void k_intersect(RaysIn R, const float *__r
 // item that again exceeds the budget hands its remaining subtrees to the next
 // level's queue (`out`; budget 0 on the last level).  One wave per block (a
 // wave's slot frees when its items end, see k_rootwalk).
-template <int W, bool PROF = false, bool HALF = false, int NB = 1>
+template <int W, bool PROF = false>
 __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_spill(RayBase ray, int64_t n,
                                                const int32_t *__restrict__ perm, const NodeW<W> *__restrict__ nodes,
                                                const ExactRec *__restrict__ xrec, float eps, float max_ray_len,
@@ -653,119 +478,13 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_spill(RayBase ray, int64_
     for (uint32_t it = blockIdx.x; it < total; it += stride) {
         const SpillItem I = SP.items[it];
         if (I.node < 0) continue;
-        Piece P;
-        memset(&P, 0, sizeof(P));
-        P.root = I.node; P.slot = I.slot;
-        trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, I.w, I.piece, eps,
-                                                max_ray_len, skey, scnt, stats, nullptr, 0, out, I.node);
+        trav_packet<W, PROF>(lds, ray, n, perm, nodes, xrec, I.slot, I.w, I.piece, eps, max_ray_len, skey, scnt,
+                             stats, out, I.node);
     }
 }
 
-// k_roots: the work queue's root items, one wave per packet (64 rays of the
-// coherence order), written into root shard (block % 8): one item per (packet,
-// piece) whose root test some ray of the packet passes -- the test a
-// k_intersect wave starts with, so the items are exactly the (packet, piece)
-// waves that would traverse.  Lanes take 64 pieces at a time and loop over the
-// packet's rays (read from LDS: broadcast), so the tests pipeline without a
-// ballot per test; one claim atomic per block and 64-piece chunk.
-__global__ __launch_bounds__(256) void k_roots(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                               const Piece *__restrict__ pieces, int npieces, QueueArgs Q,
-                                               int half)
-{
-    __shared__ float s_ray[4][6][64];
-    __shared__ uint32_t s_cnt[4];
-    __shared__ uint32_t s_base;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = q_shard(blockIdx.x);
-    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
-    const bool live = w * 64 < n;
-    {
-        const int64_t s = w * 64 + lane;
-        f3 o = mk3(0.0f, 0.0f, 0.0f), d = mk3(0.0f, 0.0f, 1.0f);
-        if (live) load_ray(R, rs, n, s < n ? s : n - 1, o, d);
-        const float u = 1.0f / sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);   // as trav_packet
-        s_ray[wv][0][lane] = o.x; s_ray[wv][1][lane] = o.y; s_ray[wv][2][lane] = o.z;
-        s_ray[wv][3][lane] = d.x * u; s_ray[wv][4][lane] = d.y * u; s_ray[wv][5][lane] = d.z * u;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (int c0 = 0; c0 < npieces; c0 += 64) {
-        const int p = c0 + lane;
-        const Piece P = pieces[min(p, npieces - 1)];
-        bool pass = false;
-        if (live && p < npieces && P.root >= 0) {
-            for (int r = 0; r < 64; ++r) {
-                const float d = half ? filter_testh(P.cx, P.cy, P.cz, P.negB, P.negA, s_ray[wv][0][r], s_ray[wv][1][r],
-                                                    s_ray[wv][2][r], s_ray[wv][3][r], s_ray[wv][4][r], s_ray[wv][5][r])
-                                     : filter_test(P.cx, P.cy, P.cz, P.negB, P.negA, s_ray[wv][0][r], s_ray[wv][1][r],
-                                                   s_ray[wv][2][r], s_ray[wv][3][r], s_ray[wv][4][r], s_ray[wv][5][r]);
-                pass = pass || d <= 0.0f;
-            }
-        }
-        const uint64_t m = __builtin_amdgcn_ballot_w64(pass);
-        if (lane == 0) s_cnt[wv] = (uint32_t)__builtin_popcountll(m);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-            s_base = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(c), tot) : 0u;
-        }
-        __syncthreads();
-        uint32_t off = s_base;
-        for (int k = 0; k < wv; ++k) off += s_cnt[k];
-        if (pass) {
-            const uint32_t pos = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-            if (pos < Q.rcap) Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)P.root, (uint32_t)P.slot);
-            else atomicOr(Q.err, 2u);             // would be lost: the host reports the launch
-        }
-        __syncthreads();                         // s_cnt / s_base reused by the next chunk
-    }
-}
-
-// k_roots for few pieces (<= 64): lanes are the packet's rays and the wave
-// loops over the pieces (one test and a ballot each); lane-per-piece would
-// leave most lanes idle through 64 ray iterations.  Same tests, same items.
-__global__ __launch_bounds__(256) void k_roots_r(RaysIn R, const float *__restrict__ rs, int64_t n,
-                                                 const Piece *__restrict__ pieces, int npieces, QueueArgs Q,
-                                                 int half)
-{
-    __shared__ uint32_t s_cnt[4];
-    __shared__ uint32_t s_base;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c = q_shard(blockIdx.x);
-    const int64_t w = (int64_t)blockIdx.x * 4 + wv;
-    const bool live = w * 64 < n;
-    const int64_t s = w * 64 + lane;
-    f3 O = mk3(0.0f, 0.0f, 0.0f), D = mk3(0.0f, 0.0f, 1.0f);
-    if (live) load_ray(R, rs, n, s < n ? s : n - 1, O, D);
-    float nx, ny, nz;
-    unit_dir(D, nx, ny, nz);
-    const Piece Pl = pieces[min(lane, npieces - 1)];
-    uint64_t m = 0;
-    if (live)
-        for (int p = 0; p < npieces; ++p) {
-            if (bcasti(Pl.root, p) < 0) continue;
-            const float d = half ? filter_testh(bcast(Pl.cx, p), bcast(Pl.cy, p), bcast(Pl.cz, p), bcast(Pl.negB, p),
-                                                bcast(Pl.negA, p), O.x, O.y, O.z, nx, ny, nz)
-                                 : filter_test(bcast(Pl.cx, p), bcast(Pl.cy, p), bcast(Pl.cz, p), bcast(Pl.negB, p),
-                                               bcast(Pl.negA, p), O.x, O.y, O.z, nx, ny, nz);
-            if (any_lane(d <= 0.0f)) m |= 1ull << p;
-        }
-    if (lane == 0) s_cnt[wv] = (uint32_t)__builtin_popcountll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-        s_base = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(c), tot) : 0u;
-    }
-    __syncthreads();
-    uint32_t off = s_base;
-    for (int k = 0; k < wv; ++k) off += s_cnt[k];
-    if ((m >> lane) & 1ull) {
-        const uint32_t pos = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-        if (pos < Q.rcap) Q.roots[(size_t)c * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)Pl.root, (uint32_t)Pl.slot);
-        else atomicOr(Q.err, 2u);                 // would be lost: the host reports the launch
-    }
-}
-
-// k_roots_s: k_roots_r's tests (lanes = a packet's rays) as tasks: a block takes
+// k_roots_s: the root items, one per (packet, piece) whose root test some ray of
+// the packet passes (lanes = a packet's rays), as tasks: a block takes
 // pb packets, task t = (packet t / S, piece class t % S) tests the pieces
 // p = class + S k (npieces <= 64 S), the block's 4 waves take the tasks in turn,
 // and the block reserves all its items with one atomic.  Small populations (few
@@ -807,8 +526,7 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
                                                    const Piece *__restrict__ pieces, int npieces,
                                                    const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
                                                    int S, int pb, int64_t vb, unsigned long long *s_m,
-                                                   uint32_t *s_off, uint32_t (*s_x)[LPC_Q_CSHARDS],
-                                                   const RootsLds &L);
+                                                   uint32_t *s_off, const RootsLds &L);
 
 template <bool HALF>
 __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restrict__ rs, int64_t n,
@@ -818,7 +536,6 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
 {
     __shared__ unsigned long long s_m[LPC_ROOTS_TASKS];
     __shared__ uint32_t s_off[LPC_ROOTS_TASKS + 1];
-    __shared__ uint32_t s_x[LPC_ROOTS_TASKS + 1][LPC_Q_CSHARDS];   // xpiece: per task and shard, then bases
     __shared__ RootsLds L;
     if (nd) n = *nd;
     for (int i = threadIdx.x; i < npieces; i += 256) {
@@ -834,7 +551,7 @@ __global__ __launch_bounds__(256) void k_roots_s(RaysIn R, const float *__restri
     __syncthreads();
     const int64_t nvb = ((n + 63) / 64 + pb - 1) / pb;
     for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off, s_x, L);
+        roots_block<HALF>(R, rs, n, pieces, npieces, groups, ngroups, Q, S, pb, vb, s_m, s_off, L);
         __syncthreads();                          // s_m / s_off reused by the next virtual block
     }
 }
@@ -844,8 +561,7 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
                                                    const Piece *__restrict__ pieces, int npieces,
                                                    const Piece *__restrict__ groups, int ngroups, const QueueArgs &Q,
                                                    int S, int pb, int64_t vb, unsigned long long *s_m,
-                                                   uint32_t *s_off, uint32_t (*s_x)[LPC_Q_CSHARDS],
-                                                   const RootsLds &L)
+                                                   uint32_t *s_off, const RootsLds &L)
 {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -904,50 +620,6 @@ static __device__ __forceinline__ void roots_block(const RaysIn &R, const float 
         if (lane == 0) s_m[t] = m;
     }
     __syncthreads();
-    if (Q.xpiece) {
-        // an item goes to shard (piece % 8): the XCD that walks a shard first keeps
-        // its pieces' records in its own L2 (k_rootwalk claim mode).  Per task and
-        // shard counts by ballots, then one claim atomic per shard and block.
-        for (int t = wv; t < ntask; t += 4) {
-            const uint64_t m = s_m[t];
-            const int cl = (t % S + S * lane) & (LPC_Q_CSHARDS - 1);
-            const bool bit = (m >> lane) & 1ull;
-#pragma unroll
-            for (int x = 0; x < LPC_Q_CSHARDS; ++x) {
-                const uint64_t bm = __builtin_amdgcn_ballot_w64(bit && cl == x);
-                if (lane == 0) s_x[t][x] = (uint32_t)__builtin_popcountll(bm);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < LPC_Q_CSHARDS) {
-            const int x = threadIdx.x;
-            uint32_t tot = 0;
-            for (int t = 0; t < ntask; ++t) { const uint32_t v = s_x[t][x]; s_x[t][x] = tot; tot += v; }
-            s_x[LPC_ROOTS_TASKS][x] = tot ? atomicAdd(Q.ctl + LPC_Q_NINIT(x), tot) : 0u;
-        }
-        __syncthreads();
-        for (int t = wv; t < ntask; t += 4) {
-            const uint64_t m = s_m[t];
-            const int p = t % S + S * lane;
-            const int cl = p & (LPC_Q_CSHARDS - 1);
-            const bool bit = (m >> lane) & 1ull;
-            uint32_t rank = 0;
-#pragma unroll
-            for (int x = 0; x < LPC_Q_CSHARDS; ++x) {
-                const uint64_t bm = __builtin_amdgcn_ballot_w64(bit && cl == x);
-                if (cl == x) rank = (uint32_t)__builtin_popcountll(bm & ((1ull << lane) - 1ull));
-            }
-            if (!bit) continue;
-            const int64_t w = vb * pb + t / S;
-            const uint32_t pos = s_x[LPC_ROOTS_TASKS][cl] + s_x[t][cl] + rank;
-            if (pos < Q.rcap)
-                Q.roots[(size_t)cl * Q.rcap + pos] = q_item((uint32_t)w, (uint32_t)pieces[p].root,
-                                                            (uint32_t)pieces[p].slot);
-            else
-                atomicOr(Q.err, 2u);
-        }
-        return;
-    }
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
         for (int t = 0; t < ntask; ++t) { s_off[t] = tot; tot += (uint32_t)__builtin_popcountll(s_m[t]); }
@@ -979,7 +651,7 @@ static __device__ __forceinline__ void sliver_launch_size(const SliverArgs &A, i
 // One wave per block: a block's slots free as soon as its item ends, where a
 // 4-wave block holds its LDS until its slowest item ends (round 2 per-item
 // records: ~2 800 of 6 144 wave slots walking on average with 4).
-template <int W, bool PROF = false, bool HALF = false, int NB = 1>
+template <int W, bool PROF = false>
 __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
@@ -991,32 +663,6 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
 {
     __shared__ WaveLds lds;
     if (nd) n = *nd;
-    if (Q.claim) {
-        // claim mode: a resident grid; each wave claims items one at a time from
-        // the shard of its XCD (block b runs on XCD b % 8), then from the others
-        // (a returning atomic per item: items run for microseconds, a claim ~1 us)
-        const int x0 = (int)(blockIdx.x % LPC_Q_CSHARDS);
-        for (int k = 0; k < LPC_Q_CSHARDS; ++k) {
-            const int c = (x0 + k) & (LPC_Q_CSHARDS - 1);
-            const uint32_t cnt = min(Q.ctl[LPC_Q_NINIT(c)], Q.rcap);
-            uint32_t *head = Q.ctl + LPC_Q_HEAD(c);
-            for (;;) {
-                if (__hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cnt) break;
-                uint32_t i = 0;
-                if ((threadIdx.x & 63) == 0) i = atomicAdd(head, 1u);
-                i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-                if (i >= cnt) break;
-                const uint64_t it = Q.roots[(size_t)c * Q.rcap + i];
-                Piece P;
-                memset(&P, 0, sizeof(P));
-                P.root = (int32_t)q_node(it);
-                P.slot = (int32_t)q_slot(it);
-                trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot,
-                                                        eps, max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
-            }
-        }
-        return;
-    }
     // the shards' item prefix in LDS: a register array indexed by a loop variable
     // would hold 9 VGPRs for the whole walk (the walk then spills at 6 waves/SIMD)
     __shared__ uint32_t s_pre[LPC_Q_CSHARDS + 1];
@@ -1032,12 +678,9 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
         int c = 0;
         while (i >= s_pre[c + 1]) ++c;
         const uint64_t it = Q.roots[(size_t)c * Q.rcap + (i - s_pre[c])];
-        Piece P;
-        memset(&P, 0, sizeof(P));
-        P.root = (int32_t)q_node(it);
-        P.slot = (int32_t)q_slot(it);
-        trav_packet<W, PROF, RayBase, HALF, NB>(lds, ray, n, perm, nodes, xrec, P, (int64_t)q_w(it), P.slot, eps,
-                                                max_ray_len, skey, scnt, stats, nullptr, 0, out, P.root);
+        const int32_t slot = (int32_t)q_slot(it);
+        trav_packet<W, PROF>(lds, ray, n, perm, nodes, xrec, slot, (int64_t)q_w(it), slot, eps, max_ray_len, skey,
+                             scnt, stats, out, (int32_t)q_node(it));
     }
     // merged sliver tests (LPC_SLIVER_MERGE): (packet group, sliver piece) units
     // grid-stride after the root items, so the waves whose items end early take
@@ -1410,6 +1053,55 @@ __global__ __launch_bounds__(256) void k_raykey(RaysIn R, int64_t n, float bx0, 
     vals[i] = (int32_t)i;
 }
 
+// set_rays' analysis of the emitted rays, one pass over the uploaded population
+// (replaces host passes over the caller's arrays): max |D|^2 (float64, NaN as
+// +inf; the filter records' Dcap check), whether every origin / direction equals
+// ray 0's (float compares: the coherence key's varying bits), whether every power
+// is >= 0 (the sharded stop rule), and the hi-digit counts of the counting sort's
+// two possible key windows -- k_raykey's own key, so the bucket estimate is exact:
+// bits [8, 16) (a point source: 16 direction bits, hi digit 8) and [23, 31) (a
+// collimated beam: 15 origin bits, hi digit 8).
+__global__ __launch_bounds__(256) void k_ray_scan(RaysIn R, int64_t n, float bx0, float by0, float bz0, float sx,
+                                                  float sy, float sz, RayScan *__restrict__ out)
+{
+    __shared__ uint32_t h[2][256];
+    __shared__ uint32_t s_f[3];
+    __shared__ unsigned long long s_m;
+    for (int i = threadIdx.x; i < 512; i += 256) h[i >> 8][i & 255] = 0u;
+    if (threadIdx.x < 3) s_f[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_m = 0ull;
+    __syncthreads();
+    const float o0x = R.ox[0], o0y = R.oy[0], o0z = R.oz[0], d0x = R.dx[0], d0y = R.dy[0], d0z = R.dz[0];
+    double m = 0.0;
+    uint32_t fo = 0u, fd = 0u, fp = 0u;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float ox = R.ox[i], oy = R.oy[i], oz = R.oz[i], dx = R.dx[i], dy = R.dy[i], dz = R.dz[i];
+        double q = (double)dx * dx + (double)dy * dy + (double)dz * dz;
+        if (q != q) q = INFINITY;
+        m = q > m ? q : m;
+        fo |= (ox != o0x || oy != o0y || oz != o0z) ? 1u : 0u;
+        fd |= (dx != d0x || dy != d0y || dz != d0z) ? 1u : 0u;
+        fp |= !(R.pw[i] >= 0.0f) ? 1u : 0u;
+        const uint32_t key = raykey_ray(R, i, bx0, by0, bz0, sx, sy, sz, nullptr);
+        atomicAdd(&h[0][(key >> 8) & 255u], 1u);
+        atomicAdd(&h[1][(key >> 23) & 255u], 1u);
+    }
+    const unsigned long long mb = (unsigned long long)__double_as_longlong(m);   // m >= 0: bits order as values
+    if (fo) atomicOr(&s_f[0], 1u);
+    if (fd) atomicOr(&s_f[1], 1u);
+    if (fp) atomicOr(&s_f[2], 1u);
+    atomicMax(&s_m, mb);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 512; i += 256)
+        if (h[i >> 8][i & 255]) atomicAdd(&out->hist[i >> 8][i & 255], h[i >> 8][i & 255]);
+    if (threadIdx.x == 0) {
+        atomicMax(&out->dmax2_bits, s_m);
+        if (s_f[0]) atomicOr(&out->diff_o, 1u);
+        if (s_f[1]) atomicOr(&out->diff_d, 1u);
+        if (s_f[2]) atomicOr(&out->neg_pow, 1u);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Counting sort of the coherence keys when the key bits that vary span <= 16
 // (the emitted rays of a traced trace from a point source or a collimated beam,
@@ -1686,11 +1378,12 @@ __global__ __launch_bounds__(LPC_BS_T) void k_bsort2(const uint8_t *__restrict__
 // Test entry (lpc_filter_eval, tests/test_gpu_filter.py): the device's own
 // filter code paths on given (ray, record) pairs, so the superset property
 // (every pair Moller-Trumbore accepts passes the filter) is checked on the code
-// the GPU runs.  mode 0: filter_test (k_roots_r / k_intersect root tests);
-// 1: filter_test2 (the packed child tests of the walk), record i packed with
-// record i ^ 1 against ray i; 2: filter_test2h (the same with the half-line
-// cull, LPC_HALF 1/2); 3: filter_testh (the piece-root half-line cull of
-// k_roots*, LPC_HALF 3, the default).  rec: cx cy cz negB negA per pair.
+// the GPU runs.  mode 0: filter_test (k_roots_s / k_gather_roots root tests
+// without the cull, a lone last piece); 1: filter_test2 (the packed child tests
+// of the walk and the packed root tests), record i packed with record i ^ 1
+// against ray i; 2: filter_test2h (the packed root tests with the half-line cull,
+// LPC_HALF 3, the default); 3: filter_testh (the same for a lone last piece).
+// rec: cx cy cz negB negA per pair.
 __global__ __launch_bounds__(256) void k_filter_eval(int64_t n, const float *__restrict__ O,
                                                      const float *__restrict__ D, const float *__restrict__ rec,
                                                      int mode, float *__restrict__ out)
@@ -2338,7 +2031,9 @@ static __device__ __forceinline__ void stage_move(MoveArgs A)
                 // trace ends (trace_run's rules, iterative_tracer.py:383-391) or a
                 // kept direction exceeds the filter records' Dcap (the host rebuilds)
                 const unsigned long long kept = a.nR + a.nT;
-                const bool dc = !((double)s_d[0] <= A.dcap2);
+                // the whole iteration's max |D|^2 (a chunked iteration: every
+                // chunk's, combined above; the last chunk publishes)
+                const bool dc = !((double)__uint_as_float(a.dmax2_bits) <= A.dcap2);
                 const bool stop = a.pow_next < A.thr || kept == 0 || dc || (long long)kept > A.nmax;
                 A.ctl->n[A.par ^ 1] = stop ? 0 : (long long)kept;
                 A.ctl->m[A.par ^ 1] = a.m_total;

@@ -70,6 +70,26 @@ const int kShadeF = 12;   // float arrays of the shade outputs
 const int kShadeI = 8;    // int arrays
 const int kAccRing = 8;   // mapped counter slots (iterations in flight: at most 2)
 
+// Launch policy.  Each value won its A/B (DESIGN.md sections 5 and 7; the losing
+// alternatives and their knobs were removed in round 5, the tables there keep the
+// record).  None of them changes a result: every path flushes with
+// order-independent atomics and the filters are supersets of the exact test.
+const int64_t kSortMin = 4096;          // populations below this are traced unsorted
+const int64_t kOnesweepMin = 500000;    // rocPRIM onesweep radix sort from this many rays (merge sort below)
+const int kRootsPerBlock = 16;          // k_roots_s packets per block (one task per packet)
+const int64_t kQTarget = 65536;         // (packet, piece) root tests to aim for: the piece level
+const int64_t kWalkWaves = 65536;       // k_rootwalk grid (single-wave blocks, grid-stride)
+const int64_t kSliverMergePpw = 4;      // packets per merged sliver unit (k_rootwalk's tail)
+const int64_t kSliverWaves = 16384;     // k_slivers: (packet, piece) waves to aim for
+const int kSpillLevels = 3;             // k_spill levels (hand-over depth) for populations >= kSpillSmallN
+const int kSpillLevelsSmall = 1;        // ... below
+const int64_t kSpillSmallN = 262144;
+const int64_t kSpillBlocks = 4096;      // k_spill level l grid: max(kSpillMinBlocks, kSpillBlocks >> l) x 4 waves
+const int64_t kSpillMinBlocks = 256;
+const int kSpillPairShift = 5;          // exact pairs per node visit in the hand-over budget (log2)
+const int kKeyObits = 6;                // re-sorted populations: origin bits per axis of the 5-D Morton key
+const double kThin = 1.0;               // thin-triangle rule factor (thin_axis; 0.25 / 2 measured slower)
+
 }  // namespace
 
 struct lpc_handle {
@@ -88,8 +108,7 @@ struct lpc_handle {
     double pop_dmax2 = INFINITY, init_dmax2 = INFINITY;   // max |D|^2 of the trace population / emitted rays
     std::vector<int32_t> run_slo, run_shi;           // sliver records per run
     int64_t n_slivers = 0;
-    int64_t n_thin = 0;                              // of them thin triangles (LPC_THIN)
-    int thin_pct = 100;                              // LPC_THIN: thin-triangle rule, k percent (0: off)
+    int64_t n_thin = 0;                              // of them thin triangles (thin_axis, k = 1)
     float box_lo[3] = {0, 0, 0}, box_scale[3] = {1, 1, 1};
     double scene_scale = 1.0;                        // half diagonal of the scene box (filter h)
     std::vector<int32_t> slot_run;
@@ -105,25 +124,12 @@ struct lpc_handle {
     DBuf w_soa, w_stage, w_sort, w_sort_tmp;
     DBuf w_aos;                                     // rays as 32-byte rows for the coherence gather
     DBuf w_tm;                                      // per ray: the slots a flush wrote (traced path, K <= 32)
-    int64_t onesweep_min = 500000;                  // onesweep radix sort from this many rays (merge sort below)
-    bool bsort = true;                              // counting sort (k_bkey..k_bsort2) for key windows <= 16 bits
     DBuf w_bhist;                                   // its per-block hi-digit counts + digit totals
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
-    int roots_s = 16;                               // k_roots_s (packets per block when one task per packet); 0: k_roots / k_roots_r
-    int roots_pb3 = 1;
-    bool gather_roots = true;                       // LPC_GATHER_ROOTS: k_gather_roots (gather + root tests)
     int64_t sliver_merge = 4000000;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
                                                     // this population size (0: always; -1: never)
-    int64_t sliver_merge_ppw = 4;                   // LPC_SLIVER_MERGE_PPW: packets per merged unit
-    int64_t fork_roots_min = INT64_MAX;             // LPC_FORK_ROOTS_MIN: slivers after k_roots_s from this population
-    bool fork_pending = false;                      // run_intersect -> run_queue: record the side fork after the root tests                              // LPC_ROOTS_PB3: k_roots_s packets per block with >= 3 tasks per packet
-    bool roots_gate = true;                         // LPC_ROOTS_GATE: k_roots_s tests the run roots first
-    int walk_nb = 1;                                // LPC_WALK_NB: nodes per walk step (1 or LPC_NB, 8-wide only)
-    int max_levels = 0;                             // deepest run hierarchy (stack bound of the batched walk)
-    int shade_ku = 1;                               // shading reads the K slots into registers first (K <= 16)
-    bool fuse_compact = true;                       // LPC_FUSE_COMPACT: traced iterations shade + staged compaction
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
     DBuf w_gsum;                                    // per 256-tile group counts, two buffers (zero when unused)
     int64_t gcap = 0;
@@ -132,53 +138,26 @@ struct lpc_handle {
     bool slots_clean = false;                       // every slot (max_ray_len slots_mrl, idx -1, count 0)
     float slots_mrl = 0.0f;
     bool misc_clean = false;                        // the launch words were reset for the next launch
-    bool sliver_late = true;                        // LPC_SLIVER_LATE: side-stream slivers launched after k_rootwalk
-    int half = 3;                                   // LPC_HALF: half-line cull (see run_intersect; 3: piece roots, not for emitted rays)
-    int half_small = 0;                             // LPC_HALF_SMALL: 1 = node-level cull for small chained populations
-    bool half_now = false;                          // ... for the launch in progress
+    int half = 3;                                   // LPC_HALF: 3 = half-line cull at the piece roots of chained
+                                                    //   populations (run_intersect), 0 = off
     bool half_roots = false;                        // ... at the piece roots (k_roots)
     bool in_trace = false;                          // run_intersect called from lpc_trace_iterate
     DBuf d_live;                                    // [K] slot written by some run
     DBuf w_pk;                                      // PacketRec per 128-ray wave (k_slivers)
     DBuf d_misc;                                    // LPC_MISC_WORDS per-launch words
     size_t sort_tmp_bytes = 0;
-    bool sort_rays = true;
-    int sliver_cull = 1;                            // skip slivers the launch's |D| cannot reach
-    int64_t sort_min = 4096;                        // populations below this are traced unsorted
     int64_t resort_min = 2000000;                   // chained traced populations from this size are sorted again
-    bool tmask = true;                              // LPC_TMASK: written-slot masks (the shading reads those slots)
     uint32_t *tm_cur = nullptr;                     // this launch's masks (the walk writes, k_shade_stage reads)
-    // launch policy (defaults; LPC_* environment overrides read at lpc_open)
-    int64_t target_blocks = 32768;                  // k_intersect: blocks x pieces to fill the GPU
+    // work hand-over (LPC_BUDGET, LPC_SPILL_CAP, LPC_LARGE_PER_TRI: tests drive the
+    // queue-overflow and budget paths at small sizes)
     int spill_budget = 20;                          // node visits before a wave hands over (0 off)
-    int spill_budget_small = -1;                    // ... for populations below spill_small_n rays (-1: spill_budget)
-    int spill_budget_large = 0;                     // ... for populations of spill_large_n rays and more (0: no hand-over)
-    int64_t spill_large_n = 0;                      // 0: spill_large_per_tri x triangles
     int64_t spill_large_per_tri = 16;
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
-    int64_t spill_blocks = 4096;                    // k_spill grid (4 waves each, grid-stride)
-    int spill_levels = 3;                           // k_spill launches (hand-over depth)
-    int spill_levels_small = 1;                     // ... for populations below spill_small_n rays
-    int64_t spill_small_n = 262144;
-    int spill_shrink = 1;                           // level l grid = spill_blocks >> (shrink * l) ...
-    int64_t spill_min_blocks = 256;                 // ... but at least this
-    int spill_pair_shift = 5;                       // exact pairs per node visit in the budget (log2)
-    int64_t wave_target = 131072;                   // k_intersect: group pieces per wave above this many waves
-    int node_w = 8;                                 // hierarchy width for the next build (4 or 8)
-    int built_w = 4;                                // width of the records in d_nodes
-    int64_t sliver_waves = 16384;                   // k_slivers: (packet, piece) waves to aim for
-    int64_t sliver_ppw = 0;                         // k_slivers: packets per wave (0: from sliver_waves)
     DBuf w_spill;                                   // k_spill queue
-    bool traced = true;                             // LPC_TRACED: aggregate iterations in coherence order
     bool pop_traced = false;                        // the population is in its parents' traced order
     bool pop_emitted = false;                       // the population is the emitted rays (set_rays)
     int init_key_lo = 0, init_key_hi = 32;          // key bits that vary over the emitted rays (set_rays)
     bool init_bsort = false;                        // their sort may be the counting sort (bsort_fits)
-    int queue = 2;                                  // LPC_QUEUE: 2 root items + k_rootwalk (default), 0 k_intersect
-    int64_t q_walk_blocks = 16384;                  // k_rootwalk grid in 4-wave units (grid-stride)
-    int xcd_claim = 0;                              // LPC_XCD_CLAIM: items sharded by piece % 8, walked by
-                                                    //   claims from the own XCD's shard first (resident grid)
-    int64_t q_target = 65536;                       // (packet, piece) root tests to aim for: piece level
     DBuf w_qroots;                                  // root items
     DevAcc *acc_host = nullptr;                     // pinned copy of d_acc (one read per iteration)
     DevAcc *acc_map = nullptr, *acc_map_dev = nullptr;   // mapped pinned ring k_scan / k_stage_move publish into
@@ -189,11 +168,12 @@ struct lpc_handle {
     DBuf d_ctl;                                     // IterCtl
     int ctl_par = 0;                                // the parity the next enqueued iteration reads
     double ds_thr = -INFINITY;                      // trace_run's power threshold (k_stage_move's stop rule)
+    bool mat_passive = false;                       // no material can raise a ray's power (lpc_scene_upload)
+    bool pow_nonneg = false;                        // every emitted power >= 0 (set_rays)
     std::vector<double> hist_r;                     // the last trace_run's populations / its first (the
     int32_t hist_iter = -1;                         //   speculation's prediction) and its iteration limit
     bool dcap_rebuilt = false;                      // check_dcap rebuilt the records (a speculative iteration is void)
     unsigned int acc_seq = 0;
-    bool early_acc = true;                          // LPC_EARLY_ACC: read the counters before k_scatter ends
     bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
     // results export (lpc_trace_iterate_export): k_export packs a chunk's part of
@@ -211,12 +191,8 @@ struct lpc_handle {
     bool mp_valid = false;                          // mp_last = the trace's measured power per measure mesh
     DBuf d_mrun;                                    // its running sums on the device (k_stage_move)
     DBuf d_cbase;                                   // chunked traced iterations: running row bases (ping-pong)
-    bool pop_box = true;                            // LPC_POPBOX: re-sorted chained populations keyed in their own box
     DBuf w_tbox, d_pbox;                            // per-tile boxes (k_shade_stage), the population's box (k_stage_move)
     bool pbox_ok = false;                           // d_pbox holds the current population's origin box
-    int key_obits = 6;                              // LPC_KEY_OBITS: origin bits per axis of that key (4..8)
-    int64_t ds_cap_max = INT64_MAX;                 // LPC_DS_CAP: largest device-sized (speculative) population
-    int key_mode = 1;                               // LPC_KEY_MODE: 0 origin-major, 1 5-D Morton, 2 direction-major
     double mp_last[LPC_MP_MAX] = {0, 0, 0, 0};
     // trace
     Pop A, B, T, I;
@@ -228,11 +204,10 @@ struct lpc_handle {
     int64_t m_cap = 0, m_total = 0;
     DBuf d_acc;
     DBuf d_tmp;                                     // misc small device scratch
+    DBuf d_scan;                                    // RayScan of set_rays (k_ray_scan)
     DBuf d_stats;                                   // k_intersect counters (profiling)
-    DBuf d_wrec;                                    // per-wave records of the last k_intersect (level 3)
-    int64_t wrec_count = 0;
     // profiling
-    bool prof = false, prof_stats = false, prof_waves = false, prof_light = false;
+    bool prof = false, prof_stats = false, prof_light = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
@@ -269,10 +244,10 @@ static int set_err(lpc_handle *h, int code, const std::string &msg)
 
 // Shading kernels templated on the register-resident slot count KU (shade_eval):
 // the smallest of 4, 8, 12, 16 that holds the scene's K meshes, 0 = slots read
-// from memory as postproc needs them (K > 16 or LPC_SHADE_KU=0).
+// from memory as postproc needs them (K > 16).
 #define LPC_KU_LAUNCH(h, KERN, grid, block, stream, ...)                                          \
     do {                                                                                         \
-        const int K_ = (h)->shade_ku ? (h)->K : 1 << 30;                                         \
+        const int K_ = (h)->K;                                                                   \
         if (K_ <= 4) hipLaunchKernelGGL(KERN<4>, grid, block, 0, stream, __VA_ARGS__);           \
         else if (K_ <= 8) hipLaunchKernelGGL(KERN<8>, grid, block, 0, stream, __VA_ARGS__);      \
         else if (K_ <= 12) hipLaunchKernelGGL(KERN<12>, grid, block, 0, stream, __VA_ARGS__);    \
@@ -282,7 +257,7 @@ static int set_err(lpc_handle *h, int code, const std::string &msg)
 
 #define LPC_KU_LAUNCH2(h, KERN, B, grid, block, stream, ...)                                      \
     do {                                                                                         \
-        const int K_ = (h)->shade_ku ? (h)->K : 1 << 30;                                         \
+        const int K_ = (h)->K;                                                                   \
         if (K_ <= 4) hipLaunchKernelGGL((KERN<4, B>), grid, block, 0, stream, __VA_ARGS__);      \
         else if (K_ <= 8) hipLaunchKernelGGL((KERN<8, B>), grid, block, 0, stream, __VA_ARGS__); \
         else if (K_ <= 12) hipLaunchKernelGGL((KERN<12, B>), grid, block, 0, stream, __VA_ARGS__); \
@@ -399,13 +374,12 @@ static void drop_piece_tables(lpc_handle *h)
 static int build_records(lpc_handle *h)
 {
     drop_piece_tables(h);   // pieces index the records built here
-    const int W = h->node_w;                        // hierarchy width (4 or 8)
-    const size_t node_bytes = W == 8 ? sizeof(Node8) : sizeof(Node4);
+    const int W = 8;                                // hierarchy width (4 measured slower, round 1)
+    const size_t node_bytes = sizeof(Node8);
     std::vector<uint8_t> nodes;                     // NodeW<W> records
     int32_t n_nodes = 0;
     std::vector<SliverRec> slivers;
     h->run_levels.clear();
-    h->max_levels = 0;
     h->node_self.clear();
     h->run_slo.clear(); h->run_shi.clear();
     h->sliver_dmin_host.clear();
@@ -427,7 +401,7 @@ static int build_records(lpc_handle *h)
             if (f.negA == INFINITY) continue;                     // never a candidate
             if (f.negB < -1e29f) { sl.push_back(t); continue; }
             // thin: the line filter about its longer edge (k_slivers) bounds it better
-            if (thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale, 0.01 * h->thin_pct)) {
+            if (thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale, kThin)) {
                 sl.push_back(t);
                 ++h->n_thin;
                 continue;
@@ -451,8 +425,7 @@ static int build_records(lpc_handle *h)
             S.v0x = V0[0]; S.v0y = V0[1]; S.v0z = V0[2];
             // a thin triangle whose longer edge is E1 filters about E1 (e2 holds it)
             const FiltRec f = filter_record(V0, V1, V2, t32, h->dcap, h->scene_scale);
-            const int ax = f.negB < -1e29f ? 1 : thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale,
-                                                           0.01 * h->thin_pct);
+            const int ax = f.negB < -1e29f ? 1 : thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale, kThin);
             S.ax1 = ax == 2 ? 1 : 0;
             const float e1[3] = {V1[0] - V0[0], V1[1] - V0[1], V1[2] - V0[2]};
             const float e2[3] = {V2[0] - V0[0], V2[1] - V0[1], V2[2] - V0[2]};
@@ -539,8 +512,7 @@ static int build_records(lpc_handle *h)
             ent.swap(up);
         } while (ent.size() > 1);
         // W-wide: at most W - 1 siblings wait per level on a wave's stack
-        if ((W - 1) * (int)levels.size() + 1 > LPC_STACK1) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
-        h->max_levels = std::max(h->max_levels, (int)levels.size());
+        if ((W - 1) * (int)levels.size() + 1 > LPC_STACK) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
         for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
             h->run_levels.back().push_back(it->first);
             h->run_levels.back().push_back(it->second);
@@ -556,7 +528,6 @@ static int build_records(lpc_handle *h)
     }
     for (const SliverRec &q : slivers) h->sliver_dmin_host.push_back(q.dmin);
     h->Mpad = n_nodes;
-    h->built_w = W;
     RETIF(dalloc(h, h->d_nodes, nodes.size()));
     RETIF(dalloc(h, h->d_srec, slivers.size() * sizeof(SliverRec)));
     HIPCHK(h, hipMemcpy(h->d_nodes.p, nodes.data(), nodes.size(), hipMemcpyHostToDevice));
@@ -565,25 +536,17 @@ static int build_records(lpc_handle *h)
     return 0;
 }
 
-// Piece table for a launch of n rays.  Hierarchy pieces = subtrees of the runs
-// that own a slot (a run whose slot a later run overwrites is skipped, as its
-// results are): each run's root, or all nodes of the shallowest level with >= g
-// nodes, g chosen so that blocks_x * pieces fills the GPU.  Sliver pieces = the
-// runs' slivers in blocks of <= 64 (one lane each).
-static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_force = 0)
+// Piece table: hierarchy pieces = subtrees of the runs that own a slot (a run
+// whose slot a later run overwrites is skipped, as its results are): all nodes
+// of the shallowest level with >= g nodes (g = 1: the run roots; q_level picks
+// g for a launch).  Sliver pieces = the runs' slivers in blocks of <= 64 (one
+// lane each).
+static int piece_table(lpc_handle *h, PieceTable **out, int32_t g)
 {
-    const int64_t bx = std::max<int64_t>(1, (n + 255) / 256);
     const size_t nr = h->run_levels.size();
     std::vector<int32_t> run_slot(nr, -1);
     for (int32_t j = 0; j < h->K; ++j)
         if (h->slot_run[(size_t)j] >= 0) run_slot[(size_t)h->slot_run[(size_t)j]] = j;
-    int64_t live_runs = 0;
-    for (int32_t v : run_slot) live_runs += v >= 0;
-    live_runs = std::max<int64_t>(live_runs, 1);
-    const int64_t target_blocks = h->target_blocks;
-    int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (target_blocks + bx * live_runs - 1) /
-                                                                        (bx * live_runs)));
-    if (g_force > 0) g = g_force;
     // the level each live run is cut at: the shallowest with >= g nodes (many g
     // give the same cut, so a scene builds only a few tables)
     std::vector<int32_t> cut(nr, -1);
@@ -656,7 +619,7 @@ static int piece_table(lpc_handle *h, int64_t n, PieceTable **out, int32_t g_for
     }
     // the gate pays when the runs are cut below their roots (<= 64 runs: one mask)
     t.ngroups = 0;
-    if (h->roots_gate && grp.size() <= 64 && grp.size() < pcs.size()) {
+    if (grp.size() <= 64 && grp.size() < pcs.size()) {
         RETIF(dalloc(h, t.groups, grp.size() * sizeof(Piece)));
         HIPCHK(h, hipMemcpy(t.groups.p, grp.data(), grp.size() * sizeof(Piece), hipMemcpyHostToDevice));
         t.ngroups = (int32_t)grp.size();
@@ -693,8 +656,7 @@ static int64_t chunk_rays(const lpc_handle *h)
 // (it runs empty) when more children are kept, and the host re-runs it.
 static int64_t ds_cap(const lpc_handle *h)
 {
-    return std::max<int64_t>(0, std::min<int64_t>({h->resort_min - 1, chunk_rays(h), (int64_t)LPC_Q_MAX_PACKETS * 64,
-                                                   h->ds_cap_max}));
+    return std::max<int64_t>(0, std::min<int64_t>({h->resort_min - 1, chunk_rays(h), (int64_t)LPC_Q_MAX_PACKETS * 64}));
 }
 
 // Workspace for a chunk of `n` rays.
@@ -815,10 +777,10 @@ static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
     SP->items = (SpillItem *)h->w_spill.p;
     SP->ctr = (uint32_t *)h->d_misc.p + LPC_MISC_SPILL;
     SP->cap = (uint32_t)std::min<int64_t>(h->spill_cap, 0x7fffffff);
-    const int64_t large_n = h->spill_large_n > 0 ? h->spill_large_n : h->spill_large_per_tri * (int64_t)h->M;
-    SP->budget = n >= large_n ? h->spill_budget_large
-                 : (n < h->spill_small_n && h->spill_budget_small >= 0) ? h->spill_budget_small : h->spill_budget;
-    SP->pair_shift = h->spill_pair_shift;
+    // no hand-over once a population fills the chip many times over (from
+    // LPC_LARGE_PER_TRI rays per triangle)
+    SP->budget = n >= h->spill_large_per_tri * (int64_t)h->M ? 0 : h->spill_budget;
+    SP->pair_shift = kSpillPairShift;
     return 0;
 }
 
@@ -838,7 +800,7 @@ static int ray_base(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n,
 // hand-over levels of a launch of n rays (0: none)
 static int spill_level_count(const lpc_handle *h, int64_t n, const SpillArgs &SP)
 {
-    const int lv = n >= h->spill_small_n ? h->spill_levels : h->spill_levels_small;
+    const int lv = n >= kSpillSmallN ? kSpillLevels : kSpillLevelsSmall;
     return SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
 }
 
@@ -852,13 +814,6 @@ static void spill_level_args(lpc_handle *h, const SpillArgs &SP, int l, int leve
     O->items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
     O->ctr = misc + LPC_MISC_SPILL + l + 1;
     O->budget = l + 1 < levels ? SP.budget : 0;
-}
-
-// The batched walk (LPC_WALK_NB > 1): 8-wide hierarchies whose stack bound
-// (NB W per level) fits LPC_STACK.
-static bool walk_batched(const lpc_handle *h)
-{
-    return h->walk_nb > 1 && h->built_w == 8 && LPC_NB * 8 * h->max_levels <= LPC_STACK;
 }
 
 // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
@@ -876,25 +831,16 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
         spill_level_args(h, SP, l, levels, &I, &O);
         // later levels hold fewer items (and often none): smaller grids, in
         // 4-wave units, launched as single-wave blocks
-        const unsigned g =
-            (unsigned)std::max<int64_t>(h->spill_min_blocks, h->spill_blocks >> (h->spill_shrink * l)) * 4u;
-#define LPC_LAUNCH_SPILL(WW, NT, PF, HF, B)                                                                      \
-    hipLaunchKernelGGL((k_spill<WW, PF, HF, B>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,                     \
-                       (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, stats, \
-                       I, O, nd)
+        const unsigned g = (unsigned)std::max<int64_t>(kSpillMinBlocks, kSpillBlocks >> l) * 4u;
         // profiling counters only in the PROF instantiation (fewer live registers without)
-        if (h->built_w == 8) {
-            if (stats) LPC_LAUNCH_SPILL(8, Node8, true, false, 1);
-            else if (walk_batched(h)) {
-                if (h->half_now) LPC_LAUNCH_SPILL(8, Node8, false, true, LPC_NB);
-                else LPC_LAUNCH_SPILL(8, Node8, false, false, LPC_NB);
-            } else if (h->half_now) LPC_LAUNCH_SPILL(8, Node8, false, true, 1);   // the half-line cull (LPC_HALF 1/2)
-            else LPC_LAUNCH_SPILL(8, Node8, false, false, 1);
-        } else {
-            if (stats) LPC_LAUNCH_SPILL(4, Node4, true, false, 1);
-            else LPC_LAUNCH_SPILL(4, Node4, false, false, 1);
-        }
-#undef LPC_LAUNCH_SPILL
+        if (stats)
+            hipLaunchKernelGGL((k_spill<8, true>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
+                               (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
+                               scnt, stats, I, O, nd);
+        else
+            hipLaunchKernelGGL((k_spill<8, false>), dim3(g), dim3(64), 0, h->stream, ray, n, perm,
+                               (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey,
+                               scnt, stats, I, O, nd);
     }
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -909,7 +855,7 @@ static int32_t q_level(const lpc_handle *h, int64_t n)
     for (int32_t j = 0; j < h->K; ++j) live_runs += h->slot_run[(size_t)j] >= 0;
     live_runs = std::max<int64_t>(live_runs, 1);
     const int64_t npk = (n + 63) / 64;
-    return (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (h->q_target + npk * live_runs - 1) /
+    return (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (kQTarget + npk * live_runs - 1) /
                                                                       (npk * live_runs)));
 }
 
@@ -934,35 +880,26 @@ static int check_qerr(lpc_handle *h)
 
 // The root-item queue of a launch of n rays: shard capacity, buffer, arguments.
 struct QueueShape {
-    int64_t npk, rblocks, rs_blocks;
+    int64_t npk, rs_blocks;
     int rs_S, rs_pb;
-    bool roots_s;
 };
 static int queue_args(lpc_handle *h, int64_t n, const PieceTable *pt, const DevSize *ds, QueueArgs *Qo,
                       QueueShape *sh)
 {
     // device-sized (ds): n is the expected size (grids), the bound sizes the shards
     const int64_t npk = (n + 63) / 64;
-    const int64_t rblocks = (npk + 3) / 4;
-    // k_roots_s: S tasks per packet (npieces <= 64 S, S <= 4; device-sized S <= 16), pb packets per block
+    // k_roots_s: S tasks per packet (npieces <= 64 S), pb packets per block
     const int rs_S = (int)((pt->npieces + 63) / 64);
-    const bool roots_s = h->roots_s > 0 && (rs_S <= 4 || (ds && rs_S <= LPC_ROOTS_TASKS));
-    if (ds && !roots_s) return set_err(h, LPC_E_STATE, "internal: device-sized root tests need k_roots_s");
-    const int rs_pb = !roots_s ? 0 : rs_S >= 3 ? std::max(1, std::min(h->roots_pb3, LPC_ROOTS_TASKS / rs_S))
-                      : rs_S == 2 ? 2 : std::max(1, std::min(h->roots_s, LPC_ROOTS_TASKS));
-    const int64_t rs_blocks = roots_s ? (npk + rs_pb - 1) / rs_pb : 0;
+    if (rs_S > LPC_ROOTS_TASKS) return set_err(h, LPC_E_STATE, "internal: more pieces than k_roots_s holds");
+    const int rs_pb = rs_S >= 3 ? 1 : rs_S == 2 ? 2 : kRootsPerBlock;
+    const int64_t rs_blocks = (npk + rs_pb - 1) / rs_pb;
     const int64_t rs_vblocks = !ds ? rs_blocks : (((ds->bound + 63) / 64) + rs_pb - 1) / rs_pb;
-    // per shard: at most its blocks' packets x pieces items (k_roots* flag an
-    // overflow through Q.err instead of dropping items silently)
-    int64_t rcap = std::max(((rblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 4 * (int64_t)pt->npieces,
-                            ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces);
+    // per shard: at most its blocks' packets x pieces items (k_roots_s / k_gather_roots
+    // flag an overflow through Q.err instead of dropping items silently)
+    int64_t rcap = ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces;
     // k_gather_roots: 16 packets per block
     rcap = std::max<int64_t>(rcap, ((((npk + 15) / 16) + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 16 *
                                        (int64_t)pt->npieces);
-    const bool xpiece = h->xcd_claim && roots_s;
-    if (xpiece)                         // a shard takes every packet's items of its pieces (piece % 8)
-        rcap = std::max<int64_t>(rcap, rs_vblocks * rs_pb *
-                                           (int64_t)((pt->npieces + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS));
     if (rcap >= 0xffffffffLL) return set_err(h, LPC_E_ARG, "root items: too many per shard");
     RETIF(dalloc(h, h->w_qroots, (size_t)LPC_Q_CSHARDS * (size_t)rcap * 8));
     QueueArgs Q;
@@ -970,18 +907,15 @@ static int queue_args(lpc_handle *h, int64_t n, const PieceTable *pt, const DevS
     Q.ctl = (uint32_t *)h->d_misc.p;
     Q.err = (uint32_t *)((char *)h->d_acc.p + offsetof(DevAcc, qerr));
     Q.rcap = (uint32_t)rcap;
-    Q.xpiece = xpiece ? 1 : 0;
-    Q.claim = h->xcd_claim ? 1 : 0;
     *Qo = Q;
-    sh->npk = npk; sh->rblocks = rblocks; sh->rs_blocks = rs_blocks; sh->rs_S = rs_S; sh->rs_pb = rs_pb;
-    sh->roots_s = roots_s;
+    sh->npk = npk; sh->rs_blocks = rs_blocks; sh->rs_S = rs_S; sh->rs_pb = rs_pb;
     return 0;
 }
 
-// The root-item form of the hierarchy stage (default): k_roots* write the
-// (packet, piece) items whose root test passes, k_rootwalk walks them grid-stride
-// and hands heavy subtrees to the k_spill levels.
-// roots_done: k_gather_roots already wrote the items (same queue arguments).
+// The hierarchy stage: k_roots_s writes the (packet, piece) items whose root test
+// passes, k_rootwalk walks them grid-stride and hands heavy subtrees to the
+// k_spill levels.  roots_done: k_gather_roots already wrote
+// the items (same queue arguments).
 static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n, const int32_t *perm,
                      const PieceTable *pt, float eps, float max_ray_len, unsigned long long *skey, int32_t *scnt,
                      unsigned long long *stats, const DevSize *ds = nullptr, const SliverArgs *merged = nullptr,
@@ -990,35 +924,20 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     QueueArgs Q;
     QueueShape sh;
     RETIF(queue_args(h, n, pt, ds, &Q, &sh));
-    const int64_t npk = sh.npk, rblocks = sh.rblocks, rs_blocks = sh.rs_blocks;
-    const int rs_S = sh.rs_S, rs_pb = sh.rs_pb;
-    const bool roots_s = sh.roots_s;
-    const int64_t rcap = (int64_t)Q.rcap;
     if (h->host_prof)
         fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d groups %d S %d pb %d blocks %lld rcap %lld\n",
-                (long long)n, (long long)npk, (int)pt->npieces, (int)pt->ngroups, rs_S, rs_pb, (long long)rs_blocks,
-                (long long)rcap);
-    if (roots_done) {
-        // k_gather_roots wrote the items
-    } else if (roots_s) {
+                (long long)n, (long long)sh.npk, (int)pt->npieces, (int)pt->ngroups, sh.rs_S, sh.rs_pb,
+                (long long)sh.rs_blocks, (long long)Q.rcap);
+    if (!roots_done) {
+        const dim3 rg((unsigned)std::max<int64_t>(sh.rs_blocks, 1));
         if (h->half_roots)
-            hipLaunchKernelGGL(k_roots_s<true>, dim3((unsigned)std::max<int64_t>(rs_blocks, 1)), dim3(256), 0,
-                               h->stream, in, rs, n, (const Piece *)pt->pieces.p, (int)pt->npieces,
-                               (const Piece *)pt->groups.p, (int)pt->ngroups, Q, rs_S, rs_pb, ds ? ds->nd : nullptr);
+            hipLaunchKernelGGL(k_roots_s<true>, rg, dim3(256), 0, h->stream, in, rs, n, (const Piece *)pt->pieces.p,
+                               (int)pt->npieces, (const Piece *)pt->groups.p, (int)pt->ngroups, Q, sh.rs_S, sh.rs_pb,
+                               ds ? ds->nd : nullptr);
         else
-            hipLaunchKernelGGL(k_roots_s<false>, dim3((unsigned)std::max<int64_t>(rs_blocks, 1)), dim3(256), 0,
-                               h->stream, in, rs, n, (const Piece *)pt->pieces.p, (int)pt->npieces,
-                               (const Piece *)pt->groups.p, (int)pt->ngroups, Q, rs_S, rs_pb, ds ? ds->nd : nullptr);
-    }
-    else if (pt->npieces <= 64)
-        hipLaunchKernelGGL(k_roots_r, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
-                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
-    else
-        hipLaunchKernelGGL(k_roots, dim3((unsigned)rblocks), dim3(256), 0, h->stream, in, rs, n,
-                           (const Piece *)pt->pieces.p, (int)pt->npieces, Q, h->half_roots ? 1 : 0);
-    if (h->fork_pending) {                  // the slivers start after the root tests (LPC_FORK_ROOTS_MIN)
-        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
-        h->fork_pending = false;
+            hipLaunchKernelGGL(k_roots_s<false>, rg, dim3(256), 0, h->stream, in, rs, n, (const Piece *)pt->pieces.p,
+                               (int)pt->npieces, (const Piece *)pt->groups.p, (int)pt->ngroups, Q, sh.rs_S, sh.rs_pb,
+                               ds ? ds->nd : nullptr);
     }
     // merged sliver tests (LPC_SLIVER_MERGE): the packet bounds before the walk,
     // on this stream; the walk's waves take the (packet group, piece) units
@@ -1034,30 +953,20 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     RETIF(ray_base(h, in, rs, n, &ray));
     SpillArgs SP;
     RETIF(spill_setup(h, n, &SP));
-    // the grid in waves (LPC_Q_WALK_BLOCKS x 4), single-wave blocks
-    // (claim mode: as many single-wave blocks as the chip holds at once)
-    const unsigned grid = h->xcd_claim ? (unsigned)std::max(1, h->cus * 4 * LPC_WALK_MINB)
-                                       : (unsigned)std::max<int64_t>(1, h->q_walk_blocks * 4);
+    const unsigned grid = (unsigned)kWalkWaves;        // single-wave blocks
     // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
-#define LPC_LAUNCH_WALK(WW, NT, PF, HF, B)                                                                       \
-    hipExtLaunchKernelGGL((k_rootwalk<WW, PF, HF, B>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm, \
-                          (const NT *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,   \
-                          stats, Q, SP, ds ? ds->nd : nullptr, SA)
-    if (h->built_w == 8) {
-        if (stats) LPC_LAUNCH_WALK(8, Node8, true, false, 1);
-        else if (walk_batched(h)) {
-            if (h->half_now) LPC_LAUNCH_WALK(8, Node8, false, true, LPC_NB);
-            else LPC_LAUNCH_WALK(8, Node8, false, false, LPC_NB);
-        } else if (h->half_now) LPC_LAUNCH_WALK(8, Node8, false, true, 1);   // the half-line cull (LPC_HALF 1/2)
-        else LPC_LAUNCH_WALK(8, Node8, false, false, 1);
-    } else {
-        if (stats) LPC_LAUNCH_WALK(4, Node4, true, false, 1);
-        else LPC_LAUNCH_WALK(4, Node4, false, false, 1);
-    }
-#undef LPC_LAUNCH_WALK
+    // profiling counters only in the PROF instantiation (fewer live registers without)
+    if (stats)
+        hipExtLaunchKernelGGL((k_rootwalk<8, true>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,
+                              (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
+                              stats, Q, SP, ds ? ds->nd : nullptr, SA);
+    else
+        hipExtLaunchKernelGGL((k_rootwalk<8, false>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,
+                              (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
+                              stats, Q, SP, ds ? ds->nd : nullptr, SA);
     if (h->prof) h->ev_kern.push_back({k0, k1});
     return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP, ds ? ds->nd : nullptr);
 }
@@ -1076,8 +985,19 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     RETIF(ensure_ws(h, n));
     const int64_t nb = n;                          // capacity
     if (ds) n = std::max<int64_t>(1, std::min(ds->pred, nb));   // launch shapes
+    if ((nb + 63) / 64 > (int64_t)LPC_Q_MAX_PACKETS)
+        return set_err(h, LPC_E_STATE, "internal: chunk above the root items' packet bound");
+    // the pieces of the root items: q_level's cut (the same sliver pieces at every
+    // cut), coarser while k_roots_s cannot hold them (tiny populations)
     PieceTable *pt;
-    RETIF(piece_table(h, n, &pt));
+    int32_t g = q_level(h, n);
+    RETIF(piece_table(h, &pt, g));
+    while (pt->npieces > 64 * LPC_ROOTS_TASKS && g > 1) {
+        g = std::max(1, g / 8);
+        RETIF(piece_table(h, &pt, g));
+    }
+    if (pt->npieces > 64 * LPC_ROOTS_TASKS)
+        return set_err(h, LPC_E_ARG, "scene has more than 1024 mesh runs (k_roots_s limit)");
     const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
     unsigned long long *skey = (unsigned long long *)h->w_key.p;
     int32_t *scnt = (int32_t *)h->w_sc.p;
@@ -1095,31 +1015,24 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     const bool chained_pop = traced && h->pop_traced;
     // a chained population keeps its parents' order, except a large one
     // (LPC_RESORT_MIN): after many generations that order has lost its coherence
-    const bool sorted = h->sort_rays && n >= h->sort_min && (!chained_pop || (!ds && n >= h->resort_min));
+    const bool sorted = n >= kSortMin && (!chained_pop || (!ds && n >= h->resort_min));
     // the slot reset rides on k_raykey when it runs before everything that reads misc
     const bool fold_init = sorted && n >= LPC_MISC_WORDS;
-    // Traced single-chunk iterations (k_shade_stage) leave every slot they read in
-    // the clean state (max_ray_len, idx -1, count 0), so once the whole slot array
-    // is clean no slot needs a reset; only the launch words do (k_stage_move
-    // reset them for the next launch; the emitted rays' k_raykey does).
-    // LPC_HALF 1 / 2: every node test (not for the emitted rays / for all); 3 / 4:
-    // the piece roots only (k_roots items), not for the emitted rays / for all.
-    // "Emitted" = the trace's first population, whatever the export mode; the
-    // drop-in kernels (lpc_intersect, lpc_bounce_host: traced == NULL, no trace
-    // population) are never culled.
-    const bool in_trace = h->in_trace;
-    const bool emitted = h->pop_emitted;
-    // LPC_HALF_SMALL 1: also every node test of chained populations below
-    // spill_small_n rays (the headline's secondaries)
-    h->half_now = in_trace && (h->half == 2 || (h->half == 1 && !emitted) ||
-                               (h->half_small == 1 && !emitted && n < h->spill_small_n));
-    h->half_roots = in_trace && (h->half_now || h->half == 4 || (h->half == 3 && !emitted));
-    const bool restore = traced && h->fuse_compact;
+    // Traced iterations (k_shade_stage) leave every slot they read in the clean
+    // state (max_ray_len, idx -1, count 0), so once the whole slot array is clean
+    // no slot needs a reset; only the launch words do (k_stage_move reset them for
+    // the next launch; the emitted rays' k_raykey does).
+    // LPC_HALF 3 (default): the half-line cull at the piece roots (k_roots_s items)
+    // of a trace's chained populations; "emitted" = the trace's first population,
+    // whatever the export mode; the drop-in kernels (lpc_intersect,
+    // lpc_bounce_host: no trace population) are never culled.  0: off.
+    h->half_roots = h->in_trace && h->half == 3 && !h->pop_emitted;
+    const bool restore = traced != nullptr;
     const bool clean = restore && h->slots_clean && h->slots_mrl == max_ray_len;
     // written-slot masks: kept by every flush of this launch, read by its
     // k_shade_stage (restore path only; a mask bit may be stale, never missing:
     // the masks are cleared with the slots, and only the restore path reads them)
-    h->tm_cur = (restore && h->tmask && h->K <= 32) ? (uint32_t *)h->w_tm.p : nullptr;
+    h->tm_cur = (restore && h->K <= 32) ? (uint32_t *)h->w_tm.p : nullptr;
     const bool misc_clean = restore && h->misc_clean;
     h->slots_clean = h->misc_clean = false;
     SlotInit SIk = SI;
@@ -1174,14 +1087,14 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                    (const uint8_t *)kout,
                                    (const int32_t *)vin, lb, (const uint32_t *)bst, vout);
         } else {
-            // a re-sorted chained population: the key's origin cells span its own
-            // box (k_stage_move of the iteration that made it), not the scene's
+            // a re-sorted chained population: the key (5-D Morton) spans its own box
+            // (k_stage_move of the iteration that made it), not the scene's
             const uint32_t *pbox = (traced && chained_pop && h->pbox_ok) ? (const uint32_t *)h->d_pbox.p : nullptr;
             hipLaunchKernelGGL(k_raykey, dim3(grid1(n)), dim3(256), 0, h->stream, in, n, h->box_lo[0], h->box_lo[1],
                                h->box_lo[2], h->box_scale[0], h->box_scale[1], h->box_scale[2], kin, vin,
-                               (float4 *)h->w_aos.p, SIk, pbox, pbox ? h->key_obits : 5, pbox ? h->key_mode : 0);
+                               (float4 *)h->w_aos.p, SIk, pbox, pbox ? kKeyObits : 5, pbox ? 1 : 0);
             size_t tb = h->sort_tmp_bytes;
-            if (n >= h->onesweep_min)       // large populations: onesweep (one pass per 8 key bits)
+            if (n >= kOnesweepMin)          // large populations: onesweep (one pass per 8 key bits)
                 HIPCHK(h, rocprim::radix_sort_pairs<RaySortOnesweep>(h->w_sort_tmp.p, tb, kin, kout, vin, vout,
                                                                      (size_t)n, b0, b1, h->stream));
             else
@@ -1189,32 +1102,26 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
                                                                 b0, b1, h->stream));
         }
         perm = vout;
-        // LPC_GATHER_ROOTS: the gather with the root tests fused in, when the launch
-        // takes the root-item path with one task per packet and no run gate
-        if (h->gather_roots && h->queue == 2 && !h->prof_waves && !ds && !h->xcd_claim && h->roots_s > 0 &&
-            (nb + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS && (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES &&
-            h->K <= LPC_Q_MAX_SLOTS) {
-            PieceTable *ptf;
-            RETIF(piece_table(h, n, &ptf, q_level(h, n)));
-            if (ptf->npieces > 0 && ptf->npieces <= 64 && ptf->ngroups == 0) {
-                QueueArgs Qf;
-                QueueShape shf;
-                RETIF(queue_args(h, n, ptf, nullptr, &Qf, &shf));
-                const dim3 gg((unsigned)((n + 1023) / 1024));
-                if (h->half_roots)
-                    hipLaunchKernelGGL(k_gather_roots<true>, gg, dim3(1024), 0, h->stream, (const float4 *)h->w_aos.p,
-                                       n, perm, (float *)h->w_rs.p, traced ? 1 : 0, (const Piece *)ptf->pieces.p,
-                                       (int)ptf->npieces, Qf);
-                else
-                    hipLaunchKernelGGL(k_gather_roots<false>, gg, dim3(1024), 0, h->stream, (const float4 *)h->w_aos.p,
-                                       n, perm, (float *)h->w_rs.p, traced ? 1 : 0, (const Piece *)ptf->pieces.p,
-                                       (int)ptf->npieces, Qf);
-                roots_done = true;
-            }
-        }
-        if (!roots_done)
+        // the gather with the root tests fused in (k_gather_roots), when the
+        // launch has one root-test task per packet and no run gate
+        if (!ds && pt->npieces > 0 && pt->npieces <= 64 && pt->ngroups == 0) {
+            QueueArgs Qf;
+            QueueShape shf;
+            RETIF(queue_args(h, n, pt, nullptr, &Qf, &shf));
+            const dim3 gg((unsigned)((n + 1023) / 1024));
+            if (h->half_roots)
+                hipLaunchKernelGGL(k_gather_roots<true>, gg, dim3(1024), 0, h->stream, (const float4 *)h->w_aos.p,
+                                   n, perm, (float *)h->w_rs.p, traced ? 1 : 0, (const Piece *)pt->pieces.p,
+                                   (int)pt->npieces, Qf);
+            else
+                hipLaunchKernelGGL(k_gather_roots<false>, gg, dim3(1024), 0, h->stream, (const float4 *)h->w_aos.p,
+                                   n, perm, (float *)h->w_rs.p, traced ? 1 : 0, (const Piece *)pt->pieces.p,
+                                   (int)pt->npieces, Qf);
+            roots_done = true;
+        } else {
             hipLaunchKernelGGL(k_gather_aos, dim3(grid1(n)), dim3(256), 0, h->stream, (const float4 *)h->w_aos.p, n,
                                perm, (float *)h->w_rs.p, traced ? 1 : 0);
+        }
         rs = (const float *)h->w_rs.p;
     }
     if (traced) {
@@ -1235,38 +1142,29 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (!(dmax2 >= 0.0)) dmax2 = INFINITY;          // NaN bound (a NaN direction): no culling
     const float dmax = (float)std::min<double>(sqrt(dmax2 * (1.0 + 1e-5)), (double)INFINITY);
     int32_t nsp = 0;
-    while (nsp < pt->nspieces && (ds || h->sliver_cull == 0 || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
-    const float dmax_k = h->sliver_cull ? dmax : INFINITY;
+    while (nsp < pt->nspieces && (ds || pt->sdmin[(size_t)nsp] <= dmax)) ++nsp;
     // device-sized: the population's max |D| read on the device (every sliver piece
     // in the grid, culled there)
-    const unsigned *dm2_dev = ds && h->sliver_cull ? ds->dm2 : nullptr;
+    const unsigned *dm2_dev = ds ? ds->dm2 : nullptr;
     const long long *nd_dev = ds ? ds->nd : nullptr;
-    // the slivers run beside the hierarchy stage on a second stream (both only
-    // add to the slots with order-independent atomics); joined at the end
-    hipStream_t ss = h->stream;
-    // LPC_SLIVER_MERGE: the sliver units run in the walk's own grid (k_rootwalk's
-    // tail) on this stream instead of k_slivers on the side stream
-    const bool merge_try = h->sliver_merge >= 0 && n >= h->sliver_merge && nsp > 0 && h->queue == 2 &&
-                           !h->prof_waves && !h->xcd_claim;
+    // LPC_SLIVER_MERGE: from this population size the sliver units run in the
+    // walk's own grid (k_rootwalk's tail) on this stream; below, k_slivers runs
+    // beside the hierarchy stage on a second stream (both only add to the slots
+    // with order-independent atomics; joined at the end), launched after the
+    // hierarchy stage's kernels (the host reaches k_roots_s / k_rootwalk sooner)
+    const bool merge_try = h->sliver_merge >= 0 && n >= h->sliver_merge && nsp > 0 && pt->npieces > 0;
     const bool side = !merge_try && nsp > 0 && h->stream2 && h->ev_side[0];
-    // LPC_FORK_ROOTS_MIN: from this population size the slivers wait for the root
-    // tests too (fork recorded after k_roots_s in run_queue): a large population's
-    // long-lived sliver waves otherwise hold the CUs while k_roots_s, which the walk
-    // waits for, gets what is left
-    h->fork_pending = side && h->sliver_late && n >= h->fork_roots_min;
+    hipStream_t ss = h->stream;
     if (side) {
         ss = h->stream2;
-        if (!h->fork_pending) HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
+        HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream));
     }
-    // on the side stream the sliver kernels are launched after the hierarchy
-    // stage's (the host reaches k_roots / k_rootwalk sooner; the slivers still
-    // run beside k_rootwalk)
     auto sliver_args = [&](int64_t ppw) {
         SliverArgs A;
         memset(&A, 0, sizeof(A));
         A.R = in; A.rs = rs; A.n = n; A.perm = perm; A.pk = (const PacketRec *)h->w_pk.p;
         A.srec = (const SliverRec *)h->d_srec.p; A.pieces = (const Piece *)pt->spieces.p; A.nsp = nsp;
-        A.ppw = (int)ppw; A.eps = eps; A.max_ray_len = max_ray_len; A.dmax = dmax_k;
+        A.ppw = (int)ppw; A.eps = eps; A.max_ray_len = max_ray_len; A.dmax = dmax;
         A.skey = skey; A.scnt = scnt; A.stats = stats; A.nd = nd_dev; A.dm2d = dm2_dev; A.tmask = h->tm_cur;
         return A;
     };
@@ -1275,8 +1173,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         if (nsp > 0) {
             // packets per wave: enough (packet, piece) waves to fill the GPU, no more
             const int64_t npkx = (n + 127) / 128;
-            const int64_t ppw = h->sliver_ppw > 0 ? h->sliver_ppw
-                                                  : std::max<int64_t>(1, npkx * nsp / h->sliver_waves);
+            const int64_t ppw = std::max<int64_t>(1, npkx * nsp / kSliverWaves);
             const dim3 sg((unsigned)((npkx + 4 * ppw - 1) / (4 * ppw)), (unsigned)nsp);
             hipLaunchKernelGGL(k_packet<2>, dim3((unsigned)((npkx + 3) / 4)), dim3(256), 0, ss, in, rs, n,
                                (PacketRec *)h->w_pk.p, nd_dev);
@@ -1286,65 +1183,13 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         if (side) HIPCHK(h, hipEventRecord(h->ev_side[1], h->stream2));
         return 0;
     };
-    const bool late = side && h->sliver_late;
-    if (!late && !merge_try) RETIF(launch_slivers());
-    auto fork_now = [&]() -> int {            // the deferred fork, if run_queue did not record it
-        if (h->fork_pending) { HIPCHK(h, hipEventRecord(h->ev_side[0], h->stream)); h->fork_pending = false; }
-        return 0;
-    };
+    if (!side && !merge_try) RETIF(launch_slivers());       // no side stream: before the walk, this stream
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
-    // root items (default): the item encoding's bounds
-    bool qpath = false, merged = false;
-    if (h->queue == 2 && !h->prof_waves) {
-        PieceTable *ptq;
-        RETIF(piece_table(h, n, &ptq, q_level(h, n)));
-        // device-sized: at most 16 root-test classes (k_roots_s), else the run roots
-        if (ds && ptq->npieces > 64 * LPC_ROOTS_TASKS) RETIF(piece_table(h, n, &ptq, 1));
-        qpath = (nb + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS && (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES &&
-                h->K <= LPC_Q_MAX_SLOTS;
-        if (qpath) {
-            pt = ptq;                   // same sliver pieces at every level
-            if (pt->npieces > 0) {
-                const SliverArgs SAm = sliver_args(std::max<int64_t>(1, h->sliver_merge_ppw));
-                RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds,
-                                merge_try ? &SAm : nullptr, roots_done));
-                merged = merge_try;
-            }
-        }
-    }
-    if (merge_try && !merged) RETIF(launch_slivers());     // no walk to carry them: on this stream
-    if (ds && !qpath) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the root-item path");
-    if (pt->npieces > 0 && !qpath) {
-        // k_intersect: one wave per (packet, piece) (LPC_QUEUE=0, per-wave records)
-        uint32_t *wrec = nullptr;
-        if (h->prof_waves) {
-            h->wrec_count = (int64_t)pt->npieces * ((n + 63) / 64);
-            RETIF(dalloc(h, h->d_wrec, (size_t)h->wrec_count * 16));
-            HIPCHK(h, hipMemsetAsync(h->d_wrec.p, 0, (size_t)h->wrec_count * 16, h->stream));
-            wrec = (uint32_t *)h->d_wrec.p;
-        }
-        SpillArgs SP{nullptr, nullptr, 0u, 0, 31, h->tm_cur};
-        if (!wrec) RETIF(spill_setup(h, n, &SP));
-        // pieces per wave: enough that the grid has about wave_target waves
-        const int64_t bxw = (n + 255) / 256;
-        int pgroup = 1;
-        if (h->wave_target > 0) pgroup = (int)std::max<int64_t>(1, (4 * bxw * pt->npieces) / h->wave_target);
-        pgroup = std::max(1, std::min(pgroup, (int)pt->npieces));
-        const int rows = (pt->npieces + pgroup - 1) / pgroup;
-        const dim3 grid((unsigned)bxw, (unsigned)rows);
-        hipEvent_t k0 = nullptr, k1 = nullptr;
-        if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); (void)hipEventRecord(k0, h->stream); }
-#define LPC_LAUNCH_ISECT(WW)                                                                                   \
-    hipLaunchKernelGGL((k_intersect<WW>), grid, dim3(256), 0, h->stream, in, rs, n, perm,                           \
-                       (const NodeW<WW> *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, (const Piece *)pt->pieces.p, \
-                       eps, max_ray_len, skey, scnt, stats, wrec, SP, pgroup, (int)pt->npieces)
-        if (h->built_w == 8) LPC_LAUNCH_ISECT(8);
-        else LPC_LAUNCH_ISECT(4);
-#undef LPC_LAUNCH_ISECT
-        if (h->prof) { (void)hipEventRecord(k1, h->stream); h->ev_kern.push_back({k0, k1}); }
-        RETIF(run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP));
-        HIPCHK(h, hipGetLastError());
+    if (pt->npieces > 0) {
+        const SliverArgs SAm = sliver_args(kSliverMergePpw);
+        RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds, merge_try ? &SAm : nullptr,
+                        roots_done));
     }
     if (h->prof) {      // the intersect stage: the walk (+ k_packet, k_slivers)
         if (!h->prof_light) {
@@ -1354,8 +1199,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
         h->prof_launches += 1;
         h->prof_pairs += n * (int64_t)h->M;
     }
-    RETIF(fork_now());
-    if (late) RETIF(launch_slivers());
+    if (side) RETIF(launch_slivers());
     if (side) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
     if (st_user) {
         hipLaunchKernelGGL(k_slot_export, dim3(grid1(n)), dim3(256), 0, h->stream, n, h->K,
@@ -1467,71 +1311,26 @@ int lpc_open(int device, lpc_handle **out)
         lpc_close(h);
         return LPC_E_HIP;
     }
-    // launch-policy overrides (A/B measurements; results do not depend on them)
+    // size switches and test hooks (results do not depend on them; DESIGN.md
+    // section 5): the tests drive the re-sort, the merged sliver units, the work
+    // hand-over and its queue overflow, chunked iterations and a filter-record
+    // rebuild inside a trace at small sizes
     auto env_int = [](const char *k, int64_t dflt) -> int64_t {
         const char *v = getenv(k);
         return (v && *v) ? strtoll(v, nullptr, 10) : dflt;
     };
-    h->target_blocks = env_int("LPC_TARGET_BLOCKS", h->target_blocks);
-    h->sort_rays = env_int("LPC_SORT", 1) != 0;
-    h->onesweep_min = env_int("LPC_ONESWEEP_MIN", h->onesweep_min);
-    h->bsort = env_int("LPC_BSORT", h->bsort) != 0;
-    h->fuse_compact = env_int("LPC_FUSE_COMPACT", h->fuse_compact) != 0;
-    h->sliver_late = env_int("LPC_SLIVER_LATE", h->sliver_late) != 0;
-    h->half = (int)env_int("LPC_HALF", h->half);
-    h->half_small = (int)env_int("LPC_HALF_SMALL", h->half_small);
-    h->thin_pct = (int)env_int("LPC_THIN", h->thin_pct);
+    h->half = env_int("LPC_HALF", h->half) == 0 ? 0 : 3;
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
-    h->sort_min = env_int("LPC_SORT_MIN", h->sort_min);
     h->resort_min = std::max<int64_t>(1, env_int("LPC_RESORT_MIN", h->resort_min));
-    h->tmask = env_int("LPC_TMASK", h->tmask) != 0;
-    h->sliver_cull = env_int("LPC_SLIVER_CULL", h->sliver_cull) != 0;
-    h->shade_ku = env_int("LPC_SHADE_KU", h->shade_ku);
-    h->roots_s = env_int("LPC_ROOTS_S", h->roots_s);
-    h->roots_pb3 = (int)std::max<int64_t>(1, env_int("LPC_ROOTS_PB3", h->roots_pb3));
-    h->fork_roots_min = env_int("LPC_FORK_ROOTS_MIN", h->fork_roots_min);
     h->sliver_merge = env_int("LPC_SLIVER_MERGE", h->sliver_merge);
-    h->gather_roots = env_int("LPC_GATHER_ROOTS", h->gather_roots ? 1 : 0) != 0;
-    h->sliver_merge_ppw = env_int("LPC_SLIVER_MERGE_PPW", h->sliver_merge_ppw);
-    h->roots_gate = env_int("LPC_ROOTS_GATE", h->roots_gate) != 0;
-    h->walk_nb = (int)env_int("LPC_WALK_NB", h->walk_nb);
     h->spec = env_int("LPC_SPEC", h->spec) != 0;
     h->dcap_init = (double)env_int("LPC_DCAP_MILLI", 16000) / 1000.0;
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
-    h->spill_budget_large = (int)env_int("LPC_BUDGET_LARGE", h->spill_budget_large);
-    h->spill_budget_small = (int)env_int("LPC_BUDGET_SMALL", h->spill_budget_small);
-    h->spill_large_n = env_int("LPC_LARGE_N", h->spill_large_n);
     h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
-    h->spill_blocks = std::max<int64_t>(env_int("LPC_SPILL_BLOCKS", h->spill_blocks), 1);
-    h->spill_levels = (int)env_int("LPC_SPILL_LEVELS", h->spill_levels);
-    h->spill_levels_small = (int)env_int("LPC_SPILL_LEVELS_SMALL", h->spill_levels_small);
-    h->spill_shrink = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_int("LPC_SPILL_SHRINK", h->spill_shrink)));
-    h->spill_min_blocks = std::max<int64_t>(1, env_int("LPC_SPILL_MIN_BLOCKS", h->spill_min_blocks));
-    h->spill_pair_shift = (int)std::min<int64_t>(31, std::max<int64_t>(0, env_int("LPC_PAIR_SHIFT", h->spill_pair_shift)));
-    h->wave_target = env_int("LPC_WAVE_TARGET", h->wave_target);
-    h->node_w = env_int("LPC_NODE_W", h->node_w) == 4 ? 4 : 8;
-    h->sliver_waves = std::max<int64_t>(env_int("LPC_SLIVER_WAVES", h->sliver_waves), 1);
-    h->sliver_ppw = env_int("LPC_SLIVER_PPW", h->sliver_ppw);
-    h->queue = env_int("LPC_QUEUE", h->queue) == 0 ? 0 : 2;
-    h->traced = env_int("LPC_TRACED", h->traced) != 0;
-    h->q_walk_blocks = std::max<int64_t>(1, env_int("LPC_Q_WALK_BLOCKS", h->q_walk_blocks));
-    h->xcd_claim = (int)env_int("LPC_XCD_CLAIM", h->xcd_claim);
-    h->pop_box = env_int("LPC_POPBOX", h->pop_box) != 0;
-    h->ds_cap_max = std::max<int64_t>(0, env_int("LPC_DS_CAP", h->ds_cap_max));
-    h->key_obits = (int)std::min<int64_t>(8, std::max<int64_t>(4, env_int("LPC_KEY_OBITS", h->key_obits)));
-    h->key_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_KEY_MODE", h->key_mode)));
-    {
-        const int dbg = (int)env_int("LPC_DBG", 0);
-        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_dbg), &dbg, sizeof(dbg)));
-        const int du = (int)std::min<int64_t>(65, std::max<int64_t>(1, env_int("LPC_DRAIN_U", 24)));
-        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(lpc_drain_u), &du, sizeof(du)));
-    }
-    h->q_target = std::max<int64_t>(1, env_int("LPC_Q_TARGET", h->q_target));
-    h->early_acc = env_int("LPC_EARLY_ACC", h->early_acc) != 0;
     h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
-    if (env_int("LPC_SIDE_STREAM", 1) != 0) {
-        const unsigned evf = hipEventDisableTiming;   // the side stream's fork / join events
+    {   // the side stream of the sliver kernels and its fork / join events
+        const unsigned evf = hipEventDisableTiming;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
@@ -1543,7 +1342,6 @@ int lpc_open(int device, lpc_handle **out)
             hipSuccess ||
         hipHostGetDevicePointer((void **)&h->acc_map_dev, h->acc_map, 0) != hipSuccess) {
         h->acc_map = h->acc_map_dev = nullptr;       // counters then come by copy + stream sync
-        h->early_acc = false;
     } else {
         memset(h->acc_map, 0, kAccRing * sizeof(DevAcc));
     }
@@ -1566,7 +1364,7 @@ int lpc_close(lpc_handle *h)
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->w_bhist, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
-                    &h->d_acc, &h->d_tmp, &h->d_stats, &h->d_misc, &h->d_wrec, &h->w_spill, &h->w_qroots,
+                    &h->d_acc, &h->d_tmp, &h->d_scan, &h->d_stats, &h->d_misc, &h->w_spill, &h->w_qroots,
                     &h->w_aos, &h->w_fc, &h->d_mrun, &h->w_gsum, &h->d_ctl, &h->d_cbase, &h->w_tbox, &h->d_pbox};
     for (DBuf *b : bufs) dfree(*b);
     if (h->acc_host) (void)hipHostFree(h->acc_host);
@@ -1611,6 +1409,8 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
         return set_err(h, LPC_E_ARG, "scene needs >= 1 triangle, >= 1 mesh and all tables");
     if (tri_count >= (1 << 28) - 1)   // root items encode node ids in 28 bits (LPC_Q_MAX_NODES)
         return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^28 - 2)");
+    if (mesh_count > 64 * LPC_ROOTS_TASKS)   // k_roots_s holds at most 1024 run roots
+        return set_err(h, LPC_E_ARG, "scene has too many meshes (limit 1024)");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const int32_t M = tri_count, K = mesh_count;
@@ -1644,6 +1444,14 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     }
     h->meas_meshes.clear();
     for (int32_t j = 0; j < K; ++j) if (mat_type[j] == 3) h->meas_meshes.push_back(j);
+    // passive materials: the children of a ray never carry more power than it
+    // (refractive: R, T = 1 - R in [0, 1] for positive indices, .cl:313-326;
+    // mirror: P R with R <= 1, .cl:443; dissipation only attenuates, .cl:385-394)
+    h->mat_passive = true;
+    for (int32_t j = 0; j < K; ++j) {
+        if ((mat_type[j] == 0 || mat_type[j] == 4) && !(ior[j] > 0.0f)) h->mat_passive = false;
+        if (mat_type[j] == 1 && !(refl[j] <= 1.0f)) h->mat_passive = false;
+    }
     // exact records and vertices
     std::vector<ExactRec> xr((size_t)M);
     std::vector<float> vv((size_t)M * 9);
@@ -1733,26 +1541,27 @@ static double host_dmax2(int64_t n, const float *dir4)
     return m;
 }
 
-// Upload (n,4) host rows into SoA arrays of a population (rows 0..n).
+// Upload (n,4) host rows into SoA arrays of a population (rows 0..n): both row
+// arrays into one staging buffer (the copies return once the host arrays are
+// read), then the unpacks on the stream; `sync`: wait for them (the caller may
+// reuse the staging buffer at once otherwise).
 static int upload_rays(lpc_handle *h, Pop &P, int64_t n, const float *origin4, const float *dir4,
-                       const float *pow, const int32_t *prev_mid)
+                       const float *pow, const int32_t *prev_mid, bool sync = true)
 {
-    RETIF(dalloc(h, h->w_stage, (size_t)n * 16));
-    HIPCHK(h, hipMemcpy(h->w_stage.p, origin4, (size_t)n * 16, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, h->stream, n,
-                       (const float4 *)h->w_stage.p, P.f(0), P.f(1), P.f(2));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(h->w_stage.p, dir4, (size_t)n * 16, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, h->stream, n,
-                       (const float4 *)h->w_stage.p, P.f(3), P.f(4), P.f(5));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    RETIF(dalloc(h, h->w_stage, (size_t)n * 32));
+    float4 *so = (float4 *)h->w_stage.p, *sd = so + n;
+    HIPCHK(h, hipMemcpy(so, origin4, (size_t)n * 16, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(sd, dir4, (size_t)n * 16, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(P.f(6), pow, (size_t)n * 4, hipMemcpyHostToDevice));
-    if (prev_mid) {
-        HIPCHK(h, hipMemcpy(P.pmid(), prev_mid, (size_t)n * 4, hipMemcpyHostToDevice));
-    } else {                                    // just emitted (-2, iterative_tracer.py:118), filled on the device
+    hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, h->stream, n, (const float4 *)so, P.f(0), P.f(1),
+                       P.f(2));
+    hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, h->stream, n, (const float4 *)sd, P.f(3), P.f(4),
+                       P.f(5));
+    if (prev_mid) HIPCHK(h, hipMemcpy(P.pmid(), prev_mid, (size_t)n * 4, hipMemcpyHostToDevice));
+    else                                        // just emitted (-2, iterative_tracer.py:118), filled on the device
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)P.pmid(), -2, (size_t)n, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-    }
+    HIPCHK(h, hipGetLastError());
+    if (sync) HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
 
@@ -1950,49 +1759,19 @@ static int reset_measured(lpc_handle *h)
 
 // May the emitted rays' coherence sort be the counting sort (k_bkey..k_bsort2)?
 // Its second level runs one block per hi bucket, so it pays only when no bucket
-// is large: a host estimate of the hi-digit counts (k_raykey's key, host float
-// arithmetic: a heuristic, the sort itself is exact either way).  A collimated
-// beam's few origin cells, or a narrow cone's few direction cells, go to rocPRIM.
-static bool bsort_fits(const lpc_handle *h, int64_t n, const float *o4, const float *d4)
+// is large: the hi-digit counts of k_raykey's key that k_ray_scan counted for
+// the key window in use.  A collimated beam's few origin cells, or a narrow
+// cone's few direction cells, go to rocPRIM (the sort is exact either way).
+static bool bsort_fits(const lpc_handle *h, int64_t n, const RayScan &S)
 {
     const int nbits = h->init_key_hi - h->init_key_lo;
-    if (!h->bsort || nbits < 1 || nbits > 16 || n < LPC_MISC_WORDS) return false;
+    if (nbits < 1 || nbits > 16 || n < LPC_MISC_WORDS) return false;
     const int hb = std::min(nbits, LPC_BS_HB), lb = nbits - hb;
     if (lb == 0) return true;                              // one level: no per-bucket pass
-    std::vector<uint32_t> c((size_t)1 << hb, 0u);
-    auto spread2 = [](uint32_t x) { x &= 0xff; x = (x | (x << 4)) & 0x0f0f; x = (x | (x << 2)) & 0x3333;
-                                    return (x | (x << 1)) & 0x5555; };
-    auto spread3 = [](uint32_t x) { x &= 0x1f; x = (x | (x << 8)) & 0x100f; x = (x | (x << 4)) & 0x10c3;
-                                    return (x | (x << 2)) & 0x1249; };
-    const int T = host_threads();
-    std::vector<std::vector<uint32_t>> cp((size_t)T, std::vector<uint32_t>((size_t)1 << hb, 0u));
-    host_parts(n, T, [&](int64_t lo, int64_t hi, int t) {
-    std::vector<uint32_t> &c = cp[(size_t)t];
-    for (int64_t i = lo; i < hi; ++i) {
-        const float dx = d4[4 * i], dy = d4[4 * i + 1], dz = d4[4 * i + 2];
-        const float l1 = fabsf(dx) + fabsf(dy) + fabsf(dz);
-        float px = l1 > 0.0f ? dx / l1 : 0.0f, py = l1 > 0.0f ? dy / l1 : 0.0f;
-        if (dz < 0.0f) {
-            const float tx = (1.0f - fabsf(py)) * (px >= 0.0f ? 1.0f : -1.0f);
-            const float ty = (1.0f - fabsf(px)) * (py >= 0.0f ? 1.0f : -1.0f);
-            px = tx; py = ty;
-        }
-        const uint32_t du = (uint32_t)fminf(fmaxf((px * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
-        const uint32_t dv = (uint32_t)fminf(fmaxf((py * 0.5f + 0.5f) * 256.0f, 0.0f), 255.0f);
-        uint32_t oc[3];
-        for (int k = 0; k < 3; ++k)
-            oc[k] = (uint32_t)fminf(fmaxf((o4[4 * i + k] - h->box_lo[k]) * h->box_scale[k], 0.0f), 31.0f);
-        const uint32_t key = ((spread3(oc[0]) | (spread3(oc[1]) << 1) | (spread3(oc[2]) << 2)) << 16) |
-                             spread2(du) | (spread2(dv) << 1);
-        ++c[(key >> (h->init_key_lo + lb)) & ((1u << hb) - 1u)];
-    }
-    });
+    const int w = h->init_key_lo + lb == 8 ? 0 : h->init_key_lo + lb == 23 ? 1 : -1;
+    if (w < 0 || hb != 8) return false;                   // windows k_ray_scan did not count
     uint32_t mx = 0;
-    for (size_t b = 0; b < ((size_t)1 << hb); ++b) {
-        uint32_t v = 0;
-        for (int t = 0; t < T; ++t) v += cp[(size_t)t][b];
-        mx = std::max(mx, v);
-    }
+    for (int b = 0; b < 256; ++b) mx = std::max(mx, S.hist[w][b]);
     return mx <= (uint32_t)LPC_BS_MAXB;
 }
 
@@ -2005,33 +1784,34 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
     if (n < 0 || (n > 0 && (!origin4 || !dir4 || !pow))) return set_err(h, LPC_E_ARG, "set_rays: missing buffer");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    h->init_dmax2 = host_dmax2(n, dir4);
-    {   // coherence key bits that can vary over these rays (k_raykey, key mode 0:
-        // [class | origin cell 15 | direction 16]): a point source has one origin
-        // cell, a collimated beam one direction, and the sort skips the rest
-        const int T = host_threads();
-        std::vector<char> so((size_t)T, 1), sd((size_t)T, 1);
-        host_parts(n, T, [&](int64_t lo, int64_t hi, int t) {
-            bool a = true, b = true;
-            for (int64_t i = std::max<int64_t>(lo, 1); i < hi && (a || b); ++i)
-                for (int k = 0; k < 3; ++k) {
-                    if (origin4[4 * i + k] != origin4[k]) a = false;
-                    if (dir4[4 * i + k] != dir4[k]) b = false;
-                }
-            so[(size_t)t] = a; sd[(size_t)t] = b;
-        });
-        bool same_o = true, same_d = true;
-        for (int t = 0; t < T; ++t) { same_o = same_o && so[(size_t)t]; same_d = same_d && sd[(size_t)t]; }
-        h->init_key_lo = 0;
-        h->init_key_hi = 31;
-        if (same_o) h->init_key_hi = 16;
-        if (same_d) h->init_key_lo = 16;
-        if (same_o && same_d) { h->init_key_lo = 0; h->init_key_hi = 8; }   // one digit pass
-        h->init_bsort = bsort_fits(h, n, origin4, dir4);
-    }
-    RETIF(check_dcap(h, h->init_dmax2));
     RETIF(pop_reserve(h, h->I, std::max<int64_t>(n, 1)));
-    if (n > 0) RETIF(upload_rays(h, h->I, n, origin4, dir4, pow, nullptr));
+    // the rays, then their analysis on the device (k_ray_scan, one 2 KB read-back)
+    RayScan S;
+    memset(&S, 0, sizeof(S));
+    if (n > 0) {
+        RETIF(upload_rays(h, h->I, n, origin4, dir4, pow, nullptr, false));
+        RETIF(dalloc(h, h->d_scan, sizeof(RayScan)));
+        HIPCHK(h, hipMemsetAsync(h->d_scan.p, 0, sizeof(RayScan), h->stream));
+        hipLaunchKernelGGL(k_ray_scan, dim3((unsigned)std::min<int64_t>(grid1(n), 2048)), dim3(256), 0, h->stream,
+                           h->I.in(), n, h->box_lo[0], h->box_lo[1], h->box_lo[2], h->box_scale[0], h->box_scale[1],
+                           h->box_scale[2], (RayScan *)h->d_scan.p);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(&S, h->d_scan.p, sizeof(RayScan), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    memcpy(&h->init_dmax2, &S.dmax2_bits, sizeof(double));
+    h->pow_nonneg = S.neg_pow == 0u;
+    // coherence key bits that can vary over these rays (k_raykey: [origin cell 15 |
+    // direction 16]): a point source has one origin cell, a collimated beam one
+    // direction, and the sort skips the rest
+    const bool same_o = S.diff_o == 0u, same_d = S.diff_d == 0u;
+    h->init_key_lo = 0;
+    h->init_key_hi = 31;
+    if (same_o) h->init_key_hi = 16;
+    if (same_d) h->init_key_lo = 16;
+    if (same_o && same_d) { h->init_key_lo = 0; h->init_key_hi = 8; }   // one digit pass
+    h->init_bsort = bsort_fits(h, n, S);
+    RETIF(check_dcap(h, h->init_dmax2));
     h->n_init = n;
     h->max_ray_len = max_ray_len;
     h->ior_env = ior_env;
@@ -2059,18 +1839,23 @@ int lpc_trace_reset(lpc_handle *h)
 }
 
 // All-reduce (sum) of the iteration's stats over the ranks of a sharded trace.
+// Slot 0 of every exchange is a failure flag (0 from a healthy rank, 1 from a
+// rank that failed locally: xchg_poison), so the data values are free to hold
+// NaN -- a trace whose ray powers are NaN keeps iterating exactly as a single
+// device (and the reference: NaN < thr is false) does.
+#define LPC_XCHG_STATS 6
 static int xchg_stats(lpc_handle *h, const lpc_iter_stats &S, lpc_iter_stats *G)
 {
-    double v[5] = {(double)S.n_in, (double)S.n_reflect, (double)S.n_refract, (double)S.n_measured, S.power_next};
+    double v[LPC_XCHG_STATS] = {0.0, (double)S.n_in, (double)S.n_reflect, (double)S.n_refract,
+                                (double)S.n_measured, S.power_next};
     const double t0 = host_us();
-    const int rc = h->xchg(h->xchg_ctx, v, 5);
+    const int rc = h->xchg(h->xchg_ctx, v, LPC_XCHG_STATS);
     h->xchg_us += host_us() - t0;
     h->xchg_calls += 1;
     if (rc != 0) return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
-    for (double x : v)
-        if (x != x) return set_err(h, LPC_E_STATE, "trace: a peer rank failed (NaN in the all-reduced stats)");
-    G->n_in = (int64_t)v[0]; G->n_reflect = (int64_t)v[1]; G->n_refract = (int64_t)v[2];
-    G->n_measured = (int64_t)v[3]; G->power_next = v[4];
+    if (v[0] != 0.0) return set_err(h, LPC_E_STATE, "trace: a peer rank failed (failure flag in the all-reduced stats)");
+    G->n_in = (int64_t)v[1]; G->n_reflect = (int64_t)v[2]; G->n_refract = (int64_t)v[3];
+    G->n_measured = (int64_t)v[4]; G->power_next = v[5];
     return 0;
 }
 
@@ -2078,13 +1863,16 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
                      int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait);
 
 // A rank that fails locally still takes part in the exchange its peers wait in,
-// with NaN values: they see NaN in the sums and fail at once (xchg_stats)
-// instead of waiting for a rank that left, and every rank has made the same
-// number of exchanges.  The local error stays the one reported.
+// with the failure flag (slot 0) set: they see it in the sums and fail at once
+// (xchg_stats, the trace-end sums) instead of waiting for a rank that left, and
+// every rank has made the same number of exchanges.  The flag sits in slot 0 of
+// every exchange shape, so the peers see it whichever exchange they are in.  The
+// local error stays the one reported.
 static void xchg_poison(lpc_handle *h, int32_t n)
 {
     if (!h->xchg) return;
     std::vector<double> v((size_t)n, std::numeric_limits<double>::quiet_NaN());
+    v[0] = 1.0;
     const std::string keep = h->err;
     (void)h->xchg(h->xchg_ctx, v.data(), n);
     h->err = keep;
@@ -2326,19 +2114,18 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     // traced mode: one chunk, no per-ray export (the population then comes out in
     // its parents' coherence order; measured rays per iteration likewise)
     const bool exports = out_origin4 || out_dest4 || out_pow || out_meas || out_next_pow || X;
-    const bool traced = h->traced && !exports;
+    const bool traced = !exports;
     // the counters come back through the mapped host ring k_scan / k_stage_move
     // write, so the host decides and launches the next iteration while the rows
     // still move (profiling: only the light level, whose events end before)
-    const bool early = h->early_acc && h->acc_map_dev && (C >= N || (traced && h->fuse_compact)) && !out_next_pow &&
-                       (!h->prof || h->prof_light);
+    const bool early = h->acc_map_dev && (C >= N || traced) && !out_next_pow && (!h->prof || h->prof_light);
     ++h->acc_seq;
     P->seq = h->acc_seq;
     P->early = early;
     P->traced = traced;
     // traced: k_shade_stage + k_stage_move (several chunks: each places its rows
     // after the earlier chunks', refracted rows staged in T, k_append at the end)
-    const bool fused = traced && h->fuse_compact;
+    const bool fused = traced;
     if (fused && C < N) RETIF(dalloc(h, h->d_cbase, 8 * sizeof(unsigned long long)));
     if (ds && !(fused && early)) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the fused path");
     P->fused = fused;
@@ -2397,7 +2184,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
             G.gsum = gs + (size_t)h->gpar * (size_t)h->gcap;
             G.tmask = h->tm_cur;            // set by this chunk's run_intersect
             // the children's origin box when they may be re-sorted (population >= LPC_RESORT_MIN)
-            const bool want_box = h->pop_box && !ds && 2 * N >= h->resort_min;
+            const bool want_box = !ds && 2 * N >= h->resort_min;
             G.tbox = want_box ? (uint32_t *)h->w_tbox.p : nullptr;
 
             if (ds) LPC_KU_LAUNCH2(h, k_shade_stage, true, dim3((unsigned)nt), dim3(LPC_ST_TILE), h->stream, G);
@@ -2626,6 +2413,17 @@ int lpc_host_free(void *p)
     return 0;
 }
 
+int lpc_host_seq_sum_f32(const float *x, int64_t n, float *out)
+{
+    if (!out || (n > 0 && !x) || n < 0) return set_err(nullptr, LPC_E_ARG, "host_seq_sum_f32: bad argument");
+    // np.add.accumulate's order: x[0], then + x[1], ... (no reassociation: the
+    // build has no fast-math; the adds form one dependent chain)
+    float s = n > 0 ? x[0] : 0.0f;
+    for (int64_t i = 1; i < n; ++i) s += x[i];
+    *out = s;
+    return 0;
+}
+
 // May the iteration after the one in flight (population <= bound rays, chained
 // traced) be enqueued device-sized?  Single chunk, fused compaction, mapped
 // counters, root-item path, no per-kernel profiling.  A sharded trace (all-reduce
@@ -2633,10 +2431,8 @@ int lpc_host_free(void *p)
 // and the host drops the iteration when the ranks' sums end the trace.
 static bool ds_ok(const lpc_handle *h, int64_t bound)
 {
-    return h->spec && h->traced && h->fuse_compact && h->early_acc && h->acc_map_dev &&
-           (!h->prof || h->prof_light) && h->queue == 2 && !h->prof_waves && h->roots_s > 0 && bound > 0 &&
-           bound <= chunk_rays(h) && bound < h->resort_min && (bound + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS &&
-           (int64_t)h->Mpad <= (int64_t)LPC_Q_MAX_NODES && h->K <= LPC_Q_MAX_SLOTS;
+    return h->spec && h->acc_map_dev && (!h->prof || h->prof_light) && bound > 0 && bound <= chunk_rays(h) &&
+           bound < h->resort_min && (bound + 63) / 64 <= (int64_t)LPC_Q_MAX_PACKETS;
 }
 
 // The trace loop (iterative_tracer.py:383-391).  With speculation (LPC_SPEC, and
@@ -2669,12 +2465,27 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     // the power left is a sum over all ranks, only the host sees it after the
     // exchange, and a speculative iteration the ranks' sums end is dropped
     h->ds_thr = h->xchg ? -INFINITY : power_threshold;
+    // sharded: a conservative local rule.  The device may stop the trace only when
+    // the ranks' sum is certain to fall below the threshold: with passive
+    // materials and non-negative powers a population's power never grows, so the
+    // other ranks' power left after the last exchanged iteration j bounds theirs
+    // at every later iteration (slack for the float32 children sums), and this
+    // rank's power below threshold - that bound ends the global trace too.
+    const bool mono = h->xchg && h->mat_passive && h->pow_nonneg && h->ior_env > 0.0f;
+    double others = INFINITY;           // upper bound of the other ranks' power left (last exchange)
+    int32_t others_it = -1;
+    auto local_thr = [&](int32_t it) {  // k_stage_move's stop threshold of iteration `it`
+        if (!h->xchg) return power_threshold;
+        if (!mono || others_it < 0 || !(others < INFINITY)) return -(double)INFINITY;
+        return power_threshold - others * (1.0 + 1e-5 * (double)(it - others_it + 1));
+    };
     int rc = 0;
     bool exchanged = false;             // rc came from the exchange itself (no poison owed)
     Pending cur, nxt;
     bool have_cur = false, have_nxt = false;
     for (int32_t i = 0; i < max_iter; ++i) {
         if (!have_cur) {
+            h->ds_thr = local_thr(i);
             if ((rc = iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &cur))) break;
             have_cur = true;
         }
@@ -2693,6 +2504,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
                 D.dm2 = &ctl->dm2[h->ctl_par];
                 D.pred = std::max<int64_t>(1, std::min(pred_n, bound));
                 D.bound = bound;
+                h->ds_thr = local_thr(i + 1);
                 if ((rc = iter_enqueue(h, nullptr, nullptr, nullptr, nullptr, nullptr, &D, &nxt))) break;
                 have_nxt = true;
             }
@@ -2710,6 +2522,10 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         lpc_iter_stats G = S;
         if (h->xchg && (rc = xchg_stats(h, S, &G))) { exchanged = true; break; }
         h->gstats.push_back(G);
+        if (h->xchg) {
+            others = std::max(0.0, G.power_next - S.power_next) * (1.0 + 1e-9);
+            others_it = i;
+        }
         const bool stop = G.power_next < power_threshold || G.n_reflect + G.n_refract == 0;   // :383, :389
         if (have_nxt) {
             const bool rebuilt = h->dcap_rebuilt;
@@ -2717,10 +2533,11 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
             if (stop || rebuilt || i + 1 >= max_iter) {
                 // not part of the trace: it ran empty on the device (its IterCtl
                 // size was 0) -- or, sharded, it may have run on this rank's kept
-                // children when the ranks' sums stopped the trace
+                // children when the ranks' sums stopped the trace; after a Dcap
+                // rebuild its measured power must not count either
                 iter_discard(h, nxt);
                 have_nxt = false;
-                if (h->xchg) RETIF(restore_mrun(h));
+                if ((h->xchg || rebuilt) && (rc = restore_mrun(h))) break;   // the peers get the poison below
             } else if (S.n_reflect + S.n_refract > nxt.n_bound) {
                 // more children than it was sized for: it ran empty on the device;
                 // the next pass of the loop runs the iteration host-sized
@@ -2740,7 +2557,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         (void)hipStreamSynchronize(h->stream);
         iter_discard(h, cur);
     }
-    if (rc && !exchanged) xchg_poison(h, 5);               // the peers wait in this iteration's exchange
+    if (rc && !exchanged) xchg_poison(h, LPC_XCHG_STATS);               // the peers wait in this iteration's exchange
     RETIF(rc);
     // this trace's populations (relative to the first) predict the next trace's
     if (n0 > 0) {
@@ -2749,22 +2566,22 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         h->hist_iter = max_iter;
     }
     if (measured_count || mesh_power) {                     // the trace's aggregates, same call
+        // [failure flag, per-mesh power (K), measured count]
         int64_t c = 0;
-        std::vector<double> mp((size_t)h->K + 1, 0.0);
-        if ((rc = lpc_trace_measured(h, &c, mp.data()))) {
-            xchg_poison(h, h->K + 1);
+        std::vector<double> mp((size_t)h->K + 2, 0.0);
+        if ((rc = lpc_trace_measured(h, &c, mp.data() + 1))) {
+            xchg_poison(h, h->K + 2);
             return rc;
         }
         if (h->xchg) {                                      // trace-end sums over the ranks
-            mp[(size_t)h->K] = (double)c;
-            if (h->xchg(h->xchg_ctx, mp.data(), h->K + 1) != 0)
+            mp[(size_t)h->K + 1] = (double)c;
+            if (h->xchg(h->xchg_ctx, mp.data(), h->K + 2) != 0)
                 return set_err(h, LPC_E_STATE, "trace: all-reduce hook failed");
-            for (double x : mp)
-                if (x != x) return set_err(h, LPC_E_STATE, "trace: a peer rank failed (NaN in the trace-end sums)");
-            c = (int64_t)mp[(size_t)h->K];
+            if (mp[0] != 0.0) return set_err(h, LPC_E_STATE, "trace: a peer rank failed (failure flag in the trace-end sums)");
+            c = (int64_t)mp[(size_t)h->K + 1];
         }
         if (measured_count) *measured_count = c;
-        if (mesh_power) memcpy(mesh_power, mp.data(), (size_t)h->K * 8);
+        if (mesh_power) memcpy(mesh_power, mp.data() + 1, (size_t)h->K * 8);
     }
     if (wait) RETIF(settle(h));                             // the trace's last kernels too
     if (h->host_prof) {
@@ -2921,8 +2738,7 @@ int lpc_prof_enable(lpc_handle *h, int on)
     RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
     h->prof = on != 0;
     h->prof_stats = on == 2;
-    h->prof_waves = on == 3;
-    h->prof_light = on == 4;                        // k_intersect events only (bench timed region)
+    h->prof_light = on == 4;                        // k_rootwalk events only (bench timed region)
     if (h->prof_stats && !h->d_stats.p) {
         RETIF(dalloc(h, h->d_stats, LPC_STATS_WORDS * 8));
         HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
@@ -2962,19 +2778,6 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
         h->prof_isect_ms = h->prof_rest_ms = h->prof_kern_ms = 0.0; h->prof_launches = h->prof_pairs = 0;
         h->xchg_us = 0.0; h->xchg_calls = 0;
         if (h->d_stats.p) HIPCHK(h, hipMemset(h->d_stats.p, 0, LPC_STATS_WORDS * 8));
-    }
-    return 0;
-}
-
-int lpc_prof_waves(lpc_handle *h, uint32_t *rec4, int64_t cap, int64_t *count)
-{
-    if (!h || !count) return set_err(h, LPC_E_ARG, "null argument");
-    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    *count = h->d_wrec.p ? h->wrec_count : 0;
-    if (rec4 && *count > 0) {
-        const int64_t m = std::min(cap, *count);
-        if (m > 0) HIPCHK(h, hipMemcpy(rec4, h->d_wrec.p, (size_t)m * 16, hipMemcpyDeviceToHost));
     }
     return 0;
 }

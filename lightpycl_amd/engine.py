@@ -394,19 +394,9 @@ class Engine:
         return (H, xe, ye) if not want_xy else (H, xe, ye, x, y, pc)
 
     # -- profiling -------------------------------------------------------------
-    def prof_enable(self, on=True, counters=False, waves=False, light=False):
-        level = (4 if light else 3 if waves else 2 if counters else 1) if on else 0
+    def prof_enable(self, on=True, counters=False, light=False):
+        level = (4 if light else 2 if counters else 1) if on else 0
         self._c(self.L.lpc_prof_enable(self.h, level))
-
-    def prof_waves(self):
-        """Per-(piece, packet) records of the last grid traversal (prof level 3):
-        uint32 (count, 4) = ticks (100 MHz), nodes visited, exact tests, piece."""
-        c = ctypes.c_int64(0)
-        self._c(self.L.lpc_prof_waves(self.h, None, 0, ctypes.byref(c)))
-        rec = np.zeros((c.value, 4), np.uint32)
-        if c.value:
-            self._c(self.L.lpc_prof_waves(self.h, ptr(rec), c.value, ctypes.byref(c)))
-        return rec
 
     def prof_read(self, reset=True):
         p = _lib.Prof()

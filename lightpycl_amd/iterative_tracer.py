@@ -25,21 +25,41 @@ reference's order (iteration, then ray).
 """
 from __future__ import annotations
 
+import ctypes
 import pickle
 import time
 
 import numpy as np
 
+from . import _lib
 from .engine import Engine, flatten_meshes, select_device
 
 
 def f32_sorted_sum(a):
     """``sum(np.sort(a))`` as the reference evaluates it (:115, :372): np.sort along the
-    last axis, then a sequential float32 accumulation."""
-    flat = np.sort(np.asarray(a), axis=-1).reshape(-1).astype(np.float32)
+    last axis, then a sequential float32 accumulation (liblpc's host loop: the
+    same adds in the same order as np.add.accumulate, without its output array)."""
+    a = np.asarray(a)
+    flat = (a if a.ndim == 2 and a.shape[-1] == 1 else np.sort(a, axis=-1)).reshape(-1)
+    flat = np.ascontiguousarray(flat, dtype=np.float32)
     if flat.size == 0:
         return np.float32(0.0)
-    return np.add.accumulate(flat, dtype=np.float32)[-1]
+    out = ctypes.c_float(0.0)
+    _lib.check(_lib.load().lpc_host_seq_sum_f32(flat.ctypes.data_as(ctypes.c_void_p), flat.size, ctypes.byref(out)))
+    return np.float32(out.value)
+
+
+_SUM_POOL = None
+
+
+def _background(fn, *args):
+    """Run fn(*args) on the tracer's helper thread (numpy's sort and the ctypes
+    call release the GIL): the input-power sum overlaps the scene and ray upload."""
+    global _SUM_POOL
+    if _SUM_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _SUM_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="lpc-sum")
+    return _SUM_POOL.submit(fn, *args)
 
 
 def _rot(axis):
@@ -145,9 +165,10 @@ class CL_Tracer:
         origin = np.asarray(origin, dtype=np.float32)
         dirs = np.asarray(dirs, dtype=np.float32)
         power = np.asarray(power, dtype=np.float32)
-        input_power = f32_sorted_sum(power)                            # :115
+        in_pow = _background(f32_sorted_sum, power)                    # :115, beside the uploads
         pow_shape0 = power.shape
-
+        ph["sources"] = clk() - t_ph
+        t_ph = clk()
         arrs = self._flatten(meshes)                                   # :121-151
         ph["flatten"] = clk() - t_ph
         t_ph = clk()
@@ -155,8 +176,13 @@ class CL_Tracer:
         self.tri_count = np.int32(arrs[0].shape[0])
         self.meshes = meshes
         self.geometry = (arrs[0], arrs[1], arrs[2])
+        ph["scene"] = clk() - t_ph
+        t_ph = clk()
         n = self.engine.set_rays(origin, dirs, power.reshape(-1), max_ray_len, ior_env)
-        ph["upload"] = clk() - t_ph
+        ph["set_rays"] = clk() - t_ph
+        t_ph = clk()
+        input_power = in_pow.result()
+        ph["input_power_wait"] = clk() - t_ph
         t_ph = clk()
 
         self.results = []

@@ -33,6 +33,7 @@
  * scratch is [ray][mesh] (iterative_tracer.py:236-237,267).
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -370,3 +371,12 @@ void orc_stereograph_project(int64_t n, const float *vecs, const float *pwrs, co
 
 /* Build-identity helper for the ctypes loader. */
 int orc_abi_version(void) { return 1; }
+
+/* The OpenMP team of the calls above (the timed CPU baseline sets it to the
+ * process's affinity mask explicitly instead of inheriting OMP_NUM_THREADS);
+ * returns the team size in effect.  Not part of the reference. */
+int32_t orc_set_threads(int32_t n)
+{
+    if (n > 0) omp_set_num_threads(n);
+    return (int32_t)omp_get_max_threads();
+}

@@ -64,11 +64,19 @@ def lib():
         L.orc_angular_project.argtypes = [_i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_stereograph_project.argtypes = [_i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                               _f32p]
+        L.orc_set_threads.argtypes = [_i32]
+        L.orc_set_threads.restype = _i32
         for fn in (L.orc_intersect, L.orc_intersect_postproc, L.orc_reflect_refract_rays,
                    L.orc_angular_project, L.orc_stereograph_project):
             fn.restype = None
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP team size for the kernels above (n <= 0: leave it); returns the
+    team size in effect."""
+    return int(lib().orc_set_threads(int(n)))
 
 
 def _v4(a, n=None):
@@ -160,17 +168,18 @@ def f32_sorted_sum(a):
 
 
 def trace(light_source, meshes, trace_iterations=100, trace_until_dissipated=0.99,
-          max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True, bounce_fn=None):
+          max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True, bounce_fn=None,
+          measured_out=None):
     """Restatement of CL_Tracer.iterative_tracer (iterative_tracer.py:77-393).
 
     Returns (results, info) where results is the list of per-iteration tuples
     (rays_origin, rays_dest, rays_pow, rays_meas) and info holds the per-iteration
     ray counts and the per-mesh measured power (float64).  ``bounce_fn`` replaces
     the three kernels (default: :func:`bounce`, the C restatement); the GPU tests
-    pass the reference's own kernels (``tests/ref_gpu.py``) here."""
-    bounce_fn = bounce if bounce_fn is None else bounce_fn
-    max_ray_len = np.float32(max_ray_len)
-    ior_env = np.float32(ior_env)
+    pass the reference's own kernels (``tests/ref_gpu.py``) here.
+    ``measured_out`` (a list): each iteration's measured rays are appended as
+    (dest (m,4), pow (m,), hit mesh (m,)) -- get_measured_rays' rows plus the
+    mesh, without keeping the whole results tuples (large traces)."""
     origin = dirs = power = None
     for k, light in enumerate(light_source):                       # :99-113
         if k == 0:
@@ -181,8 +190,21 @@ def trace(light_source, meshes, trace_iterations=100, trace_until_dissipated=0.9
             origin = np.append(origin, light.rays_origin, axis=0).astype(np.float32)
             dirs = np.append(dirs, light.rays_dir, axis=0).astype(np.float32)
             power = np.append(power, light.rays_power, axis=0).astype(np.float32)
-    origin = np.asarray(origin)
-    dirs = np.asarray(dirs)
+    return trace_rays(origin, dirs, power, meshes, trace_iterations, trace_until_dissipated, max_ray_len,
+                      ior_env, keep_results, bounce_fn, measured_out)
+
+
+def trace_rays(origin, dirs, power, meshes, trace_iterations=100, trace_until_dissipated=0.99,
+               max_ray_len=np.float32(1e3), ior_env=np.float32(1.0), keep_results=True, bounce_fn=None,
+               measured_out=None):
+    """:func:`trace` from the concatenated emitted rays (iterative_tracer.py:99-113's
+    arrays: origin (N,4), dirs (N,4), power (N,1) or (N,)) instead of light sources."""
+    bounce_fn = bounce if bounce_fn is None else bounce_fn
+    max_ray_len = np.float32(max_ray_len)
+    ior_env = np.float32(ior_env)
+    origin = np.asarray(origin, np.float32)
+    dirs = np.asarray(dirs, np.float32)
+    power = np.asarray(power, np.float32)
     ray_count = origin.shape[0]
     input_power = f32_sorted_sum(power)                            # :115
     rays_pow = np.array(power, dtype=np.float32)                   # :116
@@ -200,6 +222,8 @@ def trace(light_source, meshes, trace_iterations=100, trace_until_dissipated=0.9
         rays_meas = out["meas"]
         m = rays_meas >= 0.9
         np.add.at(mesh_power, out["isect_mid"][m], rays_pow.reshape(-1)[m].astype(np.float64))
+        if measured_out is not None:
+            measured_out.append((rays_dest[m], rays_pow.reshape(-1)[m], out["isect_mid"][m]))
         if keep_results:
             results.append((origin, rays_dest, rays_pow, rays_meas))   # :355
         keep = np.where(np.concatenate((out["r_meas"], out["t_meas"])) == 0)[0]   # :366

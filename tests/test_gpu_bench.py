@@ -2,7 +2,11 @@
 with no WORLD_SIZE starts N ranks itself (torch.distributed.run as a child
 process).  On the one-GPU test box LPC_BENCH_REHEARSE=1 puts both ranks on GPU 0
 (gloo for the trace-end exchange); the line must say n_gpus == 2, carry both
-ranks' times, and every timed step must give identical counts."""
+ranks' times, and every timed step must give identical counts.  The strong
+block (one fixed global ray set split with shard_bounds) and the config-5 block
+(fixed ray blocks split over the ranks) must give the global per-iteration
+counts of the N = 1 trace of the same rays (the reference's global termination,
+iterative_tracer.py:383-391, taken on the all-reduced sums)."""
 import json
 import os
 import subprocess
@@ -15,19 +19,38 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_gpus2_launches_two_ranks():
+ARGS = ["--steps", "5", "--warmup", "1", "--no-cpu", "--no-configs", "--rays", "200000", "--strong-steps", "5",
+        "--c5-rays", "1600000", "--c5-steps", "2"]
+
+
+def _bench(gpus):
     env = dict(os.environ, LPC_BENCH_REHEARSE="1")
     env.pop("WORLD_SIZE", None)
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5",
-                        "--warmup", "1", "--no-cpu", "--no-configs", "--rays", "200000"],
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus)] + ARGS,
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-4000:]
-    out = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_launches_two_ranks():
+    out = _bench(2)
     assert out["n_gpus"] == 2
     assert out["parity"]["steps_identical"] is True
     assert len(out["rank_ms_per_step"]["per_rank"]) == 2
     assert out["rank_ms_per_step"]["max"] == pytest.approx(out["ms_per_step"], rel=1e-9)
     assert out["exchange"]["rehearsal_one_gpu"] is True
     assert out["value"] > 0
+
+    one = _bench(1)
+    for blk in ("strong", "config5"):
+        a, b = out[blk], one[blk]
+        assert a["global_counts"] == b["global_counts"], (blk, a["global_counts"], b["global_counts"])
+        assert a["steps_identical"] and b["steps_identical"]
+        assert len(a["rank_ms_per_step"]["per_rank"]) == 2
+        # per-mesh power: the ranks' float64 sums added in rank order vs one sum
+        for x, y in zip(a["mesh_power"], b["mesh_power"]):
+            assert x == pytest.approx(y, rel=1e-9, abs=1e-300)
+    # at N = 1 the strong block traces the weak block's rays (seed 7)
+    assert one["strong"]["global_counts"] == one["weak_global_counts"]

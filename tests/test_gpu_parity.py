@@ -11,6 +11,9 @@ and the C library's exp / acos / atan2 / sin / cos: children directions and
 powers then within a few ulp, decisions and destinations still exact.
 """
 import ctypes
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -86,48 +89,25 @@ def test_bounce_bitexact_two_levels(engine, oracle_mod, checker, name, n):
     _cmp_bounce(g2, r2, exact)
 
 
-_OLD = dict(LPC_QUEUE="0")          # k_intersect + k_spill levels instead of the root items
 _POLICIES = [
-    # coherence sort off / onesweep at every size, sliver culling off, packets per sliver wave
-    dict(LPC_SORT="0"), dict(LPC_ONESWEEP_MIN="0"), dict(LPC_SLIVER_CULL="0"),
-    dict(LPC_SLIVER_PPW="1"), dict(LPC_SLIVER_PPW="7"), dict(LPC_NODE_W="4"),
-    # root items walked by k_rootwalk (default): piece level, grid, root-test kernels
-    dict(LPC_Q_TARGET="1"), dict(LPC_Q_TARGET="10000000"), dict(LPC_Q_WALK_BLOCKS="1"),
-    dict(LPC_SIDE_STREAM="0"), dict(LPC_EARLY_ACC="0"), dict(LPC_SLIVER_LATE="0"),
-    dict(LPC_HALF="0"), dict(LPC_HALF="1"), dict(LPC_HALF="2"), dict(LPC_HALF="4"), dict(LPC_SHADE_KU="0"),
-    dict(LPC_ROOTS_S="0"), dict(LPC_ROOTS_S="1"), dict(LPC_ROOTS_S="16"),
-    dict(LPC_ROOTS_GATE="0"), dict(LPC_ROOTS_GATE="0", LPC_Q_TARGET="10000000"), dict(LPC_Q_TARGET="3000000"),
-    # the batched walk (LPC_NB nodes per step), with hand-over queues that overflow
-    dict(LPC_WALK_NB="4"), dict(LPC_WALK_NB="4", LPC_BUDGET="2", LPC_SPILL_CAP="100"),
-    dict(LPC_WALK_NB="4", LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
-    # work hand-over: budgets, a queue that overflows
+    # the piece-root half-line cull off (LPC_HALF 0; 3 is the default)
+    dict(LPC_HALF="0"),
+    # work hand-over: budgets, queues that overflow (the wave carries on itself)
     dict(LPC_BUDGET="4"), dict(LPC_BUDGET="2", LPC_SPILL_CAP="100"), dict(LPC_BUDGET="0"),
-    dict(LPC_BUDGET="0", LPC_HALF="1"),
-    dict(LPC_BUDGET="3", LPC_SPILL_LEVELS_SMALL="5"),
-    dict(LPC_BUDGET="2", LPC_SPILL_LEVELS_SMALL="7", LPC_SPILL_CAP="3000"),
-    dict(LPC_LARGE_N="1000"), dict(LPC_LARGE_N="1000", LPC_BUDGET_LARGE="3"),
-    # items sharded by piece and claimed XCD-first by a resident grid; small budgets
-    dict(LPC_XCD_CLAIM="1"), dict(LPC_XCD_CLAIM="1", LPC_Q_TARGET="1000000"),
-    dict(LPC_XCD_CLAIM="1", LPC_BUDGET="3"), dict(LPC_BUDGET_SMALL="0"), dict(LPC_BUDGET_SMALL="5"),
-    dict(LPC_HALF_SMALL="1"), dict(LPC_DS_CAP="0"),
-    # slivers in the walk's grid (k_rootwalk's tail), or after the root tests
-    dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="1"),
-    dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="33", LPC_SLIVER_CULL="0"),
-    dict(_OLD, LPC_SLIVER_MERGE="0"), dict(LPC_FORK_ROOTS_MIN="0"), dict(LPC_THIN="0"), dict(LPC_THIN="25"),
-    # the gather with the root tests fused in
-    dict(LPC_GATHER_ROOTS="0"), dict(LPC_GATHER_ROOTS="1", LPC_HALF="4"), dict(LPC_GATHER_ROOTS="1", LPC_Q_TARGET="1"),
-    # the k_intersect alternative and its knobs
-    dict(_OLD), dict(_OLD, LPC_WAVE_TARGET="2000"), dict(_OLD, LPC_WAVE_TARGET="0"),
-    dict(_OLD, LPC_BUDGET="0"), dict(_OLD, LPC_BUDGET="6", LPC_SPILL_CAP="100"),
-    dict(_OLD, LPC_NODE_W="4", LPC_BUDGET="5", LPC_TARGET_BLOCKS="65536"),
+    dict(LPC_BUDGET="0", LPC_HALF="0"), dict(LPC_BUDGET="3", LPC_SPILL_CAP="3000"),
+    # no hand-over from 0 rays per triangle (always) / hand-over at every size
+    dict(LPC_LARGE_PER_TRI="0"), dict(LPC_LARGE_PER_TRI="1000000", LPC_BUDGET="3"),
+    # slivers in the walk's grid (k_rootwalk's tail) at every size
+    dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_BUDGET="2", LPC_SPILL_CAP="100"),
+    # a filter-record rebuild below the emitted |D| (Dcap 0.5: unit directions exceed it)
+    dict(LPC_DCAP_MILLI="500"),
 ]
-
-
 @pytest.mark.parametrize("cfg", _POLICIES)
 def test_launch_policies_bitexact(oracle_mod, checker, monkeypatch, cfg):
-    """The launch policies (root items or k_intersect, piece granularity, no
-    sort, hand-over budgets and queues that overflow, grid sizes) change only
-    speed."""
+    """The size switches and test hooks that remain (the half-line cull,
+    hand-over budgets and queues that overflow, merged sliver units, a record
+    rebuild) change only speed: every bounce is bit-exact against the reference's
+    kernels."""
     from lightpycl_amd.engine import Engine
     for k, v in cfg.items():
         monkeypatch.setenv(k, v)
@@ -349,74 +329,32 @@ def test_trace_run_matches_host_loop(oracle_mod, checker):
 
 @pytest.mark.parametrize("name,n,chunk", [("synthetic", 20000, 0), ("lens", 20000, 0), ("eye", 3000, 0),
                                           ("lens", 20000, 7000), ("eye", 6000, 5000), ("synthetic", 30000, 6000)])
-def test_traced_order_equals_reference_order(monkeypatch, name, n, chunk):
-    """Aggregate iterations in the launch's coherence order (traced mode, the
-    default without per-ray export) against the same trace in the reference's
-    ray order (LPC_TRACED=0): identical per-iteration counts, identical measured
-    rays as a set (bit for bit), per-mesh power to float64 summation order.
-    With a chunk size below the population the traced iterations run chunk by
-    chunk (k_shade_stage + k_stage_move per chunk, running row bases, k_append
-    of the staged refracted block)."""
+def test_aggregate_trace_matches_reference_kernels(oracle_mod, exact_ref, name, n, chunk):
+    """Aggregate iterations (traced order: the launch's coherence order, the
+    default without per-ray export) against the reference's host loop over the
+    reference's own kernels: identical per-iteration counts, per-mesh power to
+    float64 summation order, the measured rays bit for bit as a set.  With a
+    chunk size below the population the traced iterations run chunk by chunk
+    (k_shade_stage + k_stage_move per chunk, running row bases, k_append of the
+    staged refracted block)."""
+    from parity_util import assert_aggregate_equal, lib_aggregate, ref_aggregate
     from lightpycl_amd.engine import Engine
+    if exact_ref is None:
+        pytest.skip("oracle/_ref not built")
     sc = scenes.BUILDERS[name](n=n, seed=21)
     o4, d4, pw = rays_of(sc)
     thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for traced in ("1", "0"):
-        monkeypatch.setenv("LPC_TRACED", traced)
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_chunk(chunk)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-            pos, p, mm = e.fetch_measured()
-            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm))
-        finally:
-            e.close()
-    a, b = out
-    assert a[0] == b[0] and a[1] == b[1]
-    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)
-
-    def rows(pos, p, mm):
-        r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
-        return r[np.lexsort(r.T[::-1])]
-    np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("name,n", [("synthetic", 100000), ("lens", 50000), ("eye", 4000), ("cube", 3000)])
-def test_fused_compaction_equals_four_kernels(monkeypatch, name, n):
-    """k_shade_compact (shade, counts, look-back scan and scatter in one pass)
-    against k_shade + k_count + k_scan + k_scatter (LPC_FUSE_COMPACT=0): the same
-    children at the same positions, so identical per-iteration counts and the
-    identical measured record, element for element."""
-    from lightpycl_amd.engine import Engine
-    sc = scenes.BUILDERS[name](n=n, seed=23)
-    o4, d4, pw = rays_of(sc)
-    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("LPC_FUSE_COMPACT", fused)
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            for rep in range(2):            # the tile words of the first trace must not leak into the second
-                e.reset()
-                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-            pos, p, mm = e.fetch_measured()
-            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm,
-                        [s.power_next for s in stats]))
-        finally:
-            e.close()
-    a, b = out
-    assert a[0] == b[0] and a[1] == b[1]
-    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)     # per-tile vs record-order float64 sums
-    for x, y in zip(a[3:6], b[3:6]):
-        np.testing.assert_array_equal(x, y)
-    np.testing.assert_allclose(a[6], b[6], rtol=1e-12)
-
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        e.set_chunk(chunk)
+        e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+        lib = lib_aggregate(e, sc.iterations, thr, reps=2)
+    finally:
+        e.close()
+    ref = ref_aggregate(oracle_mod, exact_ref.bounce, sc.meshes, o4, d4, pw, sc.iterations, sc.tau, sc.max_ray_len,
+                        sc.ior_env)
+    assert_aggregate_equal(lib, ref, f"{name} {n} chunk {chunk}")
 
 
 def test_clean_slots_across_paths(oracle_mod):
@@ -496,15 +434,18 @@ def test_async_trace_run_equals_sync(name, n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,n", [("synthetic", 200000), ("lens", 50000), ("eye", 30000), ("same", 5000),
                                     ("beam", 60000)])
-def test_counting_sort_equals_radix_sort(monkeypatch, name, n):
-    """The emitted rays' counting sort (k_bkey / k_bprefix / k_bscatter /
-    k_bsort2, key windows of <= 16 bits: a point source's 16 direction bits, a
-    collimated beam's 15 origin-cell bits, one 8-bit level when nothing varies)
-    against rocPRIM's radix sort of the same window (LPC_BSORT=0).  Both are
-    stable sorts of the same keys, so the coherence order is the same
-    permutation: identical counts, per-mesh power and measured record, element
-    for element, in traced order."""
+def test_emitted_sort_paths_match_reference(oracle_mod, exact_ref, name, n):
+    """The emitted rays' coherence sort takes the counting sort (k_bkey /
+    k_bprefix / k_bscatter / k_bsort2, key windows of <= 16 bits: a point source's
+    16 direction bits, a collimated beam's 15 origin-cell bits, one 8-bit level
+    when nothing varies) or rocPRIM's radix sort (a narrow beam's few origin
+    cells): either way the trace equals the reference kernels' (counts, per-mesh
+    power, measured rays as a set), twice back to back (the digit counts of the
+    first trace must not leak into the second)."""
+    from parity_util import assert_aggregate_equal, lib_aggregate, ref_aggregate
     from lightpycl_amd.engine import Engine
+    if exact_ref is None:
+        pytest.skip("oracle/_ref not built")
     if name == "same":                      # every ray identical: one 8-bit level
         sc = scenes.lens(n=10, seed=3)
         o4, d4, pw = rays_of(sc)
@@ -523,196 +464,123 @@ def test_counting_sort_equals_radix_sort(monkeypatch, name, n):
         sc = scenes.BUILDERS[name](n=n, seed=29)
         o4, d4, pw = rays_of(sc)
     thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for bs in ("1", "0"):
-        monkeypatch.setenv("LPC_BSORT", bs)
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            for rep in range(2):            # the digit counts of the first trace must not leak
-                e.reset()
-                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-            pos, p, mm = e.fetch_measured()
-            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, list(mp),
-                        pos, p, mm))
-        finally:
-            e.close()
-    a, b = out
-    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
-    for x, y in zip(a[3:], b[3:]):
-        np.testing.assert_array_equal(x, y)
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+        lib = lib_aggregate(e, sc.iterations, thr, reps=2)
+    finally:
+        e.close()
+    ref = ref_aggregate(oracle_mod, exact_ref.bounce, sc.meshes, o4, d4, pw, sc.iterations, sc.tau, sc.max_ray_len,
+                        sc.ior_env)
+    assert_aggregate_equal(lib, ref, name)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n", [("lens", 30000), ("eye", 3000)])
-def test_resort_equals_chained(monkeypatch, name, n):
-    """Large chained populations sorted again (LPC_RESORT_MIN; default 2 M rays,
-    here forced from 1000) against the children kept in their parents' traced
-    order: the same per-ray results in another order, so identical per-iteration
-    counts and the identical measured rays as a set, per-mesh power to float64
-    summation order."""
+@pytest.mark.parametrize("name,n,env", [
+    # chained populations re-sorted (LPC_RESORT_MIN lowered from 2 M rays) against
+    # kept in their parents' traced order (re-sort off)
+    ("lens", 30000, dict(LPC_RESORT_MIN="1000")), ("eye", 3000, dict(LPC_RESORT_MIN="1000")),
+    ("lens", 30000, dict(LPC_RESORT_MIN="1000000000000")), ("eye", 3000, dict(LPC_RESORT_MIN="1000000000000")),
+    # every iteration of the dense scene re-sorted and keyed in its population's box
+    ("synthetic_dense", 20000, dict(LPC_RESORT_MIN="4096")),
+    # the gather with the root tests fused in, on re-sorted populations too
+    ("synthetic", 200000, dict(LPC_RESORT_MIN="20000")), ("eye", 30000, dict(LPC_RESORT_MIN="20000")),
+    ("synthetic_dense", 60000, dict(LPC_RESORT_MIN="20000")),
+    # written-slot masks over K = 10 and K = 12 meshes, three traces back to back
+    ("synthetic", 50000, dict()), ("nested_cubes", 2000, dict()),
+])
+def test_population_paths_match_reference(oracle_mod, exact_ref, monkeypatch, name, n, env):
+    """The population paths (re-sort of chained populations and its 5-D Morton
+    key in the population's own box, k_gather_roots, written-slot masks across
+    back-to-back traces) against the reference kernels' trace: identical counts,
+    per-mesh power to float64 summation order, measured rays as a set."""
+    from parity_util import assert_aggregate_equal, lib_aggregate, ref_aggregate
     from lightpycl_amd.engine import Engine
-    sc = scenes.BUILDERS[name](n=n, seed=31)
+    if exact_ref is None:
+        pytest.skip("oracle/_ref not built")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    kw = dict(iterations=8) if name == "synthetic_dense" else {}
+    sc = scenes.BUILDERS[name](n=n, seed=31, **kw)
     o4, d4, pw = rays_of(sc)
     thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for rmin in ("1000", "1000000000000"):
-        monkeypatch.setenv("LPC_RESORT_MIN", rmin)
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            for rep in range(2):
-                e.reset()
-                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-            pos, p, mm = e.fetch_measured()
-            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm))
-        finally:
-            e.close()
-    a, b = out
-    assert a[0] == b[0] and a[1] == b[1]
-    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)
-
-    def rows(pos, p, mm):
-        r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
-        return r[np.lexsort(r.T[::-1])]
-    np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+        lib = lib_aggregate(e, sc.iterations, thr, reps=3)
+    finally:
+        e.close()
+    ref = ref_aggregate(oracle_mod, exact_ref.bounce, sc.meshes, o4, d4, pw, sc.iterations, sc.tau, sc.max_ray_len,
+                        sc.ior_env)
+    assert len(ref[0]) >= 3
+    assert_aggregate_equal(lib, ref, f"{name} {env}")
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("name,n", [("synthetic", 50000), ("lens", 20000), ("nested_cubes", 2000)])
-def test_written_slot_masks_equal_full_reads(monkeypatch, name, n):
-    """Written-slot masks (LPC_TMASK, default on: the shading reads only the
-    slots a flush wrote) against the shading reading every slot: the same trace
-    bit for bit -- per-iteration counts, per-mesh power, measured rays in order.
-    Three back-to-back traces, so the masks' clearing between iterations and
-    traces is exercised too."""
-    from lightpycl_amd.engine import Engine
-    sc = scenes.BUILDERS[name](n=n, seed=37)
-    o4, d4, pw = rays_of(sc)
-    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for tm in ("1", "0"):
-        monkeypatch.setenv("LPC_TMASK", tm)
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            runs = []
-            for rep in range(3):
-                e.reset()
-                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-                runs.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt,
-                             [float(x) for x in mp]))
-            pos, p, mm = e.fetch_measured()
-            out.append((runs, pos, p, mm))
-        finally:
-            e.close()
-    a, b = out
-    assert a[0] == b[0]
-    assert a[0][0] == a[0][1] == a[0][2]
-    for x, y in zip(a[1:], b[1:]):
-        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
-
-
-@pytest.mark.parametrize("env", [dict(LPC_POPBOX="0"), dict(LPC_KEY_OBITS="7"), dict(LPC_KEY_OBITS="4"),
-                                 dict(LPC_XCD_CLAIM="1"), dict(LPC_KEY_MODE="0", LPC_KEY_OBITS="5"),
-                                 dict(LPC_KEY_MODE="2")])
-def test_resorted_populations_keys(monkeypatch, env):
-    """Re-sorted chained populations (LPC_RESORT_MIN lowered so that every
-    iteration of the dense synthetic scene is re-sorted): the coherence key in the
-    population's own origin box (default), in the scene box, or with another
-    origin/direction split changes only the order of the work -- identical
-    per-iteration counts, the measured rays as a set, per-mesh power to float64
-    summation order."""
-    from lightpycl_amd.engine import Engine
-    sc = scenes.synthetic_dense(n=20000, seed=31, iterations=8)
-    o4, d4, pw = rays_of(sc)
-    thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for e_env in (dict(), env):
-        for k in ("LPC_POPBOX", "LPC_KEY_OBITS", "LPC_XCD_CLAIM", "LPC_KEY_MODE"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in e_env.items():
-            monkeypatch.setenv(k, v)
-        monkeypatch.setenv("LPC_RESORT_MIN", "4096")
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-            pos, p, mm = e.fetch_measured()
-            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, mp, pos, p, mm))
-        finally:
-            e.close()
-    a, b = out
-    assert len(a[0]) >= 4
-    assert a[0] == b[0] and a[1] == b[1]
-    np.testing.assert_allclose(a[2], b[2], rtol=1e-12)
-
-    def rows(pos, p, mm):
-        r = np.concatenate([pos[:, :3].astype(np.float64), p.reshape(-1, 1), mm.reshape(-1, 1)], axis=1)
-        return r[np.lexsort(r.T[::-1])]
-    np.testing.assert_array_equal(rows(*a[3:]), rows(*b[3:]))
-
-
-@pytest.mark.parametrize("cfg", [dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_SLIVER_MERGE_PPW="1"),
-                                 dict(LPC_THIN="0"), dict(LPC_THIN="25"), dict(LPC_FORK_ROOTS_MIN="0"),
-                                 dict(LPC_SLIVER_MERGE="0", LPC_RESORT_MIN="4096"), dict(LPC_GATHER_ROOTS="1"),
-                                 dict(LPC_GATHER_ROOTS="1", LPC_RESORT_MIN="4096")])
-def test_eye_policies_identical(monkeypatch, cfg):
-    """The eye (the scene with thin triangles on the sliver path): whole traces in
-    results mode under the sliver placement policies equal the default's, every
-    results tuple element for element (the default itself equals the reference's
-    kernels: test_trace_results_match_reference)."""
+@pytest.mark.parametrize("cfg", [dict(), dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="-1"),
+                                 dict(LPC_SLIVER_MERGE="0", LPC_RESORT_MIN="4096"), dict(LPC_RESORT_MIN="4096")])
+def test_eye_results_mode_policies_match_reference(oracle_mod, exact_ref, monkeypatch, cfg):
+    """The eye (thin triangles on the sliver path), results mode: every results
+    tuple element for element equals the reference host loop over the
+    reference's kernels, with the sliver units merged into the walk's grid at
+    every size / never, and re-sorted chained populations."""
     from lightpycl_amd.iterative_tracer import CL_Tracer
-    sc = scenes.eye(n=3000, seed=6)
-
-    def trace():
-        tr = CL_Tracer(device=0)
-        res = tr.iterative_tracer(light_source=sc.sources, meshes=sc.meshes, trace_iterations=sc.iterations,
-                                  trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env)
-        return [tuple(np.array(a) for a in r) for r in res]
-
-    base = trace()
+    if exact_ref is None:
+        pytest.skip("oracle/_ref not built")
     for k, v in cfg.items():
         monkeypatch.setenv(k, v)
-    got = trace()
-    assert len(got) == len(base) >= 3
-    for it, (a, b) in enumerate(zip(got, base)):
-        for x, y in zip(a, b):
-            np.testing.assert_array_equal(x, y, err_msg=f"it{it} {cfg}")
+    sc = scenes.eye(n=3000, seed=6)
+    ref, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                                 bounce_fn=exact_ref.bounce)
+    tr = CL_Tracer(device=0)
+    res = tr.iterative_tracer(light_source=sc.sources, meshes=sc.meshes, trace_iterations=sc.iterations,
+                              trace_until_dissipated=sc.tau, max_ray_len=sc.max_ray_len, ior_env=sc.ior_env)
+    assert [len(r[3]) for r in res] == info["counts"] and len(res) >= 3
+    for it, (a, b) in enumerate(zip(res, ref)):
+        for k, (x, y) in enumerate(zip(a, b)):
+            x, y = np.asarray(x), np.asarray(y)
+            if x.ndim == 2 and x.shape[1] == 4:
+                x, y = x[:, :3], y[:, :3]
+            np.testing.assert_array_equal(x, y, err_msg=f"it{it} field{k} {cfg}")
 
 
-@pytest.mark.parametrize("name,n", [("synthetic", 200000), ("eye", 30000), ("synthetic_dense", 60000)])
-def test_gather_roots_equals_separate_kernels(monkeypatch, name, n):
-    """k_gather_roots (the coherence gather with the root tests fused in) writes
-    the same root items as k_gather_aos + k_roots_s (their order inside a shard
-    differs; results do not depend on it): identical traces -- counts, per-mesh
-    power and the measured record element for element, in traced order -- with
-    re-sorted chained populations too (LPC_RESORT_MIN)."""
+# The default paths that switch on only for large populations, whole traces
+# under the DEFAULT policy (no threshold overrides) against the reference host
+# loop over the reference's own kernels (iterative_tracer.py:241-391,
+# .cl:243-474): the eye's populations pass 2 M (re-sort, k_gather_roots on
+# re-sorted populations) and 4 M rays (merged sliver units) and 16 rays per
+# triangle (no hand-over); the dense synthetic layout is the scene the
+# population-box key was tuned on; a chunk size below the population runs the
+# multi-chunk traced compaction (k_stage_move per chunk, k_append).
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,chunk", [("eye", 100000, 0), ("synthetic_dense", 300000, 0),
+                                          ("eye", 30000, 1000000), ("synthetic_dense", 100000, 700000)])
+def test_large_population_defaults_match_reference(oracle_mod, exact_ref, name, n, chunk):
+    from parity_util import assert_aggregate_equal, lib_aggregate, ref_aggregate
     from lightpycl_amd.engine import Engine
-    sc = scenes.BUILDERS[name](n=n, seed=31)
+    if exact_ref is None:
+        pytest.skip("oracle/_ref not built")
+    sc = scenes.BUILDERS[name](n=n, seed=43)
     o4, d4, pw = rays_of(sc)
     thr = (1.0 - sc.tau) * float(np.sum(pw, dtype=np.float64))
-    out = []
-    for gr in ("1", "0"):
-        monkeypatch.setenv("LPC_GATHER_ROOTS", gr)
-        monkeypatch.setenv("LPC_RESORT_MIN", "20000")
-        e = Engine(0)
-        try:
-            e.upload_meshes(sc.meshes)
-            e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
-            for rep in range(2):
-                e.reset()
-                stats, (cnt, mp) = e.run_local(sc.iterations, thr)
-            pos, p, mm = e.fetch_measured()
-            out.append(([(s.n_in, s.n_reflect, s.n_refract, s.n_measured) for s in stats], cnt, list(mp),
-                        pos, p, mm))
-        finally:
-            e.close()
-    a, b = out
-    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
-    for x, y in zip(a[3:], b[3:]):
-        np.testing.assert_array_equal(x, y)
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        e.set_chunk(chunk)
+        e.set_rays(o4, d4, pw, sc.max_ray_len, sc.ior_env)
+        lib = lib_aggregate(e, sc.iterations, thr, reps=1)
+    finally:
+        e.close()
+    ref = ref_aggregate(oracle_mod, exact_ref.bounce, sc.meshes, o4, d4, pw, sc.iterations, sc.tau, sc.max_ray_len,
+                        sc.ior_env)
+    pops = ref[0]
+    if chunk == 0 and name == "eye":
+        assert max(pops) > 4_000_000, pops          # re-sort (2 M) and merged sliver units (4 M) engaged
+    if chunk:
+        assert max(pops) > chunk, pops              # some iteration ran in several chunks
+    with open(os.path.join(os.environ.get("LPC_TEST_OUT", "/tmp"), "large_population_parity.jsonl"), "a") as f:
+        f.write(json.dumps(dict(scene=name, rays=n, chunk=chunk, populations=pops, bounces=int(sum(pops)),
+                                measured=int(len(ref[2])), mesh_power=[float(x) for x in ref[1]],
+                                identical=True)) + "\n")
+    assert_aggregate_equal(lib, ref, f"{name} {n} chunk {chunk}")

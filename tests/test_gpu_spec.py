@@ -108,3 +108,40 @@ def test_speculation_dcap_rebuild(monkeypatch):
     finally:
         a.close()
         b.close()
+
+
+def test_speculation_dcap_overflow_in_an_earlier_chunk(monkeypatch):
+    """A chunked traced iteration whose kept children exceed Dcap only in a chunk
+    before the last (the sphere hitters ordered first, 5 000-ray chunks), with the
+    next iteration speculated device-sized: the device must stop that iteration
+    on the whole iteration's max |D| (not the last chunk's), and a discarded
+    iteration's measured power must not count.  The trace equals the host-sized
+    one bit for bit."""
+    from lightpycl_amd.engine import Engine
+    monkeypatch.setenv("LPC_DCAP_MILLI", "600")
+    sc = scenes.synthetic(n=60000, seed=54)
+    o4, d4, pw = _rays(sc, dscale=0.5)
+    probe = Engine(0)
+    try:
+        probe.upload_meshes(sc.meshes)
+        z = np.zeros(len(pw), np.int32)
+        g = probe.bounce(o4, d4, pw, z, np.full(len(pw), -2, np.int32), sc.max_ray_len, sc.ior_env)
+    finally:
+        probe.close()
+    hits = np.asarray(g["isect_mid"]) > 0                 # a sphere (mesh 0 is the measure hemisphere)
+    order = np.concatenate([np.where(hits)[0], np.where(~hits)[0]])
+    assert 0 < hits.sum() < 5000
+    rays = (o4[order], d4[order], pw[order])
+    a = _engine(monkeypatch, "0", sc)
+    b = _engine(monkeypatch, "1", sc)
+    try:
+        a.set_chunk(5000)
+        b.set_chunk(5000)
+        want = _trace(a, sc, rays)
+        assert len(want[0]) >= 2
+        for _ in range(3):                 # the first builds the prediction, the others speculate
+            b.upload_meshes(sc.meshes)     # Dcap back to 0.6
+            _same(_trace(b, sc, rays), want)
+    finally:
+        a.close()
+        b.close()
