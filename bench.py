@@ -246,6 +246,11 @@ def cpu_leg(sc, eng, o, d, p, nrays, first_stats, timed):
         oracle.bounce(S, o[:n16], d[:n16], p[:n16], z[:n16], pm[:n16], sc.max_ray_len, sc.ior_env)
         d16 = time.perf_counter() - t
         base["at_16_threads"] = {"value": n16 / d16, "rays": n16, "seconds": d16}
+        q = base["cgroup_cpu_max"]
+        if q and q.get("cpus") and q["cpus"] < threads:
+            base["note"] = (f"{threads} threads = every core of the affinity mask; the container's cgroup grants "
+                            f"{q['cpus']:g} CPUs of bandwidth (cpu.max {q['raw']}), so those threads share "
+                            f"{q['cpus']:g} CPUs' time and the 16-thread figure beside it is the faster one")
         oracle.set_threads(threads)
     return parity, base
 

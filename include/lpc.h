@@ -281,6 +281,8 @@ typedef struct {
                                 timestamps; intersect_ms adds k_spill, k_packet, k_slivers) */
     double xchg_us;          /* host time spent in the all-reduce hook (lpc_set_allreduce) */
     int64_t xchg_calls;      /* its calls (per-iteration stats + trace-end aggregates)  */
+    int64_t walk_cycles;     /* level 2: summed shader-clock cycles of the walk items (per wave) */
+    int64_t drain_cycles;    /* ... of them inside the exact-test drains                         */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * traversal counters (2, diagnostic: adds atomics), only the walk kernel's

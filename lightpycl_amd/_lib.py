@@ -36,7 +36,8 @@ class Prof(ctypes.Structure):
                 ("heavy_piece_ticks", ctypes.c_int64), ("piece_ticks", ctypes.c_int64),
                 ("tail_waves", ctypes.c_int64), ("tail_nodes", ctypes.c_int64),
                 ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64),
-                ("kernel_ms", ctypes.c_double), ("xchg_us", ctypes.c_double), ("xchg_calls", ctypes.c_int64)]
+                ("kernel_ms", ctypes.c_double), ("xchg_us", ctypes.c_double), ("xchg_calls", ctypes.c_int64),
+                ("walk_cycles", ctypes.c_int64), ("drain_cycles", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

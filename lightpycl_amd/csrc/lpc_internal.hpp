@@ -36,7 +36,8 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 #define LPC_STATS_HIST 8
 #define LPC_STATS_PIECE 32
 #define LPC_STATS_PIECES 4096
-#define LPC_STATS_WORDS (LPC_STATS_PIECE + LPC_STATS_PIECES)
+#define LPC_STATS_CYC (LPC_STATS_PIECE + LPC_STATS_PIECES)   // [CYC]: walk cycles, [CYC + 1]: drain cycles
+#define LPC_STATS_WORDS (LPC_STATS_CYC + 8)
 
 // Per-launch device words of the intersect stage (uint32, reset by k_slot_init
 // or k_stage_move): [6..13] hand-over queue lengths (k_intersect / k_rootwalk ->

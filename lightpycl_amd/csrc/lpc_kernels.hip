@@ -372,7 +372,13 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     // results into the per-ray accumulators with LDS atomics: atomicMin on
     // slot_key(t, idx) for t < max_ray_len and a count for every accepted t > eps,
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
-    auto drain = [&]() { drain_queue<PROF>(L, nq, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact); };
+    uint64_t cyc_drain = 0;                         // PROF: shader-clock cycles in the drains
+    const uint64_t cyc0 = (PROF && stats) ? clock64() : 0;
+    auto drain = [&]() {
+        const uint64_t c0 = (PROF && stats) ? clock64() : 0;
+        drain_queue<PROF>(L, nq, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact);
+        if (PROF && stats) cyc_drain += clock64() - c0;
+    };
     int budget = SP.budget;
     L.stack[top++] = start;
     while (top > 0) {
@@ -442,6 +448,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
                 atomicAdd(&stats[7], (unsigned long long)n_exact);
             }
             atomicAdd(&stats[0], (unsigned long long)n_nodes);
+            atomicAdd(&stats[LPC_STATS_CYC], (unsigned long long)(clock64() - cyc0));
+            atomicAdd(&stats[LPC_STATS_CYC + 1], (unsigned long long)cyc_drain);
             atomicAdd(&stats[2], 1ull);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
             atomicAdd(&stats[LPC_STATS_HIST + b], 1ull);
@@ -651,7 +659,7 @@ static __device__ __forceinline__ void sliver_launch_size(const SliverArgs &A, i
 // One wave per block: a block's slots free as soon as its item ends, where a
 // 4-wave block holds its LDS until its slowest item ends (round 2 per-item
 // records: ~2 800 of 6 144 wave slots walking on average with 4).
-template <int W, bool PROF = false>
+template <int W, bool PROF = false, bool MERGED = false>
 __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int64_t n,
                                                      const int32_t *__restrict__ perm,
                                                      const NodeW<W> *__restrict__ nodes,
@@ -685,7 +693,7 @@ __global__ __launch_bounds__(64, LPC_WALK_MINB) void k_rootwalk(RayBase ray, int
     // merged sliver tests (LPC_SLIVER_MERGE): (packet group, sliver piece) units
     // grid-stride after the root items, so the waves whose items end early take
     // them -- no second stream whose long-lived waves would hold the CUs
-    if (SA.nsp > 0) {
+    if (MERGED && SA.nsp > 0) {
         int64_t ns;
         float dmax;
         sliver_launch_size(SA, ns, dmax);

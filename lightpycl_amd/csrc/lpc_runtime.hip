@@ -78,7 +78,10 @@ const int64_t kSortMin = 4096;          // populations below this are traced uns
 const int64_t kOnesweepMin = 500000;    // rocPRIM onesweep radix sort from this many rays (merge sort below)
 const int kRootsPerBlock = 16;          // k_roots_s packets per block (one task per packet)
 const int64_t kQTarget = 65536;         // (packet, piece) root tests to aim for: the piece level
-const int64_t kWalkWaves = 65536;       // k_rootwalk grid (single-wave blocks, grid-stride)
+#ifndef LPC_WALK_GRID
+#define LPC_WALK_GRID 65536             // compile-time A/B builds (tools/build_variant.py)
+#endif
+const int64_t kWalkWaves = LPC_WALK_GRID;   // k_rootwalk grid (single-wave blocks, grid-stride)
 const int64_t kSliverMergePpw = 4;      // packets per merged sliver unit (k_rootwalk's tail)
 const int64_t kSliverWaves = 16384;     // k_slivers: (packet, piece) waves to aim for
 const int kSpillLevels = 3;             // k_spill levels (hand-over depth) for populations >= kSpillSmallN
@@ -958,15 +961,22 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
-    // profiling counters only in the PROF instantiation (fewer live registers without)
-    if (stats)
-        hipExtLaunchKernelGGL((k_rootwalk<8, true>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,
-                              (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
-                              stats, Q, SP, ds ? ds->nd : nullptr, SA);
-    else
-        hipExtLaunchKernelGGL((k_rootwalk<8, false>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,
-                              (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt,
-                              stats, Q, SP, ds ? ds->nd : nullptr, SA);
+    // profiling counters only in the PROF instantiation, the merged sliver units
+    // only in the MERGED one (fewer live registers without: the plain walk holds
+    // 7 waves per SIMD, the merged one 6)
+#define LPC_LAUNCH_WALK(PF, MG)                                                                                     \
+    hipExtLaunchKernelGGL((k_rootwalk<8, PF, MG>), dim3(grid), dim3(64), 0, h->stream, k0, k1, 0, ray, n, perm,      \
+                          (const Node8 *)h->d_nodes.p, (const ExactRec *)h->d_xrec.p, eps, max_ray_len, skey, scnt, \
+                          stats, Q, SP, ds ? ds->nd : nullptr, SA)
+    if (stats) {
+        if (merged) LPC_LAUNCH_WALK(true, true);
+        else LPC_LAUNCH_WALK(true, false);
+    } else if (merged) {
+        LPC_LAUNCH_WALK(false, true);
+    } else {
+        LPC_LAUNCH_WALK(false, false);
+    }
+#undef LPC_LAUNCH_WALK
     if (h->prof) h->ev_kern.push_back({k0, k1});
     return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP, ds ? ds->nd : nullptr);
 }
@@ -2059,8 +2069,15 @@ static int export_chunk(lpc_handle *h, const RaysIn &in, const ShadeOutPtrs &o, 
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev_xready[par], h->stream));
     HIPCHK(h, hipStreamWaitEvent(h->xstream, h->ev_xready[par], 0));
+    const double hm = h->host_prof ? host_us() : 0.0;
     if (nc == N) {
         HIPCHK(h, hipMemcpyAsync(X.host, d, (size_t)nc * row, hipMemcpyDeviceToHost, h->xstream));
+        if (h->host_prof) {
+            hipPointerAttribute_t pa;
+            const hipError_t pe = hipPointerGetAttributes(&pa, X.host);
+            fprintf(stderr, "[lpc host]   export memcpy %.1f us (host %p, %zu B, pointer type %d, rc %d)\n",
+                    host_us() - hm, (void *)X.host, (size_t)nc * row, pe == hipSuccess ? (int)pa.type : -1, (int)pe);
+        }
     } else {                                                    // chunk: each section at its rays' offset
         size_t hoff = 0, doff = 0;
         const size_t elt[4] = {orow, 16, 4, 4};
@@ -2094,11 +2111,15 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     if (N == 0) { P->empty = true; return 0; }
     const int64_t C = std::min(N, chunk_rays(h));
     if (ds && C < N) return set_err(h, LPC_E_STATE, "internal: device-sized iteration over one chunk only");
+    const double hp0 = h->host_prof ? host_us() : 0.0;
     RETIF(ensure_ws(h, C));
     RETIF(pop_reserve(h, h->B, 2 * N));
     if (!ds) RETIF(pop_reserve(h, h->T, N));
     // measured rows: the iterations still in flight may append up to their populations
     RETIF(ensure_measured(h, h->m_total + h->m_inflight + N));
+    if (h->host_prof)
+        fprintf(stderr, "[lpc host]   buffers %.1f us (m_total %lld inflight %lld m_cap %lld)\n", host_us() - hp0,
+                (long long)h->m_total, (long long)h->m_inflight, (long long)h->m_cap);
     h->m_inflight += N;
     if (ds) {
         h->acc_pending = false;         // k_stage_move writes every counter
@@ -2241,7 +2262,11 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
         }
         RETIF(run_shade(h, in, nullptr, nc, h->max_ray_len, h->ior_env, false));
         hipLaunchKernelGGL(k_count, dim3((unsigned)A.nb), dim3(256), 0, h->stream, A);
-        if (X) RETIF(export_chunk(h, in, o, nc, base, N, *X));
+        if (X) {
+            const double hx = h->host_prof ? host_us() : 0.0;
+            RETIF(export_chunk(h, in, o, nc, base, N, *X));
+            if (h->host_prof) fprintf(stderr, "[lpc host]   export chunk %.1f us\n", host_us() - hx);
+        }
         if (out_origin4 || out_dest4 || out_pow || out_meas) {
             // the copies below run on the null stream: the shading on h->stream first
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2768,6 +2793,7 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     for (int b = 0; b < 24; ++b) out->wave_hist[b] = (int64_t)st[LPC_STATS_HIST + b];
     out->tail_waves = (int64_t)st[4]; out->tail_nodes = (int64_t)st[5];
     out->tail_spread_urad = (int64_t)st[6]; out->tail_exact = (int64_t)st[7];
+    out->walk_cycles = (int64_t)st[LPC_STATS_CYC]; out->drain_cycles = (int64_t)st[LPC_STATS_CYC + 1];
     out->heavy_piece = -1; out->heavy_piece_ticks = 0; out->piece_ticks = 0;
     for (int p = 0; p < LPC_STATS_PIECES; ++p) {
         const int64_t v = (int64_t)st[LPC_STATS_PIECE + p];

@@ -407,4 +407,5 @@ class Engine:
                     wave_hist=list(p.wave_hist), heavy_piece=p.heavy_piece, heavy_piece_ticks=p.heavy_piece_ticks,
                     piece_ticks=p.piece_ticks, tail_waves=p.tail_waves, tail_nodes=p.tail_nodes,
                     tail_spread_urad=p.tail_spread_urad, tail_exact=p.tail_exact, kernel_ms=p.kernel_ms,
-                    xchg_us=p.xchg_us, xchg_calls=p.xchg_calls)
+                    xchg_us=p.xchg_us, xchg_calls=p.xchg_calls, walk_cycles=p.walk_cycles,
+                    drain_cycles=p.drain_cycles)

@@ -64,11 +64,19 @@ class PinnedPool:
             if ptr is not None:
                 self._idle -= size
         if ptr is None:
+            # an empty size class: pin two blocks, one now and one spare -- a caller
+            # that keeps the previous call's results alive (comparing or storing
+            # them) needs two sets in turn, and pinning on the next call would cost
+            # it milliseconds
             L = _lib.load()
-            p = ctypes.c_void_p()
-            _lib.check(L.lpc_host_alloc(size, ctypes.byref(p)), None)
-            ptr = p.value
-            self.allocated += 1
+            got = []
+            for _ in range(2):
+                p = ctypes.c_void_p()
+                _lib.check(L.lpc_host_alloc(size, ctypes.byref(p)), None)
+                got.append(p.value)
+                self.allocated += 1
+            ptr = got[0]
+            self._put(got[1], size)
         arr = (ctypes.c_char * size).from_address(ptr)
         arr._owner = _Owner(self, ptr, size)
         return arr

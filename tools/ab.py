@@ -24,7 +24,7 @@ for r in range(reps):
         e = dict(os.environ, **{k: v for k, v in env.items() if k != "ARGS"})
         extra = env.get("ARGS", "").split()
         steps = os.environ.get("AB_STEPS", "300")
-        out = subprocess.run([sys.executable, "bench.py", "--no-cpu", "--no-configs", "--steps", steps, "--warmup", "5"]
+        out = subprocess.run([sys.executable, "bench.py", "--no-cpu", "--no-configs", "--no-strong", "--steps", steps, "--warmup", "5"]
                              + extra, cwd=root, env=e, capture_output=True, text=True, timeout=300)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if out.returncode != 0 or not line:
