@@ -356,8 +356,7 @@ def timed_block(eng, runner, comm, o, d, p, sc, steps, warmup, sync, dist, dev):
     in_all = float(comm.allreduce_sum([in_pow])[0]) if comm else in_pow
 
     def step():
-        eng.reset()
-        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_all)
+        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_all, reset=True)
     for _ in range(warmup):
         step()
     sync()
@@ -548,8 +547,7 @@ def main():
     def step():
         # the trace returns once its outputs are final, so the next step's launches
         # queue behind its last row moves (sync() waits for all)
-        eng.reset()
-        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_pow_all)
+        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_pow_all, reset=True)
 
     def sync():
         eng.sync()

@@ -187,6 +187,11 @@ int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_i
  * to the host waits for them first; lpc_sync waits explicitly. */
 int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                         int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+/* lpc_trace_reset + lpc_trace_run_async in one call: the next batch of a caller
+ * that re-traces the rays set with lpc_trace_set_rays (one host round trip less
+ * between batches). */
+int lpc_trace_rerun_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                          int32_t *n_iter, int64_t *measured_count, double *mesh_power);
 /* ---- ray-sharded trace: one process per GPU ---------- */
 /* All-reduce (sum, in place) of n doubles over the ranks of a sharded trace;
  * every rank must receive the identical bits.  Returns 0 on success. */

@@ -67,6 +67,7 @@ _PROTOS = {
     "lpc_trace_iterate": [_P, _P, _P, _P, _P, _P, _P],
     "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P],
     "lpc_trace_run_async": [_P, _I32, _F64, _P, _P, _P, _P],
+    "lpc_trace_rerun_async": [_P, _I32, _F64, _P, _P, _P, _P],
     "lpc_sync": [_P],
     "lpc_trace_iterate_export": [_P, _P, _I32, _P],
     "lpc_trace_population_power": [_P, _P],

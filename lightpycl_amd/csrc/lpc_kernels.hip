@@ -40,9 +40,11 @@ namespace lpck {
 
 // Drain entries whose ray mask has at least this many rays are tested
 // triangle-uniform (the record by scalar loads, each lane its own ray, results
-// in registers); sparser ones are expanded into packed (triangle, ray) pairs
-// (round 3 A/B: 8 and 16 cost the synthetic scene 2-15 %).
-#define LPC_DRAIN_U 24
+// in registers); sparser ones are queued as (triangle, ray) pairs at the leaf
+// (round 5 A/B with the pair list: 32 and 40 beat 24 by 1.5 %, 16 lost 4 %).
+#ifndef LPC_DRAIN_U
+#define LPC_DRAIN_U 32
+#endif
 // The hierarchy kernels' launch bounds in waves per SIMD (compile-time A/B
 // builds, tools/build_variant.py; 5 and 7 measured equal or slower).
 #ifndef LPC_WALK_MINB
@@ -200,120 +202,86 @@ static __device__ __forceinline__ void unit_dir(const f3 &D, float &nx, float &n
 // (W - 1) per level + 1.
 #define LPC_STACK 64
 
-// k-th set bit (0-based) of m.
-static __device__ __forceinline__ int select_bit(uint64_t m, int k)
-{
-    int pos = 0;
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const int c = __builtin_popcountll((m >> pos) & ((1ull << w) - 1ull));
-        if (k >= c) { k -= c; pos += w; }
-    }
-    return pos;
-}
-
-// LDS of one wave's traversal.
+// LDS of one wave's traversal: the node stack, the deferred exact tests -- dense
+// entries (a triangle and the mask of its >= LPC_DRAIN_U rays) and sparse pairs
+// (triangle << 6 | ray lane, appended at the leaf) -- and the per-ray state.
+// LPC_PAIRS keeps the wave at 6656 bytes: 24 waves (6 per SIMD) in 160 KB of LDS.
+#ifndef LPC_PAIRS
+#define LPC_PAIRS 512
+#endif
 struct WaveLds {
     int32_t stack[LPC_STACK];
-    int32_t qidx[64], qscan[64];
+    int32_t qidx[64];
     uint64_t qmask[64];
-    float ray[6][64];                  // the packet's rays (O, D) for the drain
+    uint32_t pairs[LPC_PAIRS];
+    float ray[6][64];                  // the packet's rays (O, D) for the pairs
     unsigned long long lkey[64];       // per-ray nearest hit (slot_key)
     int32_t lcnt[64];                  // per-ray hit count
 };
 
-// Drain a wave's queue of deferred exact tests: entries (triangle ~idx, mask of
-// the wave's rays) in L.qidx / L.qmask [0, nq), results folded into the per-ray
+// Drain a wave's deferred exact tests, folding the results into the per-ray
 // accumulators L.lkey / L.lcnt (minimal slot_key(t, idx) for t < max_ray_len, a
 // count for every accepted t > eps: mt_accumulate's rule).  Dense entries
-// (>= lpc_drain_u rays) are tested triangle-uniform, the rest as packed
-// (triangle, ray) pairs, 64 per step (ray r = lane r's ray: O, D in that lane,
-// L.ray for the packed pairs).
+// (L.qidx / L.qmask [0, nq)) are tested triangle-uniform (the record by scalar
+// loads, each lane its own ray in registers), the sparse pairs (L.pairs [0, np))
+// 64 per step, one per lane (record gathered, ray read from L.ray).
 template <bool PROF>
-static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, const int lane,
+static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int32_t &np, const int lane,
                                                    const ExactRec *__restrict__ xrec, const float eps,
                                                    const float max_ray_len, const unsigned long long key0,
                                                    const f3 &O, const f3 &D, uint32_t &n_pairs, uint32_t &n_exact)
 {
-    if (nq == 0) return;
-    {   // dense entries: one triangle for all its rays at once (its record by
-        // scalar loads); the sparse entries move to the front of the queue for
-        // the packed pairs below
+    if (nq) {
         const bool ve = lane < nq;
         const int32_t my_idx = ve ? L.qidx[lane] : 0;
         const uint64_t my_mask = ve ? L.qmask[lane] : 0ull;
-        const uint64_t dense = __builtin_amdgcn_ballot_w64(ve && __builtin_popcountll(my_mask) >= LPC_DRAIN_U);
-        if (dense) {
-            const bool keep = ve && !((dense >> lane) & 1ull);
-            const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
-            if (keep) {
-                const int pos = __builtin_popcountll(km & ((1ull << lane) - 1ull));
-                L.qidx[pos] = my_idx;
-                L.qmask[pos] = my_mask;
-            }
-            auto rl64 = [](uint64_t v, int l) -> uint64_t {
-                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-            };
-            // this lane's own ray against each dense triangle, accumulated in
-            // registers with the same rule, then into its LDS accumulators
-            // (only this lane writes them here; the packed pairs' LDS atomics
-            // come later in this wave's program order)
-            unsigned long long ukey = key0;
-            int32_t ucnt = 0;
-            uint64_t dm = dense;
-            int32_t idx = __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dm));
-            ExactRec x = xrec[idx];
-            for (; dm; dm &= dm - 1) {
-                const uint64_t m = rl64(my_mask, __builtin_ctzll(dm));
-                // the next dense entry's record, loaded while this one is tested
-                const uint64_t dn = dm & (dm - 1);
-                const int32_t nidx = dn ? __builtin_amdgcn_readlane(my_idx, __builtin_ctzll(dn)) : idx;
-                const ExactRec nx = xrec[nidx];
-                if ((m >> lane) & 1ull) {
-                    float t;
-                    if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
-                                 mk3(x.e2x, x.e2y, x.e2z), &t) && t > eps) {
-                        ++ucnt;
-                        if (t < max_ray_len) {
-                            const unsigned long long k = slot_key(t, idx);
-                            ukey = k < ukey ? k : ukey;
-                        }
+        auto rl64 = [](uint64_t v, int l) -> uint64_t {
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+        };
+        // this lane's own ray against each dense triangle, accumulated in
+        // registers with the same rule, then into its LDS accumulators (only this
+        // lane writes them here; the pairs' LDS atomics come later in this wave's
+        // program order)
+        unsigned long long ukey = key0;
+        int32_t ucnt = 0;
+        int32_t idx = __builtin_amdgcn_readfirstlane(my_idx);
+        ExactRec x = xrec[idx];
+        for (int e = 0; e < nq; ++e) {
+            const uint64_t m = rl64(my_mask, e);
+            // the next dense entry's record, loaded while this one is tested
+            const int32_t nidx = e + 1 < nq ? __builtin_amdgcn_readlane(my_idx, e + 1) : idx;
+            const ExactRec nx = xrec[nidx];
+            if ((m >> lane) & 1ull) {
+                float t;
+                if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z),
+                             &t) && t > eps) {
+                    ++ucnt;
+                    if (t < max_ray_len) {
+                        const unsigned long long k = slot_key(t, idx);
+                        ukey = k < ukey ? k : ukey;
                     }
-                    if (PROF) ++n_exact;
                 }
-                n_pairs += (uint32_t)__builtin_popcountll(m);
-                idx = nidx;
-                x = nx;
+                if (PROF) ++n_exact;
             }
-            if (ucnt) {
-                L.lcnt[lane] += ucnt;
-                const unsigned long long kl = L.lkey[lane];
-                L.lkey[lane] = ukey < kl ? ukey : kl;
-            }
-            nq = __builtin_popcountll(km);
-            if (nq == 0) return;
+            n_pairs += (uint32_t)__builtin_popcountll(m);
+            idx = nidx;
+            x = nx;
         }
+        if (ucnt) {
+            L.lcnt[lane] += ucnt;
+            const unsigned long long kl = L.lkey[lane];
+            L.lkey[lane] = ukey < kl ? ukey : kl;
+        }
+        nq = 0;
     }
-    const int pc = lane < nq ? __builtin_popcountll(L.qmask[lane]) : 0;
-    int incl = pc;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
-    }
-    L.qscan[lane] = incl;
-    const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
-    n_pairs += (uint32_t)total;
-    for (int base = 0; base < total; base += 64) {
+    n_pairs += (uint32_t)np;
+    for (int base = 0; base < np; base += 64) {
         const int q = base + lane;
-        if (q < total) {
-            int e = 0;                         // first entry with qscan[e] > q
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (e + step <= 63 && L.qscan[e + step - 1] <= q) e += step;
-            const int k = q - (e > 0 ? L.qscan[e - 1] : 0);
-            const int r = select_bit(L.qmask[e], k);
-            const int32_t idx = L.qidx[e];
+        if (q < np) {
+            const uint32_t pr = L.pairs[q];
+            const int32_t idx = (int32_t)(pr >> 6);
+            const int r = (int)(pr & 63u);
             const ExactRec x = xrec[idx];
             const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
             const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
@@ -326,7 +294,7 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, cons
             if (PROF) ++n_exact;
         }
     }
-    nq = 0;
+    np = 0;
 }
 
 // One packet (64 rays of the coherence order from w*64, one per lane) against
@@ -363,7 +331,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     L.lcnt[lane] = 0;
 
     const uint64_t clk0 = (PROF && stats) ? wall_clock64() : 0;
-    int32_t top = 0, nq = 0;
+    int32_t top = 0, nq = 0, np = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
     uint32_t n_pairs = 0;                           // exact pairs drained (wave-uniform; hand-over cost)
     // Exact tests are deferred: candidate (triangle, ray lanes) entries queue up
@@ -376,7 +344,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     const uint64_t cyc0 = (PROF && stats) ? clock64() : 0;
     auto drain = [&]() {
         const uint64_t c0 = (PROF && stats) ? clock64() : 0;
-        drain_queue<PROF>(L, nq, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact);
+        drain_queue<PROF>(L, nq, np, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact);
         if (PROF && stats) cyc_drain += clock64() - c0;
     };
     int budget = SP.budget;
@@ -385,7 +353,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
         // work hand-over: after `budget` nodes the subtrees left on the stack go
         // to k_spill, one wave each (a wave stuck in a dense region would
         // otherwise be the launch's critical path)
-        // cost so far in node-visit units: one visit ~ 32 exact pairs (tools/wave_probe.py fit)
+        // cost so far in node-visit units: one visit ~ 32 exact pairs
         if (budget > 0 && (int)(n_nodes + (n_pairs >> SP.pair_shift)) >= budget && top >= 2) {
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(SP.ctr, (uint32_t)top);
@@ -421,14 +389,25 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
 #pragma unroll
             for (int k = 0; k < W; ++k)
                 if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
-        } else {                                   // leaf: triangles ~ref -> exact-test queue
-            if (nq > 64 - W) drain();              // room for the leaf's W entries (one drain site per node)
+        } else {                                   // leaf: triangles ~ref -> deferred exact tests
+            // room for the leaf's W entries / pairs (one drain site per node)
+            if (nq > 64 - W || np > LPC_PAIRS - W * (LPC_DRAIN_U - 1)) drain();
 #pragma unroll
             for (int k = 0; k < W; ++k) {
-                const uint64_t m = __builtin_amdgcn_ballot_w64(d[k] <= 0.0f);
+                const bool pass = d[k] <= 0.0f;
+                const uint64_t m = __builtin_amdgcn_ballot_w64(pass);
                 if (!m) continue;
-                if (lane == 0) { L.qidx[nq] = ~N.ref[k]; L.qmask[nq] = m; }
-                ++nq;
+                const int c = __builtin_popcountll(m);
+                if (c >= LPC_DRAIN_U) {            // dense: one entry, tested triangle-uniform
+                    if (lane == 0) { L.qidx[nq] = ~N.ref[k]; L.qmask[nq] = m; }
+                    ++nq;
+                } else {                           // sparse: one pair per passing ray
+                    if (pass)
+                        L.pairs[np + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                            ((uint32_t)(~N.ref[k]) << 6) | (uint32_t)lane;
+                    np += c;
+                }
             }
         }
     }

@@ -155,6 +155,10 @@ struct lpc_handle {
     // queue-overflow and budget paths at small sizes)
     int spill_budget = 20;                          // node visits before a wave hands over (0 off)
     int64_t spill_large_per_tri = 16;
+    // hand-over budgets of the k_spill levels (level l queues for level l + 1 with
+    // budget lv_budget[l]; the last level none) and level counts, large / small
+    int lv_budget[2][8] = {{20, 20, 20, 20, 20, 20, 20, 20}, {20, 20, 20, 20, 20, 20, 20, 20}};
+    int lv_count[2] = {kSpillLevels, kSpillLevelsSmall};
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     DBuf w_spill;                                   // k_spill queue
     bool pop_traced = false;                        // the population is in its parents' traced order
@@ -177,7 +181,8 @@ struct lpc_handle {
     int32_t hist_iter = -1;                         //   speculation's prediction) and its iteration limit
     bool dcap_rebuilt = false;                      // check_dcap rebuilt the records (a speculative iteration is void)
     unsigned int acc_seq = 0;
-    bool host_prof = false;                         // LPC_HOSTPROF: host-side timing of each iteration (stderr)
+    int host_prof = 0;                              // LPC_HOSTPROF: host-side timing of each iteration (stderr);
+                                                    //   2: also each launch's hand-over queue lengths (synchronising)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
     // results export (lpc_trace_iterate_export): k_export packs a chunk's part of
     // the results tuple into xst[par] on the main stream, the export stream copies
@@ -803,12 +808,13 @@ static int ray_base(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n,
 // hand-over levels of a launch of n rays (0: none)
 static int spill_level_count(const lpc_handle *h, int64_t n, const SpillArgs &SP)
 {
-    const int lv = n >= kSpillSmallN ? kSpillLevels : kSpillLevelsSmall;
+    const int lv = h->lv_count[n >= kSpillSmallN ? 0 : 1];
     return SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
 }
 
 // level l's input (queue l % 2, length misc[6 + l]) and output (level l + 1)
-static void spill_level_args(lpc_handle *h, const SpillArgs &SP, int l, int levels, SpillArgs *I, SpillArgs *O)
+static void spill_level_args(lpc_handle *h, int64_t n, const SpillArgs &SP, int l, int levels, SpillArgs *I,
+                             SpillArgs *O)
 {
     uint32_t *misc = (uint32_t *)h->d_misc.p;
     *I = SP; *O = SP;
@@ -816,7 +822,7 @@ static void spill_level_args(lpc_handle *h, const SpillArgs &SP, int l, int leve
     I->ctr = misc + LPC_MISC_SPILL + l;
     O->items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
     O->ctr = misc + LPC_MISC_SPILL + l + 1;
-    O->budget = l + 1 < levels ? SP.budget : 0;
+    O->budget = l + 1 < levels ? h->lv_budget[n >= kSpillSmallN ? 0 : 1][l] : 0;
 }
 
 // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
@@ -831,7 +837,7 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
     const int levels = spill_level_count(h, n, SP);
     for (int l = 0; l < levels; ++l) {
         SpillArgs I, O;
-        spill_level_args(h, SP, l, levels, &I, &O);
+        spill_level_args(h, n, SP, l, levels, &I, &O);
         // later levels hold fewer items (and often none): smaller grids, in
         // 4-wave units, launched as single-wave blocks
         const unsigned g = (unsigned)std::max<int64_t>(kSpillMinBlocks, kSpillBlocks >> l) * 4u;
@@ -978,7 +984,15 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     }
 #undef LPC_LAUNCH_WALK
     if (h->prof) h->ev_kern.push_back({k0, k1});
-    return run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP, ds ? ds->nd : nullptr);
+    RETIF(run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP, ds ? ds->nd : nullptr));
+    if (h->host_prof >= 2) {                          // diagnostic: this launch's hand-over queue lengths
+        uint32_t q[8] = {0};
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, hipMemcpy(q, (uint32_t *)h->d_misc.p + LPC_MISC_SPILL, sizeof(q), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[lpc host] hand-over: n %lld items per level %u %u %u %u\n", (long long)n, q[0], q[1], q[2],
+                q[3]);
+    }
+    return 0;
 }
 
 // intersect for n rays of `in` into the slot arrays, and optionally into a
@@ -1337,8 +1351,15 @@ int lpc_open(int device, lpc_handle **out)
     h->dcap_init = (double)env_int("LPC_DCAP_MILLI", 16000) / 1000.0;
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
+    for (int z = 0; z < 2; ++z) {                   // A/B: "levels/b0/b1/..." (level budgets)
+        const char *e = getenv(z ? "LPC_SPILL_SCHED_SMALL" : "LPC_SPILL_SCHED");
+        if (!e || !*e) continue;
+        char *q = nullptr;
+        h->lv_count[z] = (int)strtol(e, &q, 10);
+        for (int l = 0; l < 8 && q && (*q == ',' || *q == '/'); ++l) h->lv_budget[z][l] = (int)strtol(q + 1, &q, 10);
+    }
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
-    h->host_prof = env_int("LPC_HOSTPROF", 0) != 0;
+    h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
     {   // the side stream of the sliver kernels and its fork / join events
         const unsigned evf = hipEventDisableTiming;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
@@ -1417,8 +1438,10 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     if (tri_count <= 0 || mesh_count <= 0 || !v0 || !v1 || !v2 || !mesh_id || !mat_type || !ior ||
         !refl || !diss)
         return set_err(h, LPC_E_ARG, "scene needs >= 1 triangle, >= 1 mesh and all tables");
-    if (tri_count >= (1 << 28) - 1)   // root items encode node ids in 28 bits (LPC_Q_MAX_NODES)
-        return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^28 - 2)");
+    // the walk's sparse exact-test pairs hold a triangle index in 26 bits (and root
+    // items node ids in 28, LPC_Q_MAX_NODES)
+    if (tri_count >= (1 << 26))
+        return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^26 - 1)");
     if (mesh_count > 64 * LPC_ROOTS_TASKS)   // k_roots_s holds at most 1024 run roots
         return set_err(h, LPC_E_ARG, "scene has too many meshes (limit 1024)");
     HIPCHK(h, hipSetDevice(h->device));
@@ -1897,6 +1920,13 @@ int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_i
 int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                         int32_t *n_iter, int64_t *measured_count, double *mesh_power)
 {
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, false);
+}
+
+int lpc_trace_rerun_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                          int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+{
+    RETIF(lpc_trace_reset(h));
     return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, false);
 }
 

@@ -185,13 +185,15 @@ class ShardedTrace:
             return np.asarray(vals, dtype=np.float64)
         return self.comm.allreduce_sum(vals)
 
-    def run(self, iterations, tau, input_power_local, hist=None, wait=True, input_power_global=None):
+    def run(self, iterations, tau, input_power_local, hist=None, wait=True, input_power_global=None, reset=False):
         """Trace to the reference's termination.  hist=(limits, points): also bin
         the measured rays (get_binned_data_angular) on every rank and all-reduce
         the histogram (float64, bin counts are additive).  wait=False: return once
         the outputs are final, without waiting for the last rows to move on the
         device (engine.sync() waits).  input_power_global: the all-ranks input power
-        if already known (no all-reduce for it)."""
+        if already known (no all-reduce for it).  reset=True: trace the engine's
+        emitted rays again from the start (engine.reset() first; one library call
+        with the trace for a liblpc engine)."""
         in_pow = (float(input_power_global) if input_power_global is not None
                   else float(self._sum([input_power_local])[0]))
         thr = (1.0 - tau) * in_pow
@@ -202,13 +204,16 @@ class ShardedTrace:
             if self.iter_comm is not None and self._installed is not self.iter_comm:
                 self.engine.set_allreduce(self.iter_comm)
                 self._installed = self.iter_comm
-            stats, (_, mesh_pow) = self.engine.run_local(int(iterations), thr, wait=wait or hist is not None)
+            stats, (_, mesh_pow) = self.engine.run_local(int(iterations), thr, wait=wait or hist is not None,
+                                                         reset=reset)
             glob = self.engine.global_stats() if self.iter_comm is not None else stats
             bounces = sum(int(st.n_in) for st in stats)
             iters = len(stats)
             counts = [int(st.n_in) for st in glob]
             mesh_pow = np.asarray(mesh_pow, dtype=np.float64)
         else:
+            if reset:
+                self.engine.reset()
             for _ in range(int(iterations)):
                 st, _ = self.engine.iterate()
                 bounces += int(st.n_in)

@@ -286,25 +286,34 @@ class Engine:
         """lpc_sync: wait for every kernel queued on the engine's stream."""
         self._c(self.L.lpc_sync(self.h))
 
-    def run_local(self, iterations, power_threshold, wait=True):
+    def run_local(self, iterations, power_threshold, wait=True, reset=False):
         """lpc_trace_run: iterate until the next population's power is below
         power_threshold or no ray is kept (at most `iterations`).  Returns the
-        per-iteration stats and the measured (count, per-mesh power)."""
+        per-iteration stats and the measured (count, per-mesh power).
+        reset=True (with wait=False): lpc_trace_rerun_async, the reset and the
+        trace in one call (the bench's back-to-back batches)."""
         cap = max(int(iterations), 0)
-        key = (cap, self.mesh_count)
+        # output buffers and argument objects kept per (cap, mesh count): the library
+        # writes one power per mesh of the CURRENT scene into mp
+        key = (cap, int(self.mesh_count))
         bufs = self._run_bufs.get(key) if hasattr(self, "_run_bufs") else None
-        if bufs is None:            # output buffers kept per cap (one ctypes call per trace)
-            bufs = ((_lib.IterStats * max(cap, 1))(), ctypes.c_int32(0), ctypes.c_int64(0),
-                    np.zeros(max(self.mesh_count, 1), np.float64))
+        if bufs is None:
+            arr, k, c = (_lib.IterStats * max(cap, 1))(), ctypes.c_int32(0), ctypes.c_int64(0)
+            mp = np.zeros(max(key[1], 1), np.float64)
+            bufs = (arr, k, c, mp, ctypes.byref(k), ctypes.byref(c), mp.ctypes.data_as(ctypes.c_void_p))
             self.__dict__.setdefault("_run_bufs", {})[key] = bufs
-        arr, k, c, mp = bufs
+        arr, k, c, mp, pk, pc, pmp = bufs
         # wait=False: lpc_trace_run_async (the outputs are final; the last rows may
         # still move on the device and the next batch's launches queue behind them)
-        fn = self.L.lpc_trace_run if wait else self.L.lpc_trace_run_async
-        self._c(fn(self.h, cap, float(power_threshold), arr, ctypes.byref(k), ctypes.byref(c),
-                   mp.ctypes.data_as(ctypes.c_void_p)))
-        return [_lib.IterStats.from_buffer_copy(arr[i]) for i in range(k.value)], (c.value,
-                                                                                   mp[: self.mesh_count].copy())
+        if reset and not wait:
+            fn = self.L.lpc_trace_rerun_async
+        else:
+            if reset:
+                self.reset()
+            fn = self.L.lpc_trace_run if wait else self.L.lpc_trace_run_async
+        self._c(fn(self.h, cap, float(power_threshold), arr, pk, pc, pmp))
+        # one copy of the stats block (the buffers are reused by the next call)
+        return type(arr).from_buffer_copy(arr)[:k.value], (c.value, mp[: self.mesh_count].copy())
 
     # -- ray-sharded trace --------------------------------------------------------
     def set_allreduce(self, comm):
