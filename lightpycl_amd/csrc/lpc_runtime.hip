@@ -85,7 +85,8 @@ const int64_t kWalkWaves = LPC_WALK_GRID;   // k_rootwalk grid (single-wave bloc
 const int64_t kSliverMergePpw = 4;      // packets per merged sliver unit (k_rootwalk's tail)
 const int64_t kSliverWaves = 16384;     // k_slivers: (packet, piece) waves to aim for
 const int kSpillLevels = 3;             // k_spill levels (hand-over depth) for populations >= kSpillSmallN
-const int kSpillLevelsSmall = 1;        // ... below
+const int kSpillLevelsSmall = 1;        // ... below (round 5 A/B: 4 levels, level budgets 10 or 14 / 8, two
+                                        //   levels below: neutral or slower)
 const int64_t kSpillSmallN = 262144;
 const int64_t kSpillBlocks = 4096;      // k_spill level l grid: max(kSpillMinBlocks, kSpillBlocks >> l) x 4 waves
 const int64_t kSpillMinBlocks = 256;
@@ -155,10 +156,6 @@ struct lpc_handle {
     // queue-overflow and budget paths at small sizes)
     int spill_budget = 20;                          // node visits before a wave hands over (0 off)
     int64_t spill_large_per_tri = 16;
-    // hand-over budgets of the k_spill levels (level l queues for level l + 1 with
-    // budget lv_budget[l]; the last level none) and level counts, large / small
-    int lv_budget[2][8] = {{20, 20, 20, 20, 20, 20, 20, 20}, {20, 20, 20, 20, 20, 20, 20, 20}};
-    int lv_count[2] = {kSpillLevels, kSpillLevelsSmall};
     int64_t spill_cap = (int64_t)1 << 22;           // k_spill queue capacity (items)
     DBuf w_spill;                                   // k_spill queue
     bool pop_traced = false;                        // the population is in its parents' traced order
@@ -808,13 +805,12 @@ static int ray_base(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n,
 // hand-over levels of a launch of n rays (0: none)
 static int spill_level_count(const lpc_handle *h, int64_t n, const SpillArgs &SP)
 {
-    const int lv = h->lv_count[n >= kSpillSmallN ? 0 : 1];
+    const int lv = n >= kSpillSmallN ? kSpillLevels : kSpillLevelsSmall;
     return SP.budget > 0 ? std::max(1, std::min(lv, 7)) : 0;
 }
 
 // level l's input (queue l % 2, length misc[6 + l]) and output (level l + 1)
-static void spill_level_args(lpc_handle *h, int64_t n, const SpillArgs &SP, int l, int levels, SpillArgs *I,
-                             SpillArgs *O)
+static void spill_level_args(lpc_handle *h, const SpillArgs &SP, int l, int levels, SpillArgs *I, SpillArgs *O)
 {
     uint32_t *misc = (uint32_t *)h->d_misc.p;
     *I = SP; *O = SP;
@@ -822,7 +818,7 @@ static void spill_level_args(lpc_handle *h, int64_t n, const SpillArgs &SP, int 
     I->ctr = misc + LPC_MISC_SPILL + l;
     O->items = (SpillItem *)h->w_spill.p + (size_t)((l + 1) % 2) * (size_t)h->spill_cap;
     O->ctr = misc + LPC_MISC_SPILL + l + 1;
-    O->budget = l + 1 < levels ? h->lv_budget[n >= kSpillSmallN ? 0 : 1][l] : 0;
+    O->budget = l + 1 < levels ? SP.budget : 0;
 }
 
 // hand-over levels: level l reads queue l % 2 (length misc[6 + l]) and queues
@@ -837,7 +833,7 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
     const int levels = spill_level_count(h, n, SP);
     for (int l = 0; l < levels; ++l) {
         SpillArgs I, O;
-        spill_level_args(h, n, SP, l, levels, &I, &O);
+        spill_level_args(h, SP, l, levels, &I, &O);
         // later levels hold fewer items (and often none): smaller grids, in
         // 4-wave units, launched as single-wave blocks
         const unsigned g = (unsigned)std::max<int64_t>(kSpillMinBlocks, kSpillBlocks >> l) * 4u;
@@ -1351,13 +1347,6 @@ int lpc_open(int device, lpc_handle **out)
     h->dcap_init = (double)env_int("LPC_DCAP_MILLI", 16000) / 1000.0;
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
     h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
-    for (int z = 0; z < 2; ++z) {                   // A/B: "levels/b0/b1/..." (level budgets)
-        const char *e = getenv(z ? "LPC_SPILL_SCHED_SMALL" : "LPC_SPILL_SCHED");
-        if (!e || !*e) continue;
-        char *q = nullptr;
-        h->lv_count[z] = (int)strtol(e, &q, 10);
-        for (int l = 0; l < 8 && q && (*q == ',' || *q == '/'); ++l) h->lv_budget[z][l] = (int)strtol(q + 1, &q, 10);
-    }
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
     {   // the side stream of the sliver kernels and its fork / join events
