@@ -78,6 +78,7 @@ def valu_issue_peak():
                           "waves/SIMD; v_pk_fma_f32 issues at half that rate)")
     except (OSError, KeyError, ValueError):
         return VALU_ISSUE_PEAK_GUIDE, None, "MI355X_MICROARCH.md:54,473 (2 cycles per wave64 VALU instruction per SIMD)"
+PROF_EVERY = 7                 # the timed region's walk launches carrying HIP events (1 in 7)
 RAY_BYTES = 156                # algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # per triangle per bounce-iteration
 MT_FLOPS = 46                  # Moller-Trumbore flops per ray-triangle test
@@ -272,8 +273,6 @@ def run_configs(Engine, ShardedTrace, scenes):
             e.reset()                                            # the first's prediction (speculation)
             run.run(depth, sc.tau, in_pow, wait=False)
         e.sync()
-        e.prof_enable(True, light=True)
-        e.prof_read(reset=True)
         t = time.perf_counter()
         res = []
         for _ in range(steps):
@@ -281,13 +280,22 @@ def run_configs(Engine, ShardedTrace, scenes):
             res.append(run.run(depth, sc.tau, in_pow, wait=False))
         e.sync()
         dt = (time.perf_counter() - t) / steps
+        # the walk kernel's share: one more trace with HIP events on its launches
+        # (outside the timed traces: the events cost ~7 us per launch)
+        e.prof_enable(True, light=True)
+        e.prof_read(reset=True)
+        t1 = time.perf_counter()
+        e.reset()
+        run.run(depth, sc.tau, in_pow, wait=False)
+        e.sync()
+        dt1 = time.perf_counter() - t1
         pr = e.prof_read(reset=True)
         e.prof_enable(False)
         r = res[-1]
         b = int(r["bounces"])
         out[name] = {"rays": n, "depth": depth, "triangles": int(e.tri_count), "iterations": int(r["iterations"]),
                      "ray_bounces": b, "ms_per_trace": dt * 1e3, "ray_bounces_per_s": b / dt,
-                     "walk_kernel_share": pr["kernel_ms"] / steps / (dt * 1e3) if dt > 0 else None,
+                     "walk_kernel_share": pr["kernel_ms"] / (dt1 * 1e3) if dt1 > 0 else None,
                      "steps_identical": all(x["global_counts"] == r["global_counts"] for x in res),
                      "measured_power": float(np.sum(r["mesh_power"])), "input_power": in_pow}
         e.close()
@@ -564,7 +572,10 @@ def main():
     for _ in range(a.warmup):
         step()
     if not a.no_prof:
-        eng.prof_enable(True, light=True)    # HIP events around the walk kernel's launches only
+        # HIP events around the walk kernel's launches only, on every PROF_EVERY-th
+        # one (a launch with events costs ~7 us more; 7 is prime to the 3 launches
+        # of a step, so the sample cycles through the iterations)
+        eng.prof_enable(True, light=True, every=PROF_EVERY)
         # untimed: the same number of steps once with events, so the timed region
         # takes its events from the pool instead of creating them
         for _ in range(a.steps):
@@ -639,9 +650,9 @@ def main():
         return
 
     M = eng.tri_count
-    launches = max(prof["intersect_launches"], 1)
+    launches = max(prof["intersect_launches"], 1)       # the sampled walk launches
     avg_ms = prof["kernel_ms"] / launches               # the walk kernel's launches alone
-    rays_per_launch = bounces / launches                 # rank-0 launches
+    rays_per_launch = bounces / max(iters, 1)            # rank-0 launches: one walk per iteration
     alg_bytes = rays_per_launch * RAY_BYTES + M * TRI_BYTES
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     pairs_per_s = bounces_all * M / dt                   # reference-equivalent RI/s (sum N_iter * M / T)
@@ -674,8 +685,10 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": WALK_KERNEL, "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": alg_bytes,
+                     "launches_timed": int(prof["intersect_launches"]), "launches_all": int(iters),
                      "note": f"achieved = algorithmic bytes per launch (156 B x rays + 40 B x triangles) / "
-                             f"{WALK_KERNEL}'s own average launch time (HIP events on its stream); traffic = "
+                             f"{WALK_KERNEL}'s own average launch time (HIP events on its stream, every "
+                             f"{PROF_EVERY}th launch of the timed region); traffic = "
                              f"2*FETCH_SIZE+WRITE_SIZE per {WALK_KERNEL} launch from profiles/pmc_intersect.json "
                              f"(null when that summary was collected on other kernel sources)"},
         # the bound that actually limits the walk kernel: executed VALU issue

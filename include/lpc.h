@@ -291,8 +291,9 @@ typedef struct {
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * traversal counters (2, diagnostic: adds atomics), only the walk kernel's
- * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs), or
- * disable (0). */
+ * launches (4: kernel_ms, launches and pairs; the lightest, for timed runs;
+ * 4 + 256 k: only every k-th walk launch, intersect_launches and pairs counting
+ * those), or disable (0). */
 int lpc_prof_enable(lpc_handle *h, int on);
 int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset);
 

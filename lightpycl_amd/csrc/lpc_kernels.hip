@@ -226,7 +226,8 @@ struct WaveLds {
 // loads, each lane its own ray in registers), the sparse pairs (L.pairs [0, np))
 // 64 per step, one per lane (record gathered, ray read from L.ray).
 template <bool PROF>
-static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int32_t &np, const int lane,
+static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int32_t &np, const bool final,
+                                                   const int lane,
                                                    const ExactRec *__restrict__ xrec, const float eps,
                                                    const float max_ray_len, const unsigned long long key0,
                                                    const f3 &O, const f3 &D, uint32_t &n_pairs, uint32_t &n_exact)
@@ -275,10 +276,13 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
         }
         nq = 0;
     }
-    n_pairs += (uint32_t)np;
-    for (int base = 0; base < np; base += 64) {
+    // a drain inside the walk tests whole steps of 64 pairs and keeps the rest
+    // (< 64) for the next one; the final drain tests them all
+    const int todo = final ? np : (np & ~63);
+    n_pairs += (uint32_t)todo;
+    for (int base = 0; base < todo; base += 64) {
         const int q = base + lane;
-        if (q < np) {
+        if (q < todo) {
             const uint32_t pr = L.pairs[q];
             const int32_t idx = (int32_t)(pr >> 6);
             const int r = (int)(pr & 63u);
@@ -294,7 +298,12 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
             if (PROF) ++n_exact;
         }
     }
-    np = 0;
+    const int rest = np - todo;
+    if (rest > 0 && todo > 0) {
+        const uint32_t v = lane < rest ? L.pairs[todo + lane] : 0u;
+        if (lane < rest) L.pairs[lane] = v;
+    }
+    np = rest;
 }
 
 // One packet (64 rays of the coherence order from w*64, one per lane) against
@@ -342,9 +351,9 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     // which is mt_accumulate's rule (minimal t, lowest index among equal t).
     uint64_t cyc_drain = 0;                         // PROF: shader-clock cycles in the drains
     const uint64_t cyc0 = (PROF && stats) ? clock64() : 0;
-    auto drain = [&]() {
+    auto drain = [&](bool final) {
         const uint64_t c0 = (PROF && stats) ? clock64() : 0;
-        drain_queue<PROF>(L, nq, np, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact);
+        drain_queue<PROF>(L, nq, np, final, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact);
         if (PROF && stats) cyc_drain += clock64() - c0;
     };
     int budget = SP.budget;
@@ -391,7 +400,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
                 if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
         } else {                                   // leaf: triangles ~ref -> deferred exact tests
             // room for the leaf's W entries / pairs (one drain site per node)
-            if (nq > 64 - W || np > LPC_PAIRS - W * (LPC_DRAIN_U - 1)) drain();
+            if (nq > 64 - W || np > LPC_PAIRS - W * (LPC_DRAIN_U - 1)) drain(false);
 #pragma unroll
             for (int k = 0; k < W; ++k) {
                 const bool pass = d[k] <= 0.0f;
@@ -411,7 +420,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
             }
         }
     }
-    drain();
+    drain(true);
     if (PROF && stats) {
         for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
         // packet spread: max angle between a lane's direction and lane 0's

@@ -217,6 +217,9 @@ struct lpc_handle {
     std::vector<hipEvent_t> ev_pool;
     double prof_isect_ms = 0.0, prof_rest_ms = 0.0, prof_kern_ms = 0.0;
     int64_t prof_launches = 0, prof_pairs = 0;
+    int prof_every = 1;                              // light mode: events on every prof_every-th walk launch
+    int64_t prof_seq = 0;                            // ... walk launches seen
+    bool prof_sampled = false;                       // the last run_queue's walk launch carries events
     // ray-sharded trace (lpc_set_allreduce): the termination decisions and the
     // trace-end aggregates over all ranks
     lpc_allreduce_fn xchg = nullptr;
@@ -962,7 +965,10 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
-    if (h->prof) { k0 = ev_get(h); k1 = ev_get(h); }
+    // light mode samples every prof_every-th launch: a launch with events costs
+    // ~7 us more (bench A/B)
+    h->prof_sampled = h->prof && (!h->prof_light || h->prof_seq++ % h->prof_every == 0);
+    if (h->prof_sampled) { k0 = ev_get(h); k1 = ev_get(h); }
     // profiling counters only in the PROF instantiation, the merged sliver units
     // only in the MERGED one (fewer live registers without: the plain walk holds
     // 7 waves per SIMD, the merged one 6)
@@ -979,7 +985,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         LPC_LAUNCH_WALK(false, false);
     }
 #undef LPC_LAUNCH_WALK
-    if (h->prof) h->ev_kern.push_back({k0, k1});
+    if (h->prof_sampled) h->ev_kern.push_back({k0, k1});
     RETIF(run_spill_levels(h, in, rs, n, perm, eps, max_ray_len, skey, scnt, stats, SP, ds ? ds->nd : nullptr));
     if (h->host_prof >= 2) {                          // diagnostic: this launch's hand-over queue lengths
         uint32_t q[8] = {0};
@@ -1206,6 +1212,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     if (!side && !merge_try) RETIF(launch_slivers());       // no side stream: before the walk, this stream
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->prof && !h->prof_light) { e0 = ev_get(h); e1 = ev_get(h); (void)hipEventRecord(e0, h->stream); }
+    h->prof_sampled = false;
     if (pt->npieces > 0) {
         const SliverArgs SAm = sliver_args(kSliverMergePpw);
         RETIF(run_queue(h, in, rs, n, perm, pt, eps, max_ray_len, skey, scnt, stats, ds, merge_try ? &SAm : nullptr,
@@ -1216,8 +1223,10 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
             (void)hipEventRecord(e1, h->stream);
             h->ev_isect.push_back({e0, e1});
         }
-        h->prof_launches += 1;
-        h->prof_pairs += n * (int64_t)h->M;
+        if (!h->prof_light || h->prof_sampled) {
+            h->prof_launches += 1;
+            h->prof_pairs += n * (int64_t)h->M;
+        }
     }
     if (side) RETIF(launch_slivers());
     if (side) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side[1], 0));
@@ -2780,6 +2789,9 @@ int lpc_prof_enable(lpc_handle *h, int on)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
+    h->prof_every = std::max(1, on >> 8);           // 4 + 256 k: light, every k-th walk launch
+    on &= 0xff;
+    h->prof_seq = 0;
     h->prof = on != 0;
     h->prof_stats = on == 2;
     h->prof_light = on == 4;                        // k_rootwalk events only (bench timed region)

@@ -403,8 +403,10 @@ class Engine:
         return (H, xe, ye) if not want_xy else (H, xe, ye, x, y, pc)
 
     # -- profiling -------------------------------------------------------------
-    def prof_enable(self, on=True, counters=False, light=False):
-        level = (4 if light else 2 if counters else 1) if on else 0
+    def prof_enable(self, on=True, counters=False, light=False, every=1):
+        """light: HIP events on the walk kernel's launches only, on every
+        `every`-th one (lpc_prof_enable's 4 + 256 k)."""
+        level = ((4 + 256 * max(int(every), 1)) if light else 2 if counters else 1) if on else 0
         self._c(self.L.lpc_prof_enable(self.h, level))
 
     def prof_read(self, reset=True):
