@@ -78,7 +78,7 @@ def valu_issue_peak():
                           "waves/SIMD; v_pk_fma_f32 issues at half that rate)")
     except (OSError, KeyError, ValueError):
         return VALU_ISSUE_PEAK_GUIDE, None, "MI355X_MICROARCH.md:54,473 (2 cycles per wave64 VALU instruction per SIMD)"
-PROF_EVERY = 7                 # the timed region's walk launches carrying HIP events (1 in 7)
+PROF_EVERY = int(os.environ.get("LPC_BENCH_PROF_EVERY", 1))   # timed walk launches with HIP events (all)
 RAY_BYTES = 156                # algorithmic HBM bytes per ray-bounce
 TRI_BYTES = 40                 # per triangle per bounce-iteration
 MT_FLOPS = 46                  # Moller-Trumbore flops per ray-triangle test
@@ -572,9 +572,9 @@ def main():
     for _ in range(a.warmup):
         step()
     if not a.no_prof:
-        # HIP events around the walk kernel's launches only, on every PROF_EVERY-th
-        # one (a launch with events costs ~7 us more; 7 is prime to the 3 launches
-        # of a step, so the sample cycles through the iterations)
+        # HIP events around the walk kernel's launches only (created without the
+        # system-scope fence, which cost ~7 us per launch; PROF_EVERY > 1 samples
+        # every k-th launch)
         eng.prof_enable(True, light=True, every=PROF_EVERY)
         # untimed: the same number of steps once with events, so the timed region
         # takes its events from the pool instead of creating them
@@ -687,8 +687,8 @@ def main():
                      "alg_bytes_per_launch": alg_bytes,
                      "launches_timed": int(prof["intersect_launches"]), "launches_all": int(iters),
                      "note": f"achieved = algorithmic bytes per launch (156 B x rays + 40 B x triangles) / "
-                             f"{WALK_KERNEL}'s own average launch time (HIP events on its stream, every "
-                             f"{PROF_EVERY}th launch of the timed region); traffic = "
+                             f"{WALK_KERNEL}'s own average launch time (HIP events on its stream over the "
+                             f"timed region, launches_timed of launches_all); traffic = "
                              f"2*FETCH_SIZE+WRITE_SIZE per {WALK_KERNEL} launch from profiles/pmc_intersect.json "
                              f"(null when that summary was collected on other kernel sources)"},
         # the bound that actually limits the walk kernel: executed VALU issue

@@ -1446,6 +1446,8 @@ static __device__ __forceinline__ ShadeOut shade_eval(const ShadeArgs &A, int64_
         po = postproc<KU>(A.K, prev, A.mat_type, A.max_ray_len, slot);
     } else {
         auto slot = [&](int32_t j, float &t, int32_t &c, int32_t &i) {
+            // lmask: the slots a flush wrote (the others hold the clean state)
+            if (j < 32 && !((lmask >> j) & 1u)) { t = A.max_ray_len; i = -1; c = 0; return; }
             const int64_t a = (int64_t)j * n + r;
             const unsigned long long k = A.skey[a];
             t = slot_key_t(k); i = slot_key_idx(k); c = A.sc[a];

@@ -96,6 +96,17 @@ const double kThin = 1.0;               // thin-triangle rule factor (thin_axis;
 
 }  // namespace
 
+// Event flags.  The timing events of lpc_prof_enable skip the system-scope
+// fence of an event record (cache writeback + invalidate: ~7 us of GPU idle per
+// walk launch with it, ~0 without; round 5 A/B).  The side
+// stream's fork / join events keep it (ReleaseToDevice measured equal).
+#ifndef LPC_EVF_TIMING
+#define LPC_EVF_TIMING hipEventDisableSystemFence
+#endif
+#ifndef LPC_EVF_SIDE
+#define LPC_EVF_SIDE 0
+#endif
+
 struct lpc_handle {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -742,7 +753,7 @@ static hipEvent_t ev_get(lpc_handle *h)
         return e;
     }
     hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDefault) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, LPC_EVF_TIMING) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -1359,7 +1370,7 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
     {   // the side stream of the sliver kernels and its fork / join events
-        const unsigned evf = hipEventDisableTiming;
+        const unsigned evf = hipEventDisableTiming | LPC_EVF_SIDE;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
