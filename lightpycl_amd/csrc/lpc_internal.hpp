@@ -6,7 +6,7 @@
 namespace lpck {
 
 struct Piece {                       // part of one mesh run
-    int32_t root;                     // subtree root node (k_intersect)
+    int32_t root;                     // subtree root node (the root items' start)
     int32_t s_lo, s_hi;               // sliver records [s_lo, s_hi) (k_slivers)
     int32_t slot;                     // per-mesh scratch slot the run flushes into
     float cx, cy, cz, negB, negA;     // the root's own test
@@ -31,7 +31,7 @@ __host__ __device__ inline float slot_key_t(unsigned long long k)
 __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (int32_t)(uint32_t)k; }
 
 // Profiling counters (lpc_prof_enable(h, 2)): [0..3] traversal counters,
-// [HIST..HIST+24) k_intersect wave-duration histogram (log2 of 100 MHz ticks),
+// [HIST..HIST+24) walk item duration histogram (log2 of 100 MHz ticks),
 // [PIECE..PIECE+PIECES) summed wave ticks per piece.
 #define LPC_STATS_HIST 8
 #define LPC_STATS_PIECE 32
@@ -40,7 +40,7 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 #define LPC_STATS_WORDS (LPC_STATS_CYC + 8)
 
 // Per-launch device words of the intersect stage (uint32, reset by k_slot_init
-// or k_stage_move): [6..13] hand-over queue lengths (k_intersect / k_rootwalk ->
+// or k_stage_move): [6..13] hand-over queue lengths (k_rootwalk ->
 // k_spill level 0 -> level 1 ...), from word 32 the root-item shard counters
 // (k_roots*), each on a 128-byte line of its own: a device-scope atomic evicts its
 // line from the L2, and one word serialises its atomics (~11 ns each).
@@ -53,7 +53,7 @@ __host__ __device__ inline int32_t slot_key_idx(unsigned long long k) { return (
 // packet (64 rays of the coherence order) against one subtree of a mesh run,
 // packed in 64 bits: packet (24 bits) | node (28 bits) | slot (12 bits).  k_roots*
 // write the (packet, piece root) pairs whose root test some ray passes (the test
-// k_intersect's waves start with); k_rootwalk walks them grid-stride.
+// each walk item starts with); k_rootwalk walks them grid-stride.
 __host__ __device__ inline uint64_t q_item(uint32_t w, uint32_t node, uint32_t slot)
 {
     return ((uint64_t)w << 40) | ((uint64_t)node << 12) | (uint64_t)slot;
@@ -75,7 +75,7 @@ struct QueueArgs {
 // root shard of a k_roots* block
 __host__ __device__ inline int q_shard(uint32_t block) { return (int)(block % LPC_Q_CSHARDS); }
 
-// Work hand-over: a k_intersect wave that has visited `budget` nodes with two or
+// Work hand-over: a walk wave that has visited `budget` nodes with two or
 // more subtrees still on its stack queues each of them as one item; k_spill
 // runs the items, one wave each (per-ray results flush with the same
 // order-independent atomics, so the split does not change the result).

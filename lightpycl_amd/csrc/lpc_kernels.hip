@@ -85,8 +85,7 @@ static __device__ __forceinline__ T wave_red(T v, int op)   // 0 min, 1 max, 2 s
 }
 
 // Packet bound of each wave of 64 * RPL rays (one wave per packet; ray
-// w*64*RPL + r*64 + lane on lane `lane`, the map of k_intersect (RPL 1) and
-// k_slivers (RPL 2)).
+// w*64*RPL + r*64 + lane on lane `lane`: k_slivers' map for RPL 2).
 template <int RPL>
 static __device__ __forceinline__ void packet_bound(const RaysIn &R, const float *__restrict__ rs, int64_t n,
                                                     PacketRec *__restrict__ pk, int64_t w, int lane)
@@ -640,10 +639,10 @@ static __device__ __forceinline__ void sliver_group(const SliverArgs &A, int64_t
                                                     int64_t w1, int piece);
 static __device__ __forceinline__ void sliver_launch_size(const SliverArgs &A, int64_t &n, float &dmax);
 
-// k_rootwalk: the root items (k_roots), grid-stride, one item per wave at a
-// time -- k_intersect's (packet, piece) waves without the waves whose root test
-// fails.  A wave that exceeds the hand-over budget queues its remaining
-// subtrees for k_spill (`out`), as k_intersect does.
+// k_rootwalk: the root items (k_roots_s / k_gather_roots: the (packet, piece)
+// pairs whose root test some ray of the packet passes), grid-stride, one item per
+// wave at a time.  A wave that exceeds the hand-over budget queues its remaining
+// subtrees for k_spill (`out`).
 // One wave per block: a block's slots free as soon as its item ends, where a
 // 4-wave block holds its LDS until its slowest item ends (round 2 per-item
 // records: ~2 800 of 6 144 wave slots walking on average with 4).

@@ -59,7 +59,7 @@ struct Pop {
 };
 
 struct PieceTable {
-    DBuf pieces, spieces;              // hierarchy pieces (k_rootwalk / k_intersect), sliver pieces (k_slivers)
+    DBuf pieces, spieces;              // hierarchy pieces (k_roots_s / k_rootwalk), sliver pieces (k_slivers)
     int32_t npieces = 0, nspieces = 0;
     DBuf groups;                       // k_roots_s gate: the runs' root records, s_lo/s_hi = their pieces
     int32_t ngroups = 0;               // 0: no gate (pieces are the run roots, or > 64 runs)
@@ -96,16 +96,11 @@ const double kThin = 1.0;               // thin-triangle rule factor (thin_axis;
 
 }  // namespace
 
-// Event flags.  The timing events of lpc_prof_enable skip the system-scope
-// fence of an event record (cache writeback + invalidate: ~7 us of GPU idle per
-// walk launch with it, ~0 without; round 5 A/B).  The side
-// stream's fork / join events keep it (ReleaseToDevice measured equal).
-#ifndef LPC_EVF_TIMING
-#define LPC_EVF_TIMING hipEventDisableSystemFence
-#endif
-#ifndef LPC_EVF_SIDE
-#define LPC_EVF_SIDE 0
-#endif
+// The timing events of lpc_prof_enable skip the system-scope fence of an event
+// record (cache writeback + invalidate: ~7 us of GPU idle per walk launch with
+// it, ~0 without; round 5 A/B).  The side stream's fork /
+// join events keep it (a device-scope release measured equal).
+static const unsigned kEvTimingFlags = hipEventDisableSystemFence;
 
 struct lpc_handle {
     int device = 0;
@@ -221,7 +216,7 @@ struct lpc_handle {
     DBuf d_acc;
     DBuf d_tmp;                                     // misc small device scratch
     DBuf d_scan;                                    // RayScan of set_rays (k_ray_scan)
-    DBuf d_stats;                                   // k_intersect counters (profiling)
+    DBuf d_stats;                                   // walk counters (profiling)
     // profiling
     bool prof = false, prof_stats = false, prof_light = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
@@ -753,7 +748,7 @@ static hipEvent_t ev_get(lpc_handle *h)
         return e;
     }
     hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, LPC_EVF_TIMING) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, kEvTimingFlags) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -1370,7 +1365,7 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
     {   // the side stream of the sliver kernels and its fork / join events
-        const unsigned evf = hipEventDisableTiming | LPC_EVF_SIDE;
+        const unsigned evf = hipEventDisableTiming;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
             hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
