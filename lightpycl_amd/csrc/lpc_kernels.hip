@@ -2203,6 +2203,21 @@ __global__ __launch_bounds__(256) void k_export(int64_t n, RaysIn in, ShadeOutPt
 }
 
 // (n,4) rows -> SoA xyz
+// Results export into a mapped host block (the drop-in's results mode): a
+// grid-stride copy with 16-byte vector stores (a 4-byte tail) written over PCIe
+// from the export stream, instead of a DMA copy.
+typedef uint32_t lpc_u4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy_host(const lpc_u4 *__restrict__ src, lpc_u4 *__restrict__ dst,
+                                                   int64_t n16, int64_t bytes)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        __builtin_nontemporal_store(src[i], &dst[i]);
+    const int64_t t0 = n16 * 16, nt = (bytes - t0) / 4;
+    if (blockIdx.x == 0 && (int64_t)threadIdx.x < nt)
+        ((uint32_t *)((char *)dst + t0))[threadIdx.x] = ((const uint32_t *)((const char *)src + t0))[threadIdx.x];
+}
+
 __global__ __launch_bounds__(256) void k_unpack4(int64_t n, const float4 *__restrict__ in,
                                                  float *__restrict__ x, float *__restrict__ y,
                                                  float *__restrict__ z)
