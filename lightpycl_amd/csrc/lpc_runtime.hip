@@ -21,7 +21,6 @@
 #include <map>
 #include <string>
 #include <vector>
-#include <unordered_set>
 
 using namespace lpck;
 
@@ -185,8 +184,6 @@ struct lpc_handle {
     int32_t hist_iter = -1;                         //   speculation's prediction) and its iteration limit
     bool dcap_rebuilt = false;                      // check_dcap rebuilt the records (a speculative iteration is void)
     unsigned int acc_seq = 0;
-    int xcopy = 0;                                   // LPC_XCOPY (A/B): results export by a copy kernel
-    std::unordered_set<void *> xseen;                // host blocks an export has written
     int host_prof = 0;                              // LPC_HOSTPROF: host-side timing of each iteration (stderr);
                                                     //   2: also each launch's hand-over queue lengths (synchronising)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
@@ -1367,7 +1364,6 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
-    h->xcopy = (int)env_int("LPC_XCOPY", 0);
     {   // the side stream of the sliver kernels and its fork / join events
         const unsigned evf = hipEventDisableTiming;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
@@ -2108,29 +2104,32 @@ static int export_chunk(lpc_handle *h, const RaysIn &in, const ShadeOutPtrs &o, 
     HIPCHK(h, hipEventRecord(h->ev_xready[par], h->stream));
     HIPCHK(h, hipStreamWaitEvent(h->xstream, h->ev_xready[par], 0));
     const double hm = h->host_prof ? host_us() : 0.0;
-    void *hdev = nullptr;
-    const bool first_use = h->xseen.insert(X.host).second;
-    if (nc == N && (h->xcopy == 1 || (h->xcopy == 2 && first_use)) &&
-        hipHostGetDevicePointer(&hdev, X.host, 0) == hipSuccess && hdev && ((uintptr_t)hdev & 15u) == 0) {
-        const size_t bytes = (size_t)nc * row;
-        hipLaunchKernelGGL(k_copy_host, dim3(1024), dim3(256), 0, h->xstream, (const lpc_u4 *)d, (lpc_u4 *)hdev,
-                           (int64_t)(bytes / 16), (int64_t)bytes);
-        HIPCHK(h, hipGetLastError());
-    } else if (nc == N) {
-        HIPCHK(h, hipMemcpyAsync(X.host, d, (size_t)nc * row, hipMemcpyDeviceToHost, h->xstream));
-        if (h->host_prof) {
-            hipPointerAttribute_t pa;
-            const hipError_t pe = hipPointerGetAttributes(&pa, X.host);
-            fprintf(stderr, "[lpc host]   export memcpy %.1f us (host %p, %zu B, pointer type %d, rc %d)\n",
-                    host_us() - hm, (void *)X.host, (size_t)nc * row, pe == hipSuccess ? (int)pa.type : -1, (int)pe);
+    // the copy into the caller's pinned block: a copy kernel writing the mapped
+    // block over PCIe (round 5: hipMemcpyAsync into a block stalled the host 4-15 ms
+    // on the block's first asynchronous copy, whatever primed it, DESIGN.md
+    // section 7e), or a DMA copy when the block is not device-mapped / aligned
+    auto copy_out = [&](char *host, const char *dev, size_t bytes) -> int {
+        void *hdev = nullptr;
+        if (hipHostGetDevicePointer(&hdev, host, 0) == hipSuccess && hdev && (((uintptr_t)hdev | (uintptr_t)dev) & 15u) == 0) {
+            hipLaunchKernelGGL(k_copy_host, dim3(1024), dim3(256), 0, h->xstream, (const lpc_u4 *)dev, (lpc_u4 *)hdev,
+                               (int64_t)(bytes / 16), (int64_t)bytes);
+            HIPCHK(h, hipGetLastError());
+        } else {
+            HIPCHK(h, hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, h->xstream));
         }
+        return 0;
+    };
+    if (nc == N) {
+        RETIF(copy_out(X.host, d, (size_t)nc * row));
+        if (h->host_prof)
+            fprintf(stderr, "[lpc host]   export copy %.1f us (host %p, %zu B)\n", host_us() - hm, (void *)X.host,
+                    (size_t)nc * row);
     } else {                                                    // chunk: each section at its rays' offset
         size_t hoff = 0, doff = 0;
         const size_t elt[4] = {orow, 16, 4, 4};
         for (int k = 0; k < 4; ++k) {
             if (elt[k] == 0) continue;
-            HIPCHK(h, hipMemcpyAsync(X.host + hoff + (size_t)base * elt[k], d + doff, (size_t)nc * elt[k],
-                                     hipMemcpyDeviceToHost, h->xstream));
+            RETIF(copy_out(X.host + hoff + (size_t)base * elt[k], d + doff, (size_t)nc * elt[k]));
             hoff += (size_t)N * elt[k];
             doff += (size_t)nc * elt[k];
         }
@@ -2475,17 +2474,6 @@ int lpc_host_alloc(size_t bytes, void **out)
     *out = nullptr;
     const hipError_t e = hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault);
     if (e != hipSuccess) return set_err(nullptr, LPC_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
-    const int prime = getenv("LPC_HOST_PRIME") ? atoi(getenv("LPC_HOST_PRIME")) : 0;
-    if (prime == 1) {                               // A/B: a device fill of the new block
-        (void)hipMemset(*out, 0, bytes ? bytes : 16);
-        (void)hipDeviceSynchronize();
-    } else if (prime == 2) {                        // A/B: one DMA copy into the whole new block
-        void *d = nullptr;
-        if (hipMalloc(&d, bytes ? bytes : 16) == hipSuccess) {
-            (void)hipMemcpy(*out, d, bytes ? bytes : 16, hipMemcpyDeviceToHost);
-            (void)hipFree(d);
-        }
-    }
     return 0;
 }
 
