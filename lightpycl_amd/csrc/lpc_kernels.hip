@@ -279,22 +279,24 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
     // (< 64) for the next one; the final drain tests them all
     const int todo = final ? np : (np & ~63);
     n_pairs += (uint32_t)todo;
+    auto pair_test = [&](uint32_t pr, const ExactRec &x) {
+        const int32_t idx = (int32_t)(pr >> 6);
+        const int r = (int)(pr & 63u);
+        const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
+        const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
+        float t;
+        if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
+            t > eps) {
+            atomicAdd(&L.lcnt[r], 1);
+            if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
+        }
+        if (PROF) ++n_exact;
+    };
     for (int base = 0; base < todo; base += 64) {
         const int q = base + lane;
         if (q < todo) {
             const uint32_t pr = L.pairs[q];
-            const int32_t idx = (int32_t)(pr >> 6);
-            const int r = (int)(pr & 63u);
-            const ExactRec x = xrec[idx];
-            const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
-            const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
-            float t;
-            if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
-                t > eps) {
-                atomicAdd(&L.lcnt[r], 1);
-                if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
-            }
-            if (PROF) ++n_exact;
+            pair_test(pr, xrec[(int32_t)(pr >> 6)]);
         }
     }
     const int rest = np - todo;
