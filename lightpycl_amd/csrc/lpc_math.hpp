@@ -166,7 +166,8 @@ LPC_HD PostOut postproc(int32_t K, int32_t prev, const int32_t *mat_type, float 
     float t_min = max_ray_len;
     int32_t hit_cnt = 0;
     constexpr int32_t KL = KU > 0 ? KU : 0x7fffffff;
-#pragma unroll
+    constexpr int32_t UF = KU > 0 ? KU : 1;                             // unroll factor (KU = 0: a loop)
+#pragma unroll UF
     for (int32_t j = 0; j < KL; ++j) {                                  // .cl:127-135
         if (KU == 0 && j >= K) break;
         float tj; int32_t cj, ij;
@@ -185,7 +186,7 @@ LPC_HD PostOut postproc(int32_t K, int32_t prev, const int32_t *mat_type, float 
         }
         float t_minmin = t_min, t_maxmin = t_min, t_minmax = max_ray_len;
         int32_t maxmin_entering = 0, maxmin_idx = -1, minmax_idx = -1;
-#pragma unroll
+#pragma unroll UF
         for (int32_t j = 0; j < KL; ++j) {                              // .cl:193-214
             if (KU == 0 && j >= K) break;
             int32_t mt = j < K ? mat_type[j] : -1;
