@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LPC_ABI_VERSION 2
+#define LPC_ABI_VERSION 3
 
 enum {
     LPC_OK = 0,
@@ -288,6 +288,7 @@ typedef struct {
     int64_t xchg_calls;      /* its calls (per-iteration stats + trace-end aggregates)  */
     int64_t walk_cycles;     /* level 2: summed shader-clock cycles of the walk items (per wave) */
     int64_t drain_cycles;    /* ... of them inside the exact-test drains                         */
+    int64_t fan_exact;       /* level 2: exact tests on fan triangles (a vertex shared by >= 32) */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * traversal counters (2, diagnostic: adds atomics), only the walk kernel's

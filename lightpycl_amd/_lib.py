@@ -37,7 +37,8 @@ class Prof(ctypes.Structure):
                 ("tail_waves", ctypes.c_int64), ("tail_nodes", ctypes.c_int64),
                 ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("xchg_us", ctypes.c_double), ("xchg_calls", ctypes.c_int64),
-                ("walk_cycles", ctypes.c_int64), ("drain_cycles", ctypes.c_int64)]
+                ("walk_cycles", ctypes.c_int64), ("drain_cycles", ctypes.c_int64),
+                ("fan_exact", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p
@@ -137,7 +138,7 @@ def load(path: str = LIB_PATH):
         fn.restype = ctypes.c_int
     L.lpc_last_error.argtypes = [_P]
     L.lpc_last_error.restype = ctypes.c_char_p
-    if L.lpc_abi_version() != 2:
+    if L.lpc_abi_version() != 3:
         raise LpcError("liblpc ABI version mismatch")
     _lib = L
     return L

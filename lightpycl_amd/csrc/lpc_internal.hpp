@@ -89,6 +89,7 @@ struct SpillArgs {
     int budget;                       // cost before hand-over (0: never), in node visits
     int pair_shift;                   // exact pairs per node visit = 1 << pair_shift (31: not counted)
     uint32_t *tmask;                  // per ray: bit j set when a flush wrote slot j (NULL: not kept)
+    const uint8_t *fan;               // profiling (PROF): triangles with a vertex shared by >= 32 others
 };
 
 struct RaysIn {                       // a ray population (SoA)

@@ -226,7 +226,7 @@ struct WaveLds {
 // 64 per step, one per lane (record gathered, ray read from L.ray).
 template <bool PROF>
 static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int32_t &np, const bool final,
-                                                   const int lane,
+                                                   const int lane, const uint8_t *__restrict__ fan, uint32_t &n_fan,
                                                    const ExactRec *__restrict__ xrec, const float eps,
                                                    const float max_ray_len, const unsigned long long key0,
                                                    const f3 &O, const f3 &D, uint32_t &n_pairs, uint32_t &n_exact)
@@ -262,7 +262,7 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
                         ukey = k < ukey ? k : ukey;
                     }
                 }
-                if (PROF) ++n_exact;
+                if (PROF) { ++n_exact; if (fan && fan[idx]) ++n_fan; }
             }
             n_pairs += (uint32_t)__builtin_popcountll(m);
             idx = nidx;
@@ -290,7 +290,7 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
             atomicAdd(&L.lcnt[r], 1);
             if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
         }
-        if (PROF) ++n_exact;
+        if (PROF) { ++n_exact; if (fan && fan[idx]) ++n_fan; }
     };
     for (int base = 0; base < todo; base += 64) {
         const int q = base + lane;
@@ -344,6 +344,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     int32_t top = 0, nq = 0, np = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
     uint32_t n_pairs = 0;                           // exact pairs drained (wave-uniform; hand-over cost)
+    uint32_t n_fan = 0;                             // PROF: exact tests on fan triangles (SpillArgs::fan)
     // Exact tests are deferred: candidate (triangle, ray lanes) entries queue up
     // in LDS; a drain expands them into (triangle, ray) pairs, runs 64 pairs at a
     // time one per lane (exact record gathered, ray read from LDS) and folds the
@@ -354,7 +355,8 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     const uint64_t cyc0 = (PROF && stats) ? clock64() : 0;
     auto drain = [&](bool final) {
         const uint64_t c0 = (PROF && stats) ? clock64() : 0;
-        drain_queue<PROF>(L, nq, np, final, lane, xrec, eps, max_ray_len, key0, O, D, n_pairs, n_exact);
+        drain_queue<PROF>(L, nq, np, final, lane, PROF ? SP.fan : nullptr, n_fan, xrec, eps, max_ray_len, key0, O, D,
+                          n_pairs, n_exact);
         if (PROF && stats) cyc_drain += clock64() - c0;
     };
     int budget = SP.budget;
@@ -423,7 +425,10 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     }
     drain(true);
     if (PROF && stats) {
-        for (int o = 32; o >= 1; o >>= 1) n_exact += __shfl_xor(n_exact, o, 64);
+        for (int o = 32; o >= 1; o >>= 1) {
+            n_exact += __shfl_xor(n_exact, o, 64);
+            n_fan += __shfl_xor(n_fan, o, 64);
+        }
         // packet spread: max angle between a lane's direction and lane 0's
         const float cs = nx * bcast(nx, 0) + ny * bcast(ny, 0) + nz * bcast(nz, 0);
         const float cmin = wave_red(cs, 0);
@@ -439,6 +444,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
             atomicAdd(&stats[0], (unsigned long long)n_nodes);
             atomicAdd(&stats[LPC_STATS_CYC], (unsigned long long)(clock64() - cyc0));
             atomicAdd(&stats[LPC_STATS_CYC + 1], (unsigned long long)cyc_drain);
+            if (n_fan) atomicAdd(&stats[LPC_STATS_CYC + 2], (unsigned long long)n_fan);
             atomicAdd(&stats[2], 1ull);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
             atomicAdd(&stats[LPC_STATS_HIST + b], 1ull);

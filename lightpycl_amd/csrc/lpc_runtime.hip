@@ -11,6 +11,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -217,6 +218,7 @@ struct lpc_handle {
     DBuf d_tmp;                                     // misc small device scratch
     DBuf d_scan;                                    // RayScan of set_rays (k_ray_scan)
     DBuf d_stats;                                   // walk counters (profiling)
+    DBuf d_fan;                                     // profiling: fan-triangle flags (SpillArgs::fan)
     // profiling
     bool prof = false, prof_stats = false, prof_light = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_isect, ev_rest, ev_kern;
@@ -785,7 +787,24 @@ struct DevSize {
 // Work hand-over (k_spill levels): queue, budget by population size.
 static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
 {
-    *SP = SpillArgs{nullptr, nullptr, 0u, 0, 31, h->tm_cur};
+    *SP = SpillArgs{nullptr, nullptr, 0u, 0, 31, h->tm_cur, nullptr};
+    if (h->prof_stats) {                // diagnostic: the fan triangles (apex valence >= 32), built once
+        if (!h->d_fan.p) {
+            std::map<std::array<uint32_t, 3>, int32_t> val;
+            auto key = [&](const std::vector<float> &v, int32_t i) {
+                std::array<uint32_t, 3> k;
+                memcpy(k.data(), &v[4 * (size_t)i], 12);
+                return k;
+            };
+            for (int32_t i = 0; i < h->M; ++i) { ++val[key(h->hv0, i)]; ++val[key(h->hv1, i)]; ++val[key(h->hv2, i)]; }
+            std::vector<uint8_t> f((size_t)h->M, 0);
+            for (int32_t i = 0; i < h->M; ++i)
+                f[(size_t)i] = val[key(h->hv0, i)] >= 32 || val[key(h->hv1, i)] >= 32 || val[key(h->hv2, i)] >= 32;
+            RETIF(dalloc(h, h->d_fan, (size_t)h->M));
+            HIPCHK(h, hipMemcpy(h->d_fan.p, f.data(), (size_t)h->M, hipMemcpyHostToDevice));
+        }
+        SP->fan = (const uint8_t *)h->d_fan.p;
+    }
     if (h->spill_budget <= 0) return 0;
     RETIF(dalloc(h, h->w_spill, (size_t)2 * h->spill_cap * sizeof(SpillItem)));
     SP->items = (SpillItem *)h->w_spill.p;
@@ -1455,6 +1474,7 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
         if (mesh_id[i] < 0 || mesh_id[i] >= K)
             return set_err(h, LPC_E_ARG, "mesh_id[" + std::to_string(i) + "] out of range");
     h->M = M; h->K = K;
+    dfree(h->d_fan);                                // profiling flags of the previous scene
     h->hv0.assign(v0, v0 + 4 * (size_t)M);
     h->hv1.assign(v1, v1 + 4 * (size_t)M);
     h->hv2.assign(v2, v2 + 4 * (size_t)M);
@@ -2842,6 +2862,7 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     out->tail_waves = (int64_t)st[4]; out->tail_nodes = (int64_t)st[5];
     out->tail_spread_urad = (int64_t)st[6]; out->tail_exact = (int64_t)st[7];
     out->walk_cycles = (int64_t)st[LPC_STATS_CYC]; out->drain_cycles = (int64_t)st[LPC_STATS_CYC + 1];
+    out->fan_exact = (int64_t)st[LPC_STATS_CYC + 2];
     out->heavy_piece = -1; out->heavy_piece_ticks = 0; out->piece_ticks = 0;
     for (int p = 0; p < LPC_STATS_PIECES; ++p) {
         const int64_t v = (int64_t)st[LPC_STATS_PIECE + p];

@@ -45,8 +45,9 @@ for counters in (False, True):
             print(f"    walk items: {pr['walk_cycles'] / waves:.0f} shader cycles each, "
                   f"{100.0 * pr['drain_cycles'] / wc:.1f}% in exact-test drains; "
                   f"{(pr['walk_cycles'] - pr['drain_cycles']) / max(pr['node_visits'], 1):.0f} cycles per node visit "
-                  f"outside drains, {pr['drain_cycles'] / max(pr['exact_tests'], 1):.1f} drain cycles per exact test",
-                  flush=True)
+                  f"outside drains, {pr['drain_cycles'] / max(pr['exact_tests'], 1):.1f} drain cycles per exact test; "
+                  f"{100.0 * pr['fan_exact'] / max(pr['exact_tests'], 1):.1f}% of exact tests on fan triangles "
+                  f"({pr['fan_exact'] / max(nin, 1):.1f} per ray)", flush=True)
             tw = max(pr["tail_waves"], 1)
             print(f"    tail waves {pr['tail_waves']}: nodes/wave {pr['tail_nodes']/tw:.0f} "
                   f"spread {pr['tail_spread_urad']/tw/1e6:.4f} rad exact/wave {pr['tail_exact']/tw:.0f}; "
