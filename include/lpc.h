@@ -289,6 +289,8 @@ typedef struct {
     int64_t walk_cycles;     /* level 2: summed shader-clock cycles of the walk items (per wave) */
     int64_t drain_cycles;    /* ... of them inside the exact-test drains                         */
     int64_t fan_exact;       /* level 2: exact tests on fan triangles (a vertex shared by >= 32) */
+    int64_t behind_exact;    /* ... on triangles wholly behind the ray origin                    */
+    int64_t hit_exact;       /* ... accepted (t > eps)                                            */
 } lpc_prof;
 /* Enable per-launch HIP-event timing of the hot kernels (1), timing plus
  * traversal counters (2, diagnostic: adds atomics), only the walk kernel's

@@ -38,7 +38,8 @@ class Prof(ctypes.Structure):
                 ("tail_spread_urad", ctypes.c_int64), ("tail_exact", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("xchg_us", ctypes.c_double), ("xchg_calls", ctypes.c_int64),
                 ("walk_cycles", ctypes.c_int64), ("drain_cycles", ctypes.c_int64),
-                ("fan_exact", ctypes.c_int64)]
+                ("fan_exact", ctypes.c_int64), ("behind_exact", ctypes.c_int64),
+                ("hit_exact", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

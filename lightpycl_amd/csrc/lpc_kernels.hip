@@ -224,9 +224,25 @@ struct WaveLds {
 // (L.qidx / L.qmask [0, nq)) are tested triangle-uniform (the record by scalar
 // loads, each lane its own ray in registers), the sparse pairs (L.pairs [0, np))
 // 64 per step, one per lane (record gathered, ray read from L.ray).
+// PROF: an exact test's class -- on a fan triangle, wholly behind the ray origin
+// (all three vertices at (V - O).D < 0), an accepted hit (t > eps).
+struct ExactClass {
+    uint32_t fan, behind, hit;
+};
+static __device__ __forceinline__ void exact_class(ExactClass &c, const uint8_t *__restrict__ fan, int32_t idx,
+                                                   const f3 &O, const f3 &D, const ExactRec &x, bool hit)
+{
+    if (fan && fan[idx]) ++c.fan;
+    const float a0 = (x.v0x - O.x) * D.x + (x.v0y - O.y) * D.y + (x.v0z - O.z) * D.z;
+    const float a1 = a0 + (x.e1x * D.x + x.e1y * D.y + x.e1z * D.z);
+    const float a2 = a0 + (x.e2x * D.x + x.e2y * D.y + x.e2z * D.z);
+    if (a0 < 0.0f && a1 < 0.0f && a2 < 0.0f) ++c.behind;
+    if (hit) ++c.hit;
+}
+
 template <bool PROF>
 static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int32_t &np, const bool final,
-                                                   const int lane, const uint8_t *__restrict__ fan, uint32_t &n_fan,
+                                                   const int lane, const uint8_t *__restrict__ fan, ExactClass &xc,
                                                    const ExactRec *__restrict__ xrec, const float eps,
                                                    const float max_ray_len, const unsigned long long key0,
                                                    const f3 &O, const f3 &D, uint32_t &n_pairs, uint32_t &n_exact)
@@ -254,15 +270,16 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
             const ExactRec nx = xrec[nidx];
             if ((m >> lane) & 1ull) {
                 float t;
-                if (mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z),
-                             &t) && t > eps) {
+                const bool hit = mt_exact(O, D, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
+                                          mk3(x.e2x, x.e2y, x.e2z), &t) && t > eps;
+                if (hit) {
                     ++ucnt;
                     if (t < max_ray_len) {
                         const unsigned long long k = slot_key(t, idx);
                         ukey = k < ukey ? k : ukey;
                     }
                 }
-                if (PROF) { ++n_exact; if (fan && fan[idx]) ++n_fan; }
+                if (PROF) { ++n_exact; exact_class(xc, fan, idx, O, D, x, hit); }
             }
             n_pairs += (uint32_t)__builtin_popcountll(m);
             idx = nidx;
@@ -285,12 +302,13 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
         const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
         const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
         float t;
-        if (mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z), mk3(x.e2x, x.e2y, x.e2z), &t) &&
-            t > eps) {
+        const bool hit = mt_exact(Or, Dr, mk3(x.v0x, x.v0y, x.v0z), mk3(x.e1x, x.e1y, x.e1z),
+                                  mk3(x.e2x, x.e2y, x.e2z), &t) && t > eps;
+        if (hit) {
             atomicAdd(&L.lcnt[r], 1);
             if (t < max_ray_len) atomicMin(&L.lkey[r], slot_key(t, idx));
         }
-        if (PROF) { ++n_exact; if (fan && fan[idx]) ++n_fan; }
+        if (PROF) { ++n_exact; exact_class(xc, fan, idx, Or, Dr, x, hit); }
     };
     for (int base = 0; base < todo; base += 64) {
         const int q = base + lane;
@@ -344,7 +362,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     int32_t top = 0, nq = 0, np = 0;
     uint32_t n_nodes = 0, n_exact = 0;              // profiling counters (stats != NULL)
     uint32_t n_pairs = 0;                           // exact pairs drained (wave-uniform; hand-over cost)
-    uint32_t n_fan = 0;                             // PROF: exact tests on fan triangles (SpillArgs::fan)
+    ExactClass xc = {0u, 0u, 0u};                   // PROF: exact tests by class (exact_class)
     // Exact tests are deferred: candidate (triangle, ray lanes) entries queue up
     // in LDS; a drain expands them into (triangle, ray) pairs, runs 64 pairs at a
     // time one per lane (exact record gathered, ray read from LDS) and folds the
@@ -355,7 +373,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     const uint64_t cyc0 = (PROF && stats) ? clock64() : 0;
     auto drain = [&](bool final) {
         const uint64_t c0 = (PROF && stats) ? clock64() : 0;
-        drain_queue<PROF>(L, nq, np, final, lane, PROF ? SP.fan : nullptr, n_fan, xrec, eps, max_ray_len, key0, O, D,
+        drain_queue<PROF>(L, nq, np, final, lane, PROF ? SP.fan : nullptr, xc, xrec, eps, max_ray_len, key0, O, D,
                           n_pairs, n_exact);
         if (PROF && stats) cyc_drain += clock64() - c0;
     };
@@ -427,7 +445,9 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
     if (PROF && stats) {
         for (int o = 32; o >= 1; o >>= 1) {
             n_exact += __shfl_xor(n_exact, o, 64);
-            n_fan += __shfl_xor(n_fan, o, 64);
+            xc.fan += __shfl_xor(xc.fan, o, 64);
+            xc.behind += __shfl_xor(xc.behind, o, 64);
+            xc.hit += __shfl_xor(xc.hit, o, 64);
         }
         // packet spread: max angle between a lane's direction and lane 0's
         const float cs = nx * bcast(nx, 0) + ny * bcast(ny, 0) + nz * bcast(nz, 0);
@@ -444,7 +464,9 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
             atomicAdd(&stats[0], (unsigned long long)n_nodes);
             atomicAdd(&stats[LPC_STATS_CYC], (unsigned long long)(clock64() - cyc0));
             atomicAdd(&stats[LPC_STATS_CYC + 1], (unsigned long long)cyc_drain);
-            if (n_fan) atomicAdd(&stats[LPC_STATS_CYC + 2], (unsigned long long)n_fan);
+            if (xc.fan) atomicAdd(&stats[LPC_STATS_CYC + 2], (unsigned long long)xc.fan);
+            if (xc.behind) atomicAdd(&stats[LPC_STATS_CYC + 3], (unsigned long long)xc.behind);
+            if (xc.hit) atomicAdd(&stats[LPC_STATS_CYC + 4], (unsigned long long)xc.hit);
             atomicAdd(&stats[2], 1ull);
             atomicAdd(&stats[3], (unsigned long long)n_exact);
             atomicAdd(&stats[LPC_STATS_HIST + b], 1ull);

@@ -2863,6 +2863,8 @@ int lpc_prof_read(lpc_handle *h, lpc_prof *out, int reset)
     out->tail_spread_urad = (int64_t)st[6]; out->tail_exact = (int64_t)st[7];
     out->walk_cycles = (int64_t)st[LPC_STATS_CYC]; out->drain_cycles = (int64_t)st[LPC_STATS_CYC + 1];
     out->fan_exact = (int64_t)st[LPC_STATS_CYC + 2];
+    out->behind_exact = (int64_t)st[LPC_STATS_CYC + 3];
+    out->hit_exact = (int64_t)st[LPC_STATS_CYC + 4];
     out->heavy_piece = -1; out->heavy_piece_ticks = 0; out->piece_ticks = 0;
     for (int p = 0; p < LPC_STATS_PIECES; ++p) {
         const int64_t v = (int64_t)st[LPC_STATS_PIECE + p];

@@ -419,4 +419,5 @@ class Engine:
                     piece_ticks=p.piece_ticks, tail_waves=p.tail_waves, tail_nodes=p.tail_nodes,
                     tail_spread_urad=p.tail_spread_urad, tail_exact=p.tail_exact, kernel_ms=p.kernel_ms,
                     xchg_us=p.xchg_us, xchg_calls=p.xchg_calls, walk_cycles=p.walk_cycles,
-                    drain_cycles=p.drain_cycles, fan_exact=p.fan_exact)
+                    drain_cycles=p.drain_cycles, fan_exact=p.fan_exact,
+                    behind_exact=p.behind_exact, hit_exact=p.hit_exact)

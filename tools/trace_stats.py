@@ -47,7 +47,8 @@ for counters in (False, True):
                   f"{(pr['walk_cycles'] - pr['drain_cycles']) / max(pr['node_visits'], 1):.0f} cycles per node visit "
                   f"outside drains, {pr['drain_cycles'] / max(pr['exact_tests'], 1):.1f} drain cycles per exact test; "
                   f"{100.0 * pr['fan_exact'] / max(pr['exact_tests'], 1):.1f}% of exact tests on fan triangles "
-                  f"({pr['fan_exact'] / max(nin, 1):.1f} per ray)", flush=True)
+                  f"({pr['fan_exact'] / max(nin, 1):.1f} per ray); {100.0 * pr['behind_exact'] / max(pr['exact_tests'], 1):.1f}% "
+                  f"wholly behind the origin, {100.0 * pr['hit_exact'] / max(pr['exact_tests'], 1):.1f}% accepted", flush=True)
             tw = max(pr["tail_waves"], 1)
             print(f"    tail waves {pr['tail_waves']}: nodes/wave {pr['tail_nodes']/tw:.0f} "
                   f"spread {pr['tail_spread_urad']/tw/1e6:.4f} rad exact/wave {pr['tail_exact']/tw:.0f}; "
