@@ -426,6 +426,13 @@ def test_async_trace_run_equals_sync(name, n):
         e.run_local(sc.iterations, thr, wait=False)
         for x, y in zip(e.fetch_measured(), rec):
             np.testing.assert_array_equal(x, y)
+        # lpc_trace_rerun_async: the reset and the asynchronous trace in one call
+        for rep in range(3):
+            stats, (cnt, mp) = e.run_local(sc.iterations, thr, wait=False, reset=True)
+            got = ([(s.n_in, s.n_reflect, s.n_refract, s.n_measured, s.power_next) for s in stats], cnt, mp.tolist())
+            assert got == want
+        for x, y in zip(e.fetch_measured(), rec):
+            np.testing.assert_array_equal(x, y)
         e.sync()
     finally:
         e.close()
