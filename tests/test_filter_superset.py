@@ -129,7 +129,7 @@ def cluster_harness(harness):
 @pytest.mark.parametrize("name", ["lens", "eye", "synthetic", "parabolic"])
 def test_node_test_passes_for_every_accepted_triangle(cluster_harness, name):
     """Every ray whose line the exact test accepts against some triangle of a
-    64-triangle node must pass the node's test (k_intersect skips the node's
+    64-triangle node must pass the node's test (the walk skips the node's
     triangles otherwise).  Nodes are consecutive triangles of the real scenes'
     meshes; rays are aimed at those triangles (and their edges) from near and far
     origins, including grazing ones."""
@@ -424,7 +424,7 @@ def _packets(rng, V, npk, ball, dist, spread, line=False):
 @pytest.mark.parametrize("ball,dist,spread", [(0.0, 100.0, 1e-3), (1e-3, 30.0, 1e-2), (1.0, 10.0, 0.05),
                                               (30.0, 500.0, 1e-4), (0.0, 1e3, 0.0), (5.0, 2.0, 0.3)])
 def test_packet_tests_are_sound(packet_harness, sliver_harness, name, ball, dist, spread):
-    """k_intersect skips a cluster / triangle / sliver for a whole wave when the
+    """The sliver tests skip a cluster / triangle / sliver for a whole wave when the
     packet bound of its 128 rays (origin ball + direction cone, k_packet) fails the
     record's packet test; that must never happen while some ray of the packet passes
     the record's per-ray test."""

@@ -1,4 +1,4 @@
-"""GPU box: traversal statistics of k_intersect per bench iteration (diagnostic)."""
+"""GPU box: traversal statistics of the walk (k_rootwalk / k_spill) per bench iteration (diagnostic)."""
 import os
 import sys
 import time
