@@ -91,10 +91,8 @@ const int kSpillLevelsSmall = 1;        // ... below (round 5 A/B: 4 levels, lev
 const int64_t kSpillSmallN = 262144;
 const int64_t kSpillBlocks = 4096;      // k_spill level l grid: max(kSpillMinBlocks, kSpillBlocks >> l) x 4 waves
 const int64_t kSpillMinBlocks = 256;
-#ifndef LPC_PAIR_SHIFT
-#define LPC_PAIR_SHIFT 5
-#endif
-const int kSpillPairShift = LPC_PAIR_SHIFT;   // exact pairs per node visit in the hand-over budget (log2)
+const int kSpillPairShift = 5;          // exact pairs per node visit in the hand-over budget (log2; round 5
+                                        //   A/B with the pair list: 4 and 6 equal)
 const int kKeyObits = 6;                // re-sorted populations: origin bits per axis of the 5-D Morton key
 const double kThin = 1.0;               // thin-triangle rule factor (thin_axis; 0.25 / 2 measured slower)
 
