@@ -665,6 +665,18 @@ def main():
     valu_per_launch = None if stale else pmc.get("sq_insts_valu_mean")
     valu_rate = valu_per_launch / (avg_ms * 1e-3) if valu_per_launch and avg_ms > 0 else None
     valu_peak, valu_peak_pk, valu_peak_src = valu_issue_peak()
+    # the same HBM-traffic figure split by bounce: the primary launch (all rays) and the
+    # secondary launches (the survivors), each against its own algorithmic bytes
+    split = None
+    ips = iters / max(a.steps, 1)
+    if not stale and ips > 1:
+        sec_rays = (bounces / max(a.steps, 1) - a.rays) / (ips - 1)
+        split = {}
+        for k, n in (("primary", a.rays), ("secondary", sec_rays)):
+            hb = (pmc.get(k + "_launch") or {}).get("hbm_bytes")
+            ab = n * RAY_BYTES + M * TRI_BYTES
+            split[k] = {"rays_per_launch": n, "hbm_bytes": hb, "alg_bytes": ab,
+                        "traffic_over_alg": hb / ab if hb else None}
     out = {
         "metric": "ray-bounces/sec @ 1M rays x 100k tris",
         "value": bounces_all / dt,
@@ -688,6 +700,7 @@ def main():
                      "kernel": WALK_KERNEL, "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "launches_timed": int(prof["intersect_launches"]), "launches_all": int(iters),
+                     "traffic_by_bounce": split,
                      "note": f"achieved = algorithmic bytes per launch (156 B x rays + 40 B x triangles) / "
                              f"{WALK_KERNEL}'s own average launch time (HIP events on its stream over the "
                              f"timed region, launches_timed of launches_all); traffic = "

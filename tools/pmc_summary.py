@@ -25,7 +25,11 @@ kst = os.path.join(src, "kt", "kt_kernel_stats.csv")
 if os.path.exists(kst):                 # a kernel trace of the same run, when there is one
     shutil.copy(kst, os.path.join(out, f"{tag}_kernel_stats.csv"))
 per = collections.defaultdict(lambda: collections.defaultdict(list))
-for d in sorted(os.listdir(src)):
+if src.endswith(".json"):               # re-derive from a committed <tag>_pmc.json
+    for k, cs in json.load(open(src)).items():
+        for c, v in cs.items():
+            per[k][c] = list(v["values"])
+for d in ([] if src.endswith(".json") else sorted(os.listdir(src))):
     f = os.path.join(src, d, "pmc_counter_collection.csv")
     if d.startswith("pmc") and os.path.exists(f):
         for r in csv.DictReader(open(f)):
@@ -33,7 +37,8 @@ for d in sorted(os.listdir(src)):
             per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 summary = {k: {c: {"launches": len(v), "mean": sum(v) / len(v), "values": v} for c, v in cs.items()}
            for k, cs in per.items()}
-json.dump(summary, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
+if not src.endswith(".json"):
+    json.dump(summary, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
 ki = next((v for k, v in summary.items() if kname in k), {})
 if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
     fetch, write = ki["FETCH_SIZE"]["mean"], ki["WRITE_SIZE"]["mean"]
@@ -50,14 +55,19 @@ if "FETCH_SIZE" in ki and "WRITE_SIZE" in ki:
     # the primary (1 M-ray) launches alone: bench.py --steps 1 --warmup 0 runs the
     # first iteration by itself (launch 0), then traces of three iterations each
     # (pre-warm, timed, histogram): launches 1, 4, 7, ... are primaries
-    prim = {}
+    # the other launches are the secondary bounces (iterations 2 and 3)
+    prim, sec = {}, {}
     for c, v in ki.items():
-        idx = [0] + [i for i in range(1, len(v["values"])) if (i - 1) % 3 == 0]
-        vals = [v["values"][i] for i in idx if i < len(v["values"])]
-        if vals:
-            prim[c] = sum(vals) / len(vals)
-    if "FETCH_SIZE" in prim and "WRITE_SIZE" in prim:
-        prim["hbm_bytes"] = (2.0 * prim["FETCH_SIZE"] + prim["WRITE_SIZE"]) * 1024.0
+        n = len(v["values"])
+        idx = [0] + [i for i in range(1, n) if (i - 1) % 3 == 0]
+        for want, dst in ((idx, prim), ([i for i in range(n) if i not in idx], sec)):
+            vals = [v["values"][i] for i in want]
+            if vals:
+                dst[c] = sum(vals) / len(vals)
+    for dst in (prim, sec):
+        if "FETCH_SIZE" in dst and "WRITE_SIZE" in dst:
+            dst["hbm_bytes"] = (2.0 * dst["FETCH_SIZE"] + dst["WRITE_SIZE"]) * 1024.0
     rec["primary_launch"] = prim
+    rec["secondary_launch"] = sec
     json.dump(rec, open(os.path.join(out, "pmc_intersect.json"), "w"), indent=1)
     print(json.dumps(rec, indent=1))
