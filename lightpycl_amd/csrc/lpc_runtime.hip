@@ -79,6 +79,15 @@ const int64_t kSortMin = 4096;          // populations below this are traced uns
 const int64_t kOnesweepMin = 500000;    // rocPRIM onesweep radix sort from this many rays (merge sort below)
 const int kRootsPerBlock = 16;          // k_roots_s packets per block (one task per packet)
 const int64_t kQTarget = 65536;         // (packet, piece) root tests to aim for: the piece level
+#ifndef LPC_CHAIN_PIECES
+#define LPC_CHAIN_PIECES 4              // compile-time A/B builds (tools/build_variant.py)
+#endif
+// chained populations up to kChainPiecesMax rays whose target gives the run roots
+// (g = 1) take the pieces of g = kChainPieces instead (round 5 A/B, DESIGN.md
+// section 7e: lens 10 M -19 %, synthetic_dense -3 %; the eye's >= 38 M-ray
+// iterations +1-2 %, hence the cap; populations with g > 1 unchanged)
+const int32_t kChainPieces = LPC_CHAIN_PIECES;
+const int64_t kChainPiecesMax = (int64_t)32 << 20;
 #ifndef LPC_WALK_GRID
 #define LPC_WALK_GRID 65536             // compile-time A/B builds (tools/build_variant.py)
 #endif
@@ -883,14 +892,15 @@ static int run_spill_levels(lpc_handle *h, const RaysIn &in, const float *rs, in
 // Piece level of the work queue: pieces per run so that (packets x pieces) root
 // tests reach q_target (mesh run roots for large populations, finer pieces for
 // small ones, whose few packets would otherwise be few items).
-static int32_t q_level(const lpc_handle *h, int64_t n)
+static int32_t q_level(const lpc_handle *h, int64_t n, bool chained)
 {
     int64_t live_runs = 0;
     for (int32_t j = 0; j < h->K; ++j) live_runs += h->slot_run[(size_t)j] >= 0;
     live_runs = std::max<int64_t>(live_runs, 1);
     const int64_t npk = (n + 63) / 64;
-    return (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (kQTarget + npk * live_runs - 1) /
-                                                                      (npk * live_runs)));
+    const int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (kQTarget + npk * live_runs - 1) /
+                                                                               (npk * live_runs)));
+    return (g == 1 && chained && n <= kChainPiecesMax) ? kChainPieces : g;
 }
 
 // A device-side consistency check failed (QueueArgs::err / the compaction's
@@ -1042,7 +1052,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // the pieces of the root items: q_level's cut (the same sliver pieces at every
     // cut), coarser while k_roots_s cannot hold them (tiny populations)
     PieceTable *pt;
-    int32_t g = q_level(h, n);
+    int32_t g = q_level(h, n, traced && h->pop_traced);
     RETIF(piece_table(h, &pt, g));
     while (pt->npieces > 64 * LPC_ROOTS_TASKS && g > 1) {
         g = std::max(1, g / 8);
