@@ -83,11 +83,13 @@ const int64_t kQTarget = 65536;         // (packet, piece) root tests to aim for
 #define LPC_CHAIN_PIECES 4              // compile-time A/B builds (tools/build_variant.py)
 #endif
 // chained populations up to kChainPiecesMax rays whose target gives the run roots
-// (g = 1) take the pieces of g = kChainPieces instead (round 5 A/B, DESIGN.md
-// section 7e: lens 10 M -19 %, synthetic_dense -3 %; the eye's >= 38 M-ray
-// iterations +1-2 %, hence the cap; populations with g > 1 unchanged)
+// (g = 1) in a scene of fewer than kChainPiecesRuns live mesh runs take the pieces
+// of g = kChainPieces instead (round 5 A/B, DESIGN.md section 5: lens 10 M -21 %;
+// the eye's >= 38 M-ray iterations +1-2 %, hence the size cap; the 10-run
+// synthetic scene's config 5 +5 % (dense -3 %), hence the run bound)
 const int32_t kChainPieces = LPC_CHAIN_PIECES;
 const int64_t kChainPiecesMax = (int64_t)32 << 20;
+const int64_t kChainPiecesRuns = 8;
 #ifndef LPC_WALK_GRID
 #define LPC_WALK_GRID 65536             // compile-time A/B builds (tools/build_variant.py)
 #endif
@@ -900,7 +902,7 @@ static int32_t q_level(const lpc_handle *h, int64_t n, bool chained)
     const int64_t npk = (n + 63) / 64;
     const int32_t g = (int32_t)std::min<int64_t>(4096, std::max<int64_t>(1, (kQTarget + npk * live_runs - 1) /
                                                                                (npk * live_runs)));
-    return (g == 1 && chained && n <= kChainPiecesMax) ? kChainPieces : g;
+    return (g == 1 && chained && n <= kChainPiecesMax && live_runs < kChainPiecesRuns) ? kChainPieces : g;
 }
 
 // A device-side consistency check failed (QueueArgs::err / the compaction's
