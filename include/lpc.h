@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LPC_ABI_VERSION 3
+#define LPC_ABI_VERSION 4
 
 enum {
     LPC_OK = 0,
@@ -177,21 +177,23 @@ int lpc_host_seq_sum_f32(const float *x, int64_t n, float *out);
  * receives each iteration's stats, *n_iter their number.  Same results as
  * calling lpc_trace_iterate from the host loop, without a host round trip
  * through the caller per iteration.  measured_count / mesh_power (may be NULL)
- * receive lpc_trace_measured's outputs at the end. */
+ * receive lpc_trace_measured's outputs at the end: mesh_power one double per
+ * mesh of the current scene, into a buffer of mesh_power_cap doubles
+ * (LPC_E_ARG, before anything runs, when the scene has more meshes; ABI 4). */
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                  int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+                  int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap);
 /* lpc_trace_run without waiting for the last iteration's kernels (the moves of
  * the next population's rows and of the measured record; the outputs above are
  * final when it returns): a caller that traces batch after batch lets the next
  * batch's launches queue behind them.  Every entry point that copies device data
  * to the host waits for them first; lpc_sync waits explicitly. */
 int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                        int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+                        int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap);
 /* lpc_trace_reset + lpc_trace_run_async in one call: the next batch of a caller
  * that re-traces the rays set with lpc_trace_set_rays (one host round trip less
  * between batches). */
 int lpc_trace_rerun_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                          int32_t *n_iter, int64_t *measured_count, double *mesh_power);
+                          int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap);
 /* ---- ray-sharded trace: one process per GPU ---------- */
 /* All-reduce (sum, in place) of n doubles over the ranks of a sharded trace;
  * every rank must receive the identical bits.  Returns 0 on success. */
@@ -205,9 +207,12 @@ typedef int (*lpc_allreduce_fn)(void *ctx, double *vals, int32_t n);
  * float64 sums: its rounding differs from a single device's tile-order sum
  * (and both from the reference's float32 sorted sum, :372), so a trace whose
  * power left lands within ~1e-12 relative of the threshold may stop one
- * iteration apart from a single-device trace.  A rank whose trace fails
- * locally still joins the exchange its peers wait in, with NaN values; a rank
- * that receives NaN sums fails with LPC_E_STATE ("a peer rank failed"). */
+ * iteration apart from a single-device trace.  Every exchange carries a
+ * failure flag in slot 0 (0 from a healthy rank): a rank whose trace fails
+ * locally still joins the exchange its peers wait in, with the flag set to 1;
+ * a rank whose summed flag is not 0 fails with LPC_E_STATE ("a peer rank
+ * failed").  The data slots may hold NaN (NaN powers are data: the trace goes
+ * on, as the reference's `NaN < thr` is false). */
 int lpc_set_allreduce(lpc_handle *h, lpc_allreduce_fn fn, void *ctx);
 /* The all-reduced per-iteration stats of the last lpc_trace_run(_async) (this
  * rank's own without a hook).  *n_iter = iterations; at most cap are copied. */
@@ -232,8 +237,9 @@ int lpc_shm_comm_close(lpc_shm_comm *comm);
 int lpc_sync(lpc_handle *h);
 /* Current population size. */
 int lpc_trace_population(lpc_handle *h, int64_t *n);
-/* Measured record so far: count and per-mesh measured power (double[mesh_count]). */
-int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_power);
+/* Measured record so far: count and per-mesh measured power (double[mesh_count]
+ * into a buffer of mesh_power_cap doubles; LPC_E_ARG when it is smaller). */
+int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_power, int32_t mesh_power_cap);
 /* Copy the measured record to host: pos4 (count,4), pow (count), mesh (count);
  * any pointer may be NULL. */
 int lpc_trace_fetch_measured(lpc_handle *h, float *pos4, float *pow, int32_t *mesh);

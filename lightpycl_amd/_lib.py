@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblpc.so")
 
 _lib = None
+ABI_VERSION = 4         # include/lpc.h LPC_ABI_VERSION
 
 
 class LpcError(RuntimeError):
@@ -67,9 +68,9 @@ _PROTOS = {
     "lpc_trace_set_rays": [_P, _I64, _P, _P, _P, _F32, _F32],
     "lpc_trace_reset": [_P],
     "lpc_trace_iterate": [_P, _P, _P, _P, _P, _P, _P],
-    "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P],
-    "lpc_trace_run_async": [_P, _I32, _F64, _P, _P, _P, _P],
-    "lpc_trace_rerun_async": [_P, _I32, _F64, _P, _P, _P, _P],
+    "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
+    "lpc_trace_run_async": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
+    "lpc_trace_rerun_async": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
     "lpc_sync": [_P],
     "lpc_trace_iterate_export": [_P, _P, _I32, _P],
     "lpc_trace_population_power": [_P, _P],
@@ -77,7 +78,7 @@ _PROTOS = {
     "lpc_host_free": [_P],
     "lpc_host_seq_sum_f32": [_P, _I64, _P],
     "lpc_trace_population": [_P, _P],
-    "lpc_trace_measured": [_P, _P, _P],
+    "lpc_trace_measured": [_P, _P, _P, _I32],
     "lpc_trace_fetch_measured": [_P, _P, _P, _P],
     "lpc_set_chunk": [_P, _I64],
     "lpc_project_hist": [_P, _INT, _I64, _P, _P, _P, _P, _P, _INT, _P, _INT, _F64, _P, _P, _P,
@@ -139,7 +140,7 @@ def load(path: str = LIB_PATH):
         fn.restype = ctypes.c_int
     L.lpc_last_error.argtypes = [_P]
     L.lpc_last_error.restype = ctypes.c_char_p
-    if L.lpc_abi_version() != 3:
+    if L.lpc_abi_version() != ABI_VERSION:
         raise LpcError("liblpc ABI version mismatch")
     _lib = L
     return L

@@ -294,15 +294,17 @@ class Engine:
         trace in one call (the bench's back-to-back batches)."""
         cap = max(int(iterations), 0)
         # output buffers and argument objects kept per (cap, mesh count): the library
-        # writes one power per mesh of the CURRENT scene into mp
+        # writes one power per mesh of the CURRENT scene into mp, and refuses a
+        # buffer below that count (its capacity travels with the call)
         key = (cap, int(self.mesh_count))
         bufs = self._run_bufs.get(key) if hasattr(self, "_run_bufs") else None
         if bufs is None:
             arr, k, c = (_lib.IterStats * max(cap, 1))(), ctypes.c_int32(0), ctypes.c_int64(0)
             mp = np.zeros(max(key[1], 1), np.float64)
-            bufs = (arr, k, c, mp, ctypes.byref(k), ctypes.byref(c), mp.ctypes.data_as(ctypes.c_void_p))
+            bufs = (arr, k, c, mp, ctypes.byref(k), ctypes.byref(c), mp.ctypes.data_as(ctypes.c_void_p),
+                    ctypes.c_int32(mp.size))
             self.__dict__.setdefault("_run_bufs", {})[key] = bufs
-        arr, k, c, mp, pk, pc, pmp = bufs
+        arr, k, c, mp, pk, pc, pmp, mcap = bufs
         # wait=False: lpc_trace_run_async (the outputs are final; the last rows may
         # still move on the device and the next batch's launches queue behind them)
         if reset and not wait:
@@ -311,7 +313,7 @@ class Engine:
             if reset:
                 self.reset()
             fn = self.L.lpc_trace_run if wait else self.L.lpc_trace_run_async
-        self._c(fn(self.h, cap, float(power_threshold), arr, pk, pc, pmp))
+        self._c(fn(self.h, cap, float(power_threshold), arr, pk, pc, pmp, mcap))
         # one copy of the stats block (the buffers are reused by the next call)
         return type(arr).from_buffer_copy(arr)[:k.value], (c.value, mp[: self.mesh_count].copy())
 
@@ -355,13 +357,13 @@ class Engine:
         """(count, per-mesh measured power float64[K])."""
         c = ctypes.c_int64(0)
         mp = np.zeros(max(self.mesh_count, 1), np.float64)
-        self._c(self.L.lpc_trace_measured(self.h, ctypes.byref(c), ptr(mp)))
+        self._c(self.L.lpc_trace_measured(self.h, ctypes.byref(c), ptr(mp), mp.size))
         return c.value, mp[: self.mesh_count]
 
     def fetch_measured(self):
         """Measured record: pos (Nm,4) float32, pwr (Nm,) float32, mesh (Nm,) int32."""
         c = ctypes.c_int64(0)
-        self._c(self.L.lpc_trace_measured(self.h, ctypes.byref(c), None))
+        self._c(self.L.lpc_trace_measured(self.h, ctypes.byref(c), None, 0))
         n = c.value
         pos = np.zeros((n, 4), np.float32)
         pw = np.zeros(n, np.float32)

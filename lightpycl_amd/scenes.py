@@ -161,5 +161,31 @@ def synthetic_dense(n=1_000_000, seed=7, iterations=16):
     return sc
 
 
+def cube_field(n=2000, seed=1, iterations=8, count=1100):
+    """Many meshes (a capability case, not a BASELINE config): a measure hemisphere
+    (r = 1000) plus `count` small cubes (12 triangles each) on a square grid at
+    z = 40 in front of a point source pointing +z, every 7th a mirror, the rest
+    refractive (IOR 1.5, every 5th dissipative).  Above 1 024 live mesh runs the
+    root tests run in batches of pieces; above 128 each packet takes >= 3 tasks."""
+    np.random.seed(seed)
+    oe = goe.optical_elements()
+    ms = oe.hemisphere(center=[0, 0, 0, 0], radius=1000.0)
+    ms.setMaterial(mat_type="measure")
+    meshes = [ms]
+    side = int(np.ceil(np.sqrt(count)))
+    for i in range(count):
+        cx = (i % side - (side - 1) / 2.0) * 2.5
+        cy = (i // side - (side - 1) / 2.0) * 2.5
+        m = oe.cube(center=(cx, cy, 40.0 + 0.3 * (i % 3), 0), size=[1.5, 1.5, 1.5, 0])
+        if i % 7 == 0:
+            m.setMaterial(mat_type="mirror")
+        else:
+            m.setMaterial(mat_type="refractive", IOR=1.5, dissipation=0.05 if i % 5 == 0 else 0.0)
+        meshes.append(m)
+    ls0 = lsrc.light_source(center=np.array([0, 0, 0, 0], dtype=np.float32), direction=(0, 0, 1),
+                            directivity=lambda x, y: np.cos(y), power=1.0, ray_count=n)
+    return SceneSpec("cube_field", [ls0], meshes, np.float32(2e3), iterations=iterations)
+
+
 BUILDERS = dict(parabolic=parabolic, lens=lens, eye=eye, cube=cube, nested_cubes=nested_cubes,
-                synthetic=synthetic, synthetic_dense=synthetic_dense)
+                synthetic=synthetic, synthetic_dense=synthetic_dense, cube_field=cube_field)

@@ -132,7 +132,7 @@ def test_c_abi_exports_every_header_symbol():
     L = _lib.load()
     for name in declared:
         assert getattr(L, name) is not None
-    assert L.lpc_abi_version() == 3
+    assert L.lpc_abi_version() == 4
 
 
 def test_c_abi_errors_without_device():
