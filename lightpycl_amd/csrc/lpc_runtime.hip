@@ -6,6 +6,7 @@
 #include "lpc_kernels.hip"
 #include "lpc.h"
 #include "lpc_comm.hpp"
+#include "lpc_build.hpp"
 #include <hip/hip_ext.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -352,214 +353,56 @@ static int pop_reserve(lpc_handle *h, Pop &P, int64_t n)
 static inline unsigned grid1(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
 
 // ---------------------------------------------------------------------------
-// scene records
-// Top-down partition of idx[0, n) for a subtree of capacity cap (4 * 2^k): split
-// at min(n, cap/2) along the longest axis of the centroids' bbox (nth_element),
-// recurse on both halves with cap/2, down to groups of 4.
-static void split_order(int32_t *idx, int64_t n, int64_t cap, const std::vector<double> &cen, int64_t leaf = 4)
-{
-    if (cap <= leaf || n <= 1) return;
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int64_t i = 0; i < n; ++i)
-        for (int k = 0; k < 3; ++k) {
-            const double c = cen[3 * (size_t)idx[i] + k];
-            if (std::isfinite(c)) { lo[k] = std::min(lo[k], c); hi[k] = std::max(hi[k], c); }
-        }
-    int ax = 0;
-    for (int k = 1; k < 3; ++k)
-        if (hi[k] - lo[k] > hi[ax] - lo[ax]) ax = k;
-    const int64_t half = std::min(n, cap / 2);
-    if (half < n)
-        std::nth_element(idx, idx + half, idx + n, [&](int32_t a, int32_t b) {
-            const double ca = cen[3 * (size_t)a + ax], cb = cen[3 * (size_t)b + ax];
-            return ca < cb || (ca == cb && a < b);
-        });
-    split_order(idx, half, cap / 2, cen, leaf);
-    split_order(idx + half, n - half, cap / 2, cen, leaf);
-}
-
-// Per mesh run: a 4-wide sphere hierarchy built bottom-up over its triangles in
-// a top-down median-split order (split_order; bottom nodes hold up to 4
-// triangles); every
-// node's test is node_record() of ALL triangles below it (their vertices), so
-// the slack does not compound from level to level.  Triangles whose sphere test is degenerate
-// ("always", B >= 0.5) go to the run's sliver list (line filter, sliver_params)
-// instead; triangles that can never be hit are dropped.  Results do not depend
-// on the order (ties are resolved by triangle index).
-static FiltRec test_rec(float cx, float cy, float cz, float negB, float negA)
-{
-    FiltRec r;
-    r.cx = cx; r.cy = cy; r.cz = cz; r.negB = negB; r.negA = negA; r.idx = -1; r.pad0 = r.pad1 = 0;
-    return r;
-}
-
+// scene records: lpc_build.hpp builds them on the host (runs on host threads)
 static void drop_piece_tables(lpc_handle *h)
 {
     for (auto &kv : h->ptabs) { dfree(kv.second.pieces); dfree(kv.second.spieces); dfree(kv.second.groups); }
     h->ptabs.clear();
 }
 
+static int host_threads();
+
+// Per mesh run: an 8-wide sphere hierarchy over its triangles in a top-down
+// median-split order, every node's test node_record() of ALL triangles below it
+// (so the slack does not compound from level to level); triangles whose sphere
+// test is degenerate (slivers) or far wider than the triangle (thin) go to the
+// run's line-filter list; triangles that can never be hit are dropped.  Results
+// do not depend on the order (ties are resolved by triangle index).
 static int build_records(lpc_handle *h)
 {
     drop_piece_tables(h);   // pieces index the records built here
-    const int W = 8;                                // hierarchy width (4 measured slower, round 1)
-    const size_t node_bytes = sizeof(Node8);
-    std::vector<uint8_t> nodes;                     // NodeW<W> records
-    int32_t n_nodes = 0;
-    std::vector<SliverRec> slivers;
-    h->run_levels.clear();
-    h->node_self.clear();
-    h->run_slo.clear(); h->run_shi.clear();
-    h->sliver_dmin_host.clear();
-    h->n_slivers = 0;
-    h->n_thin = 0;
-    const FiltRec never = test_rec(0.0f, 0.0f, 0.0f, 0.0f, INFINITY);
-    auto vptr = [&](int32_t t, int v) -> const float * {
-        return v == 0 ? &h->hv0[4 * (size_t)t] : v == 1 ? &h->hv1[4 * (size_t)t] : &h->hv2[4 * (size_t)t];
-    };
-    for (size_t r = 0; r < h->run_lo.size(); ++r) {
-        const int32_t lo = h->run_lo[r], cnt_all = h->run_hi[r] - lo;
-        std::vector<FiltRec> fr;                     // hierarchy triangles
-        std::vector<double> cen;
-        std::vector<int32_t> sl;
-        for (int32_t i = 0; i < cnt_all; ++i) {
-            const int32_t t = lo + i;
-            const float *V0 = vptr(t, 0), *V1 = vptr(t, 1), *V2 = vptr(t, 2);
-            const FiltRec f = filter_record(V0, V1, V2, t, h->dcap, h->scene_scale);
-            if (f.negA == INFINITY) continue;                     // never a candidate
-            if (f.negB < -1e29f) { sl.push_back(t); continue; }
-            // thin: the line filter about its longer edge (k_slivers) bounds it better
-            if (thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale, kThin)) {
-                sl.push_back(t);
-                ++h->n_thin;
-                continue;
-            }
-            fr.push_back(f);
-            for (int k = 0; k < 3; ++k) cen.push_back(((double)V0[k] + V1[k] + V2[k]) / 3.0);
-        }
-        h->run_slo.push_back((int32_t)slivers.size());
-        // slivers ordered by dmin, so a 64-sliver piece holds similar ones
-        std::vector<std::pair<float, int32_t>> sld;
-        for (int32_t t32 : sl) sld.push_back({sliver_dmin(vptr(t32, 0), vptr(t32, 1), vptr(t32, 2)), t32});
-        std::stable_sort(sld.begin(), sld.end(),
-                         [](const std::pair<float, int32_t> &x, const std::pair<float, int32_t> &y) {
-                             return x.first < y.first;
-                         });
-        for (size_t q = 0; q < sld.size(); ++q) sl[q] = sld[q].second;
-        for (int32_t t32 : sl) {
-            const float *V0 = vptr(t32, 0), *V1 = vptr(t32, 1), *V2 = vptr(t32, 2);
-            SliverRec S;
-            memset(&S, 0, sizeof(S));
-            S.v0x = V0[0]; S.v0y = V0[1]; S.v0z = V0[2];
-            // a thin triangle whose longer edge is E1 filters about E1 (e2 holds it)
-            const FiltRec f = filter_record(V0, V1, V2, t32, h->dcap, h->scene_scale);
-            const int ax = f.negB < -1e29f ? 1 : thin_axis(V0, V1, V2, f.cx, f.cy, f.cz, h->scene_scale, kThin);
-            S.ax1 = ax == 2 ? 1 : 0;
-            const float e1[3] = {V1[0] - V0[0], V1[1] - V0[1], V1[2] - V0[2]};
-            const float e2[3] = {V2[0] - V0[0], V2[1] - V0[1], V2[2] - V0[2]};
-            const float *ea = S.ax1 ? e1 : e2, *eb = S.ax1 ? e2 : e1;
-            S.e2x = ea[0]; S.e2y = ea[1]; S.e2z = ea[2];
-            S.e1x = eb[0]; S.e1y = eb[1]; S.e1z = eb[2];
-            sliver_params_axis(V0, V1, V2, S.ax1, &S.a, &S.b);
-            S.idx = t32;
-            S.dmin = sliver_dmin(V0, V1, V2);
-            slivers.push_back(S);
-        }
-        h->run_shi.push_back((int32_t)slivers.size());
-        h->n_slivers += (int64_t)sl.size();
-        h->run_levels.push_back(std::vector<int32_t>());
-        // hierarchy entries: the triangles (each with its test, child ref,
-        // centroid and triangle list)
-        struct Entry { FiltRec t; int32_t ref; double c[3]; int32_t t0, t1; };
-        std::vector<Entry> E;
-        std::vector<int32_t> etri;                   // triangle ids of the entries, [t0, t1) each
-        for (size_t i = 0; i < fr.size(); ++i) {
-            Entry e;
-            e.t = fr[i]; e.ref = ~fr[i].idx;
-            for (int k = 0; k < 3; ++k) e.c[k] = cen[3 * i + k];
-            e.t0 = (int32_t)etri.size(); etri.push_back(fr[i].idx); e.t1 = (int32_t)etri.size();
-            E.push_back(e);
-        }
-        const int32_t cnt = (int32_t)E.size();
-        if (cnt == 0) continue;
-        // top-down order: every aligned group of 4^k entries is one median-split
-        // cluster, so the bottom-up 4-wide grouping below reproduces that tree
-        std::vector<double> ecen((size_t)cnt * 3);
-        for (int32_t i = 0; i < cnt; ++i)
-            for (int k = 0; k < 3; ++k) ecen[3 * (size_t)i + k] = E[(size_t)i].c[k];
-        std::vector<int32_t> perm_t((size_t)cnt);
-        for (int32_t i = 0; i < cnt; ++i) perm_t[(size_t)i] = i;
-        int64_t cap = W;
-        while (cap < cnt) cap *= W;
-        split_order(perm_t.data(), cnt, cap, ecen, W);
-        // every hierarchy entry covers a contiguous range of ordered entries; its
-        // test is node_record() of all their triangles
-        std::vector<const float *> tv;
-        std::vector<int32_t> eo((size_t)cnt + 1, 0);
-        for (int32_t i = 0; i < cnt; ++i) {
-            const Entry &e = E[(size_t)perm_t[(size_t)i]];
-            for (int32_t q = e.t0; q < e.t1; ++q)
-                for (int v = 0; v < 3; ++v) tv.push_back(vptr(etri[(size_t)q], v));
-            eo[(size_t)i + 1] = (int32_t)(tv.size() / 3);
-        }
-        auto range_test = [&](int32_t a, int32_t b) {
-            FiltRec t = never;
-            node_record(&tv[3 * (size_t)eo[(size_t)a]], eo[(size_t)b] - eo[(size_t)a], h->scene_scale, &t.cx, &t.cy,
-                        &t.cz, &t.negB, &t.negA);
-            return t;
-        };
-        struct Ent { FiltRec t; int32_t ref, a, b; };
-        std::vector<Ent> ent((size_t)cnt);
-        for (int32_t a = 0; a < cnt; ++a) {
-            const Entry &e = E[(size_t)perm_t[(size_t)a]];
-            ent[(size_t)a] = {e.t, e.ref, a, a + 1};
-        }
-        std::vector<std::pair<int32_t, int32_t>> levels;   // (first node, count), bottom up
-        do {
-            std::vector<Ent> up;
-            const int32_t first = n_nodes;
-            for (size_t i = 0; i < ent.size(); i += (size_t)W) {
-                // NodeW<W> layout: cx cy cz negB negA [W] floats, ref [W], pad
-                std::vector<uint32_t> N(node_bytes / 4, 0u);
-                for (int k = 0; k < W; ++k) {
-                    const bool use = i + k < ent.size();
-                    const FiltRec &m = use ? ent[i + k].t : never;
-                    const float f5[5] = {m.cx, m.cy, m.cz, m.negB, m.negA};
-                    for (int q = 0; q < 5; ++q) memcpy(&N[(size_t)q * W + k], &f5[q], 4);
-                    const int32_t ref = use ? ent[i + k].ref : ~0;
-                    memcpy(&N[(size_t)5 * W + k], &ref, 4);
-                }
-                const int32_t a = ent[i].a, b = ent[std::min(i + (size_t)W - 1, ent.size() - 1)].b;
-                const FiltRec self = range_test(a, b);
-                up.push_back({self, n_nodes, a, b});
-                nodes.insert(nodes.end(), (const uint8_t *)N.data(), (const uint8_t *)N.data() + node_bytes);
-                ++n_nodes;
-                h->node_self.push_back(self);
-            }
-            levels.push_back({first, (int32_t)up.size()});
-            ent.swap(up);
-        } while (ent.size() > 1);
-        // W-wide: at most W - 1 siblings wait per level on a wave's stack
-        if ((W - 1) * (int)levels.size() + 1 > LPC_STACK) return set_err(h, LPC_E_ARG, "mesh hierarchy too deep");
-        for (auto it = levels.rbegin(); it != levels.rend(); ++it) {
-            h->run_levels.back().push_back(it->first);
-            h->run_levels.back().push_back(it->second);
-        }
-    }
+    SceneBuildIn in;
+    in.v0 = h->hv0.data(); in.v1 = h->hv1.data(); in.v2 = h->hv2.data();
+    in.run_lo = h->run_lo.data(); in.run_hi = h->run_hi.data(); in.nr = h->run_lo.size();
+    in.dcap = h->dcap; in.scene_scale = h->scene_scale; in.thin_k = kThin; in.stack_max = LPC_STACK;
+    SceneBuildOut out;
+    const double t0 = h->host_prof ? host_us() : 0.0;
+    const std::string err = build_scene_records(in, out, host_threads());
+    if (!err.empty()) return set_err(h, LPC_E_ARG, err);
+    if (h->host_prof)
+        fprintf(stderr, "[lpc host] scene records %.1f us (%zu nodes, %zu slivers, %d threads)\n", host_us() - t0,
+                out.nodes.size(), out.slivers.size(), host_threads());
+    h->run_levels.swap(out.run_levels);
+    h->node_self.swap(out.node_self);
+    h->run_slo.swap(out.run_slo);
+    h->run_shi.swap(out.run_shi);
+    h->n_slivers = out.n_slivers;
+    h->n_thin = out.n_thin;
     // spare records so no buffer is empty
-    if (n_nodes == 0) { nodes.assign(node_bytes, 0); n_nodes = 1; }
-    if (slivers.empty()) {
+    if (out.nodes.empty()) { Node8 z; memset(&z, 0, sizeof(z)); out.nodes.push_back(z); }
+    if (out.slivers.empty()) {
         SliverRec ss;
         memset(&ss, 0, sizeof(ss));
         ss.a = NAN; ss.idx = -1; ss.dmin = INFINITY;
-        slivers.push_back(ss);
+        out.slivers.push_back(ss);
     }
-    for (const SliverRec &q : slivers) h->sliver_dmin_host.push_back(q.dmin);
-    h->Mpad = n_nodes;
-    RETIF(dalloc(h, h->d_nodes, nodes.size()));
-    RETIF(dalloc(h, h->d_srec, slivers.size() * sizeof(SliverRec)));
-    HIPCHK(h, hipMemcpy(h->d_nodes.p, nodes.data(), nodes.size(), hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->d_srec.p, slivers.data(), slivers.size() * sizeof(SliverRec),
+    h->sliver_dmin_host.clear();
+    for (const SliverRec &q : out.slivers) h->sliver_dmin_host.push_back(q.dmin);
+    h->Mpad = (int32_t)out.nodes.size();
+    RETIF(dalloc(h, h->d_nodes, out.nodes.size() * sizeof(Node8)));
+    RETIF(dalloc(h, h->d_srec, out.slivers.size() * sizeof(SliverRec)));
+    HIPCHK(h, hipMemcpy(h->d_nodes.p, out.nodes.data(), out.nodes.size() * sizeof(Node8), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_srec.p, out.slivers.data(), out.slivers.size() * sizeof(SliverRec),
                         hipMemcpyHostToDevice));
     return 0;
 }
@@ -925,24 +768,47 @@ static int check_qerr(lpc_handle *h)
 }
 
 // The root-item queue of a launch of n rays: shard capacity, buffer, arguments.
+// k_roots_s holds at most 64 LPC_ROOTS_TASKS pieces in LDS: a table with more
+// (more than 1 024 live mesh runs, cut at their roots, no gate) is tested in
+// batches of that many pieces, one k_roots_s launch each, into the same queue.
+#define LPC_ROOTS_BATCH (64 * LPC_ROOTS_TASKS)
+struct RootsBatch {
+    int S, pb;
+    int64_t blocks, vblocks;
+};
+static RootsBatch roots_batch(int64_t npk, const DevSize *ds, int32_t npieces)
+{
+    RootsBatch b;
+    b.S = (int)((npieces + 63) / 64);           // S tasks per packet (npieces <= 64 S)
+    b.pb = b.S >= 3 ? 1 : b.S == 2 ? 2 : kRootsPerBlock;   // pb packets per block
+    b.blocks = (npk + b.pb - 1) / b.pb;
+    b.vblocks = !ds ? b.blocks : (((ds->bound + 63) / 64) + b.pb - 1) / b.pb;
+    return b;
+}
 struct QueueShape {
     int64_t npk, rs_blocks;
     int rs_S, rs_pb;
+    int nbatch;                                 // k_roots_s launches (pieces in batches of LPC_ROOTS_BATCH)
 };
 static int queue_args(lpc_handle *h, int64_t n, const PieceTable *pt, const DevSize *ds, QueueArgs *Qo,
                       QueueShape *sh)
 {
     // device-sized (ds): n is the expected size (grids), the bound sizes the shards
     const int64_t npk = (n + 63) / 64;
-    // k_roots_s: S tasks per packet (npieces <= 64 S), pb packets per block
-    const int rs_S = (int)((pt->npieces + 63) / 64);
-    if (rs_S > LPC_ROOTS_TASKS) return set_err(h, LPC_E_STATE, "internal: more pieces than k_roots_s holds");
-    const int rs_pb = rs_S >= 3 ? 1 : rs_S == 2 ? 2 : kRootsPerBlock;
-    const int64_t rs_blocks = (npk + rs_pb - 1) / rs_pb;
-    const int64_t rs_vblocks = !ds ? rs_blocks : (((ds->bound + 63) / 64) + rs_pb - 1) / rs_pb;
-    // per shard: at most its blocks' packets x pieces items (k_roots_s / k_gather_roots
-    // flag an overflow through Q.err instead of dropping items silently)
-    int64_t rcap = ((rs_vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * rs_pb * (int64_t)pt->npieces;
+    const int nbatch = std::max(1, (int)((pt->npieces + LPC_ROOTS_BATCH - 1) / LPC_ROOTS_BATCH));
+    if (nbatch > 1 && pt->ngroups > 0) return set_err(h, LPC_E_STATE, "internal: gated pieces in several batches");
+    const RootsBatch b0 = roots_batch(npk, ds, std::min<int32_t>(pt->npieces, LPC_ROOTS_BATCH));
+    // per shard: at most its blocks' packets x pieces items, summed over the batches
+    // (k_roots_s / k_gather_roots flag an overflow through Q.err instead of dropping
+    // items silently)
+    int64_t rcap = 0;
+    for (int k = 0; k < nbatch; ++k) {
+        const int32_t np = std::min<int32_t>(pt->npieces - k * LPC_ROOTS_BATCH, LPC_ROOTS_BATCH);
+        const RootsBatch b = roots_batch(npk, ds, np);
+        rcap += ((b.vblocks + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * b.pb * (int64_t)np;
+    }
+    const int rs_S = b0.S, rs_pb = b0.pb;
+    const int64_t rs_blocks = b0.blocks;
     // k_gather_roots: 16 packets per block
     rcap = std::max<int64_t>(rcap, ((((npk + 15) / 16) + LPC_Q_CSHARDS - 1) / LPC_Q_CSHARDS) * 16 *
                                        (int64_t)pt->npieces);
@@ -955,6 +821,7 @@ static int queue_args(lpc_handle *h, int64_t n, const PieceTable *pt, const DevS
     Q.rcap = (uint32_t)rcap;
     *Qo = Q;
     sh->npk = npk; sh->rs_blocks = rs_blocks; sh->rs_S = rs_S; sh->rs_pb = rs_pb;
+    sh->nbatch = nbatch;
     return 0;
 }
 
@@ -974,16 +841,17 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
         fprintf(stderr, "[lpc host] roots: n %lld packets %lld pieces %d groups %d S %d pb %d blocks %lld rcap %lld\n",
                 (long long)n, (long long)sh.npk, (int)pt->npieces, (int)pt->ngroups, sh.rs_S, sh.rs_pb,
                 (long long)sh.rs_blocks, (long long)Q.rcap);
-    if (!roots_done) {
-        const dim3 rg((unsigned)std::max<int64_t>(sh.rs_blocks, 1));
+    for (int k = 0; !roots_done && k < sh.nbatch; ++k) {
+        const int32_t np = std::min<int32_t>(pt->npieces - k * LPC_ROOTS_BATCH, LPC_ROOTS_BATCH);
+        const RootsBatch b = roots_batch(sh.npk, ds, np);
+        const Piece *pc = (const Piece *)pt->pieces.p + (size_t)k * LPC_ROOTS_BATCH;
+        const dim3 rg((unsigned)std::max<int64_t>(b.blocks, 1));
         if (h->half_roots)
-            hipLaunchKernelGGL(k_roots_s<true>, rg, dim3(256), 0, h->stream, in, rs, n, (const Piece *)pt->pieces.p,
-                               (int)pt->npieces, (const Piece *)pt->groups.p, (int)pt->ngroups, Q, sh.rs_S, sh.rs_pb,
-                               ds ? ds->nd : nullptr);
+            hipLaunchKernelGGL(k_roots_s<true>, rg, dim3(256), 0, h->stream, in, rs, n, pc, (int)np,
+                               (const Piece *)pt->groups.p, (int)pt->ngroups, Q, b.S, b.pb, ds ? ds->nd : nullptr);
         else
-            hipLaunchKernelGGL(k_roots_s<false>, rg, dim3(256), 0, h->stream, in, rs, n, (const Piece *)pt->pieces.p,
-                               (int)pt->npieces, (const Piece *)pt->groups.p, (int)pt->ngroups, Q, sh.rs_S, sh.rs_pb,
-                               ds ? ds->nd : nullptr);
+            hipLaunchKernelGGL(k_roots_s<false>, rg, dim3(256), 0, h->stream, in, rs, n, pc, (int)np,
+                               (const Piece *)pt->groups.p, (int)pt->ngroups, Q, b.S, b.pb, ds ? ds->nd : nullptr);
     }
     // merged sliver tests (LPC_SLIVER_MERGE): the packet bounds before the walk,
     // on this stream; the walk's waves take the (packet group, piece) units
@@ -1056,12 +924,11 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     PieceTable *pt;
     int32_t g = q_level(h, n, traced && h->pop_traced);
     RETIF(piece_table(h, &pt, g));
-    while (pt->npieces > 64 * LPC_ROOTS_TASKS && g > 1) {
+    // (a table of more than 1 024 run roots, g = 1, goes to k_roots_s in batches)
+    while (pt->npieces > LPC_ROOTS_BATCH && g > 1) {
         g = std::max(1, g / 8);
         RETIF(piece_table(h, &pt, g));
     }
-    if (pt->npieces > 64 * LPC_ROOTS_TASKS)
-        return set_err(h, LPC_E_ARG, "scene has more than 1024 mesh runs (k_roots_s limit)");
     const float eps = 0.000001f * max_ray_len;   // .cl:245, single-precision constant
     unsigned long long *skey = (unsigned long long *)h->w_key.p;
     int32_t *scnt = (int32_t *)h->w_sc.p;
@@ -1478,8 +1345,9 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     // items node ids in 28, LPC_Q_MAX_NODES)
     if (tri_count >= (1 << 26))
         return set_err(h, LPC_E_ARG, "scene has too many triangles (limit 2^26 - 1)");
-    if (mesh_count > 64 * LPC_ROOTS_TASKS)   // k_roots_s holds at most 1024 run roots
-        return set_err(h, LPC_E_ARG, "scene has too many meshes (limit 1024)");
+    // the root items carry a mesh's scratch slot in 12 bits (q_item)
+    if (mesh_count > LPC_Q_MAX_SLOTS + 1)
+        return set_err(h, LPC_E_ARG, "scene has too many meshes (limit " + std::to_string(LPC_Q_MAX_SLOTS + 1) + ")");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const int32_t M = tri_count, K = mesh_count;
@@ -1515,12 +1383,15 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     h->meas_meshes.clear();
     for (int32_t j = 0; j < K; ++j) if (mat_type[j] == 3) h->meas_meshes.push_back(j);
     // passive materials: the children of a ray never carry more power than it
-    // (refractive: R, T = 1 - R in [0, 1] for positive indices, .cl:313-326;
-    // mirror: P R with R <= 1, .cl:443; dissipation only attenuates, .cl:385-394)
+    // (refractive: R, T = 1 - R in [0, 1] for finite positive indices,
+    // .cl:313-326; mirror: P R with 0 <= R <= 1, .cl:443 -- a negative R flips the
+    // sign, so a population's summed power could grow; dissipation only
+    // attenuates, .cl:385-394)
     h->mat_passive = true;
     for (int32_t j = 0; j < K; ++j) {
-        if ((mat_type[j] == 0 || mat_type[j] == 4) && !(ior[j] > 0.0f)) h->mat_passive = false;
-        if (mat_type[j] == 1 && !(refl[j] <= 1.0f)) h->mat_passive = false;
+        if ((mat_type[j] == 0 || mat_type[j] == 4) && !(ior[j] > 0.0f && std::isfinite(ior[j])))
+            h->mat_passive = false;
+        if (mat_type[j] == 1 && !(refl[j] >= 0.0f && refl[j] <= 1.0f)) h->mat_passive = false;
     }
     // exact records and vertices
     std::vector<ExactRec> xr((size_t)M);
@@ -1930,7 +1801,8 @@ static int xchg_stats(lpc_handle *h, const lpc_iter_stats &S, lpc_iter_stats *G)
 }
 
 static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait);
+                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap,
+                     bool wait);
 
 // A rank that fails locally still takes part in the exchange its peers wait in,
 // with the failure flag (slot 0) set: they see it in the sums and fail at once
@@ -1949,22 +1821,27 @@ static void xchg_poison(lpc_handle *h, int32_t n)
 }
 
 int lpc_trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                  int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+                  int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap)
 {
-    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, true);
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, mesh_power_cap,
+                     true);
 }
 
 int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                        int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+                        int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap)
 {
-    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, false);
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, mesh_power_cap,
+                     false);
 }
 
 int lpc_trace_rerun_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                          int32_t *n_iter, int64_t *measured_count, double *mesh_power)
+                          int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap)
 {
+    if (h && mesh_power && mesh_power_cap < h->K)       // before the reset: nothing changed on error
+        return set_err(h, LPC_E_ARG, "trace: mesh_power capacity below the scene's mesh count");
     RETIF(lpc_trace_reset(h));
-    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, false);
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, mesh_power_cap,
+                     false);
 }
 
 int lpc_set_allreduce(lpc_handle *h, lpc_allreduce_fn fn, void *ctx)
@@ -2092,6 +1969,7 @@ struct Pending {
     bool ds = false;            // device-sized (speculative)
     bool empty = false;         // nothing to do (n_in 0, host-sized)
     int64_t n_bound = 0;        // device-sized: population bound
+    double thr = -INFINITY;     // fused: the stop threshold its k_stage_move applied (ds_thr)
     // host state before its enqueue (undo of a discarded speculative iteration)
     bool was_init = false, was_traced = false, was_emitted = false, was_pbox = false;
 };
@@ -2228,6 +2106,7 @@ static int iter_enqueue(lpc_handle *h, float *out_origin4, float *out_dest4, flo
     if (fused && C < N) RETIF(dalloc(h, h->d_cbase, 8 * sizeof(unsigned long long)));
     if (ds && !(fused && early)) return set_err(h, LPC_E_STATE, "internal: device-sized iteration off the fused path");
     P->fused = fused;
+    P->thr = h->ds_thr;
     const size_t Cs = (size_t)h->ws_rays;
     const int64_t ntc = (int64_t)((Cs + LPC_ST_TILE - 1) / LPC_ST_TILE);   // staging tile arrays' stride
     IterCtl *ctl = (IterCtl *)h->d_ctl.p;
@@ -2547,10 +2426,15 @@ static bool ds_ok(const lpc_handle *h, int64_t bound)
 // host's rules; an iteration the trace turns out not to need runs empty and is
 // dropped (iter_discard); a Dcap overflow (records rebuilt) re-runs it host-sized.
 static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
-                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, bool wait)
+                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap,
+                     bool wait)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
     if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
+    // mesh_power receives one double per mesh of the CURRENT scene: a buffer sized
+    // for an earlier scene with fewer meshes is refused, not overrun
+    if (mesh_power && mesh_power_cap < h->K)
+        return set_err(h, LPC_E_ARG, "trace: mesh_power capacity below the scene's mesh count");
     if (!h->traced_ready) return set_err(h, LPC_E_STATE, "trace_run before trace_set_rays");
     if (h->host_prof)                           // the caller's time between traces
         fprintf(stderr, "[lpc host] trace enter  since last %.1f us\n", host_us() - h->host_last);
@@ -2574,7 +2458,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     // other ranks' power left after the last exchanged iteration j bounds theirs
     // at every later iteration (slack for the float32 children sums), and this
     // rank's power below threshold - that bound ends the global trace too.
-    const bool mono = h->xchg && h->mat_passive && h->pow_nonneg && h->ior_env > 0.0f;
+    const bool mono = h->xchg && h->mat_passive && h->pow_nonneg && h->ior_env > 0.0f && std::isfinite(h->ior_env);
     double others = INFINITY;           // upper bound of the other ranks' power left (last exchange)
     int32_t others_it = -1;
     auto local_thr = [&](int32_t it) {  // k_stage_move's stop threshold of iteration `it`
@@ -2584,6 +2468,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
     };
     int rc = 0;
     bool exchanged = false;             // rc came from the exchange itself (no poison owed)
+    int32_t post_fail = -1;             // failed after this iteration's exchange: the shape the peers wait in next
     Pending cur, nxt;
     bool have_cur = false, have_nxt = false;
     for (int32_t i = 0; i < max_iter; ++i) {
@@ -2613,6 +2498,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
             }
         }
         lpc_iter_stats S;
+        const double cur_thr = cur.thr;     // the stop rule cur's k_stage_move sized nxt with
         rc = iter_collect(h, cur, nullptr, &S);
         have_cur = false;
         if (rc) break;
@@ -2640,12 +2526,20 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
                 // rebuild its measured power must not count either
                 iter_discard(h, nxt);
                 have_nxt = false;
-                if ((h->xchg || rebuilt) && (rc = restore_mrun(h))) break;   // the peers get the poison below
-            } else if (S.n_reflect + S.n_refract > nxt.n_bound) {
-                // more children than it was sized for: it ran empty on the device;
-                // the next pass of the loop runs the iteration host-sized
+                if ((h->xchg || rebuilt) && (rc = restore_mrun(h))) {
+                    // this iteration's exchange is done: the peers wait next in
+                    // the trace-end sums (stop) or the next iteration's stats
+                    post_fail = stop ? ((measured_count || mesh_power) ? h->K + 2 : 0) : LPC_XCHG_STATS;
+                    break;
+                }
+            } else if (S.n_reflect + S.n_refract > nxt.n_bound || S.power_next < cur_thr) {
+                // more children than it was sized for, or this device's stop rule
+                // fired where the trace goes on (a sharded rank's local bound,
+                // should its premise fail): it ran empty on the device; the next
+                // pass of the loop runs the iteration host-sized
                 iter_discard(h, nxt);
                 have_nxt = false;
+                if (h->xchg && (rc = restore_mrun(h))) { post_fail = LPC_XCHG_STATS; break; }
             } else {
                 nxt.n_in = S.n_reflect + S.n_refract;           // this rank's population
                 cur = nxt;
@@ -2660,7 +2554,10 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         (void)hipStreamSynchronize(h->stream);
         iter_discard(h, cur);
     }
-    if (rc && !exchanged) xchg_poison(h, LPC_XCHG_STATS);               // the peers wait in this iteration's exchange
+    if (rc && !exchanged) {
+        if (post_fail < 0) xchg_poison(h, LPC_XCHG_STATS);               // the peers wait in this iteration's exchange
+        else if (post_fail > 0) xchg_poison(h, post_fail);
+    }
     RETIF(rc);
     // this trace's populations (relative to the first) predict the next trace's
     if (n0 > 0) {
@@ -2672,7 +2569,7 @@ static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lp
         // [failure flag, per-mesh power (K), measured count]
         int64_t c = 0;
         std::vector<double> mp((size_t)h->K + 2, 0.0);
-        if ((rc = lpc_trace_measured(h, &c, mp.data() + 1))) {
+        if ((rc = lpc_trace_measured(h, &c, mp.data() + 1, h->K))) {
             xchg_poison(h, h->K + 2);
             return rc;
         }
@@ -2721,9 +2618,11 @@ static int mesh_power(lpc_handle *h, double *out)
     return 0;
 }
 
-int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_pow)
+int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_pow, int32_t mesh_pow_cap)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (mesh_pow && mesh_pow_cap < h->K)
+        return set_err(h, LPC_E_ARG, "trace_measured: mesh_power capacity below the scene's mesh count");
     HIPCHK(h, hipSetDevice(h->device));
     if (count) *count = h->m_total;
     if (mesh_pow) RETIF(mesh_power(h, mesh_pow));
