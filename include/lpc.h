@@ -194,6 +194,26 @@ int lpc_trace_run_async(lpc_handle *h, int32_t max_iter, double power_threshold,
  * between batches). */
 int lpc_trace_rerun_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
                           int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap);
+/* ---- streamed batches of new rays (round 6) ------------------------------- */
+/* The reference uploads each partition's rays inside its loop
+ * (iterative_tracer.py:280-284) and its examples trace batch after batch of new
+ * sources.  lpc_trace_stage_rays queues the next batch (at most two staged): a
+ * helper thread copies the caller's (n,4) rows and power into pinned staging and
+ * DMAs them to the device on a copy stream, with the emitted rays' analysis,
+ * while the handle traces the batch before it.  The caller's arrays must stay
+ * valid and unchanged until the lpc_trace_run_staged_async that traces the batch
+ * returns.  lpc_trace_run_staged_async makes the oldest staged batch the emitted
+ * rays (as lpc_trace_set_rays does, without the host copy inside the call) and
+ * runs lpc_trace_run_async on it; its first kernels queue behind the previous
+ * trace's last ones.  The pipelined caller stages batch k + 1, then traces batch
+ * k.  Batches may be staged before a scene is uploaded (the drop-in stages its
+ * rays before it builds the scene records) and survive a scene upload. */
+int lpc_trace_stage_rays(lpc_handle *h, int64_t n, const float *origin4, const float *dir4, const float *pow,
+                         float max_ray_len, float ior_env);
+int lpc_trace_run_staged_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                               int32_t *n_iter, int64_t *measured_count, double *mesh_power,
+                               int32_t mesh_power_cap);
+
 /* ---- ray-sharded trace: one process per GPU ---------- */
 /* All-reduce (sum, in place) of n doubles over the ranks of a sharded trace;
  * every rank must receive the identical bits.  Returns 0 on success. */

@@ -71,6 +71,8 @@ _PROTOS = {
     "lpc_trace_run": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
     "lpc_trace_run_async": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
     "lpc_trace_rerun_async": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
+    "lpc_trace_stage_rays": [_P, _I64, _P, _P, _P, _F32, _F32],
+    "lpc_trace_run_staged_async": [_P, _I32, _F64, _P, _P, _P, _P, _I32],
     "lpc_sync": [_P],
     "lpc_trace_iterate_export": [_P, _P, _I32, _P],
     "lpc_trace_population_power": [_P, _P],

@@ -40,6 +40,8 @@ struct SceneBuildOut {
     std::vector<std::vector<int32_t>> run_levels;   // per run: (first node, count) per level, top down
     std::vector<FiltRec> node_self;                 // per node: its own test (node_record of all below)
     std::vector<int32_t> run_slo, run_shi;          // per run: its slivers [slo, shi)
+    std::vector<int32_t> xorder;                    // per hierarchy position: the triangle (exact records
+                                                    //   in leaf order; a leaf child's ref is ~position)
     std::vector<float> sliver_dmin;                 // per sliver record
     int64_t n_slivers = 0, n_thin = 0;
 };
@@ -87,6 +89,7 @@ struct RunOut {
     std::vector<FiltRec> self;
     std::vector<SliverRec> sl;
     std::vector<std::pair<int32_t, int32_t>> levels;   // (first local node, count), bottom up
+    std::vector<int32_t> order;         // the run's hierarchy triangles in leaf order (local positions)
     int64_t n_thin = 0;
     bool too_deep = false;
 };
@@ -202,9 +205,11 @@ static inline void build_run(const SceneBuildIn &in, size_t r, RunOut &out)
     };
     struct Ent { FiltRec t; int32_t ref, a, b; Agg g; };
     std::vector<Ent> ent((size_t)cnt);
+    out.order.resize((size_t)cnt);
     for (int32_t a = 0; a < cnt; ++a) {
         const FiltRec &f = fr[(size_t)perm[(size_t)a]];
-        ent[(size_t)a] = {f, ~f.idx, a, a + 1, tagg[(size_t)a]};
+        ent[(size_t)a] = {f, ~a, a, a + 1, tagg[(size_t)a]};      // a leaf child: ~ its (local) position
+        out.order[(size_t)a] = f.idx;
     }
     do {
         std::vector<Ent> up;
@@ -274,14 +279,18 @@ static inline std::string build_scene_records(const SceneBuildIn &in, SceneBuild
         detail::RunOut &R = runs[r];
         if (R.too_deep) return "mesh hierarchy too deep";
         const int32_t base = (int32_t)out.nodes.size();
+        const int32_t pbase = (int32_t)out.xorder.size();
+        out.xorder.insert(out.xorder.end(), R.order.begin(), R.order.end());
         out.run_slo.push_back((int32_t)out.slivers.size());
         out.slivers.insert(out.slivers.end(), R.sl.begin(), R.sl.end());
         out.run_shi.push_back((int32_t)out.slivers.size());
         out.n_slivers += (int64_t)R.sl.size();
         out.n_thin += R.n_thin;
         for (Node8 &N : R.nodes)
-            for (int k = 0; k < 8; ++k)
-                if (N.ref[k] >= 0) N.ref[k] += base;
+            for (int k = 0; k < 8; ++k) {
+                if (N.ref[k] >= 0) N.ref[k] += base;                          // child node
+                else if (N.negA[k] != INFINITY) N.ref[k] = ~(~N.ref[k] + pbase);   // triangle (unused: never)
+            }
         out.nodes.insert(out.nodes.end(), R.nodes.begin(), R.nodes.end());
         out.node_self.insert(out.node_self.end(), R.self.begin(), R.self.end());
         std::vector<int32_t> lv;

@@ -275,11 +275,11 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
                 if (hit) {
                     ++ucnt;
                     if (t < max_ray_len) {
-                        const unsigned long long k = slot_key(t, idx);
+                        const unsigned long long k = slot_key(t, x.idx);
                         ukey = k < ukey ? k : ukey;
                     }
                 }
-                if (PROF) { ++n_exact; exact_class(xc, fan, idx, O, D, x, hit); }
+                if (PROF) { ++n_exact; exact_class(xc, fan, x.idx, O, D, x, hit); }
             }
             n_pairs += (uint32_t)__builtin_popcountll(m);
             idx = nidx;
@@ -297,7 +297,7 @@ static __device__ __forceinline__ void drain_queue(WaveLds &L, int32_t &nq, int3
     const int todo = final ? np : (np & ~63);
     n_pairs += (uint32_t)todo;
     auto pair_test = [&](uint32_t pr, const ExactRec &x) {
-        const int32_t idx = (int32_t)(pr >> 6);
+        const int32_t idx = x.idx;
         const int r = (int)(pr & 63u);
         const f3 Or = mk3(L.ray[0][r], L.ray[1][r], L.ray[2][r]);
         const f3 Dr = mk3(L.ray[3][r], L.ray[4][r], L.ray[5][r]);
@@ -419,7 +419,7 @@ static __device__ __forceinline__ void trav_packet(WaveLds &L, const RayBase &ra
 #pragma unroll
             for (int k = 0; k < W; ++k)
                 if (any_lane(d[k] <= 0.0f)) L.stack[top++] = N.ref[k];
-        } else {                                   // leaf: triangles ~ref -> deferred exact tests
+        } else {                                   // leaf: exact records ~ref -> deferred exact tests
             // room for the leaf's W entries / pairs (one drain site per node)
             if (nq > 64 - W || np > LPC_PAIRS - W * (LPC_DRAIN_U - 1)) drain(false);
 #pragma unroll

@@ -434,12 +434,13 @@ LPC_HD float filter_testh(float cx, float cy, float cz, float negB, float negA, 
 #define LPC_FILT_ABS 2e-10
 
 // One node of a mesh run's W-wide sphere hierarchy (W = 4 or 8), children in
-// SoA form.  ref[k] >= 0: child node; ref[k] < 0: triangle ~ref[k], whose test
+// SoA form.  ref[k] >= 0: child node; ref[k] < 0: exact record ~ref[k] (records in
+// leaf order, ExactRec::idx the triangle), whose test
 // is the triangle's own filter record.  A node's test (in its parent) is
 // node_record() of ALL triangles below it, so a ray whose line Moller-Trumbore
 // accepts against some triangle passes every test on the way down.  Unused
 // children: never.  128 B (W 4) / 256 B (W 8): whole scalar-load lines.
-// ref >= 0: child node; ref < 0: triangle ~ref.
+// ref >= 0: child node; ref < 0: exact record ~ref (leaf order).
 template <int W>
 struct NodeW {
     float cx[W], cy[W], cz[W], negB[W], negA[W];
@@ -561,8 +562,10 @@ LPC_HD void packet_angle_finish(float angmax, bool finite, PacketRec &Q)
     Q.cth = cosf(Q.th);
 }
 
-struct ExactRec {       // V0, E1 = V1-V0, E2 = V2-V0 (float, exactly as the reference)
-    float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, pad0, pad1, pad2;
+struct ExactRec {       // V0, E1 = V1-V0, E2 = V2-V0 (float, exactly as the reference), the triangle index
+    float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z;
+    int32_t idx;
+    float pad1, pad2;
 };
 
 // Host: float record of the exact bound dist^2 <= A + B ww (A rounded up, B up).

@@ -248,6 +248,30 @@ struct lpc_handle {
     std::vector<lpc_iter_stats> gstats;             // all-reduced per-iteration stats of the last lpc_trace_run
     double xchg_us = 0.0;                           // host time inside the hook (lpc_prof)
     int64_t xchg_calls = 0;
+    // streamed batches of new rays (lpc_trace_stage_rays / lpc_trace_run_staged_async):
+    // a FIFO of up to two staged batches, each copied to the device by a helper
+    // thread on the copy stream while the handle traces the batch before it
+    struct RaySlot {
+        Pop P;                                      // the batch as SoA rows (swapped with I when it is traced)
+        DBuf aos;                                   // its (n,4) origin / direction rows (stage modes 0, 1)
+        void *pin = nullptr;                        // pinned host staging of the caller's rows
+        size_t pin_bytes = 0;
+        DBuf scan;                                  // k_ray_scan of the batch (device) ...
+        RayScan *scan_host = nullptr;               // ... and its pinned copy
+        hipEvent_t ev = nullptr;                    // the batch's copies, unpacks and scan done (cstream)
+        std::thread th;
+        int rc = 0;
+        std::string err;
+        int64_t n = 0;
+        float max_ray_len = 1e3f, ior_env = 1.0f;
+        int64_t scan_gen = -1;                      // the scene generation its scan keyed to (-1: none)
+    } rslot[2];
+    int64_t scene_gen = 0;                          // lpc_scene_upload count (the scan's key box)
+    int rs_head = 0, rs_count = 0;
+    hipStream_t cstream = nullptr;                  // copy stream of the staged batches
+    int stage_mode = 1;
+    bool xrec_leaf_order = true;                    // LPC_XREC_ORDER: exact records in leaf order (1) / by triangle (0)                             // LPC_STAGE_MODE: 0 pageable DMA, 1 pinned rows, 2 pinned SoA chunks
+    hipEvent_t ev_stage = nullptr;                  // main-stream work before a stage call (cstream waits)
 };
 
 static std::string g_open_err;
@@ -361,6 +385,7 @@ static void drop_piece_tables(lpc_handle *h)
 }
 
 static int host_threads();
+static void stage_drop(lpc_handle *h);
 
 // Per mesh run: an 8-wide sphere hierarchy over its triangles in a top-down
 // median-split order, every node's test node_record() of ALL triangles below it
@@ -399,6 +424,29 @@ static int build_records(lpc_handle *h)
     h->sliver_dmin_host.clear();
     for (const SliverRec &q : out.slivers) h->sliver_dmin_host.push_back(q.dmin);
     h->Mpad = (int32_t)out.nodes.size();
+    // exact records in leaf order (a leaf's triangles adjacent: the drains' gathers
+    // touch few lines), each with its triangle index; LPC_XREC_ORDER=0 keeps
+    // round 5's layout (records by triangle index, leaf refs ~triangle) for A/B
+    if (!h->xrec_leaf_order) {
+        for (Node8 &N : out.nodes)
+            for (int k = 0; k < 8; ++k)
+                if (N.ref[k] < 0 && N.negA[k] != INFINITY) N.ref[k] = ~out.xorder[(size_t)~N.ref[k]];
+        out.xorder.resize((size_t)h->M);
+        for (int32_t i = 0; i < h->M; ++i) out.xorder[(size_t)i] = i;
+    }
+    std::vector<ExactRec> xr(std::max<size_t>(out.xorder.size(), 1));
+    memset(xr.data(), 0, xr.size() * sizeof(ExactRec));
+    for (size_t p = 0; p < out.xorder.size(); ++p) {
+        const int32_t i = out.xorder[p];
+        const float *a = &h->hv0[4 * (size_t)i], *b = &h->hv1[4 * (size_t)i], *c = &h->hv2[4 * (size_t)i];
+        ExactRec &x = xr[p];
+        x.v0x = a[0]; x.v0y = a[1]; x.v0z = a[2];
+        x.e1x = b[0] - a[0]; x.e1y = b[1] - a[1]; x.e1z = b[2] - a[2];
+        x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
+        x.idx = i;
+    }
+    RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
+    HIPCHK(h, hipMemcpy(h->d_xrec.p, xr.data(), xr.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
     RETIF(dalloc(h, h->d_nodes, out.nodes.size() * sizeof(Node8)));
     RETIF(dalloc(h, h->d_srec, out.slivers.size() * sizeof(SliverRec)));
     HIPCHK(h, hipMemcpy(h->d_nodes.p, out.nodes.data(), out.nodes.size() * sizeof(Node8), hipMemcpyHostToDevice));
@@ -1263,6 +1311,8 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_large_per_tri = env_int("LPC_LARGE_PER_TRI", h->spill_large_per_tri);
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
+    h->stage_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_STAGE_MODE", h->stage_mode)));
+    h->xrec_leaf_order = env_int("LPC_XREC_ORDER", 1) != 0;
     {   // the side stream of the sliver kernels and its fork / join events
         const unsigned evf = hipEventDisableTiming;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
@@ -1293,6 +1343,15 @@ int lpc_close(lpc_handle *h)
     if (!h) return 0;
     (void)settle(h);                     // a trace still running (lpc_trace_iterate / _run_async)
     (void)hipSetDevice(h->device);
+    stage_drop(h);
+    for (auto &rs : h->rslot) {
+        dfree(rs.P.buf); dfree(rs.aos); dfree(rs.scan);
+        if (rs.pin) (void)hipHostFree(rs.pin);
+        if (rs.scan_host) (void)hipHostFree(rs.scan_host);
+        if (rs.ev) (void)hipEventDestroy(rs.ev);
+    }
+    if (h->ev_stage) (void)hipEventDestroy(h->ev_stage);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     DBuf *bufs[] = {&h->d_nodes, &h->w_pk, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
@@ -1350,6 +1409,7 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
         return set_err(h, LPC_E_ARG, "scene has too many meshes (limit " + std::to_string(LPC_Q_MAX_SLOTS + 1) + ")");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    ++h->scene_gen;                     // staged batches' scans keyed to the old box are redone when traced
     const int32_t M = tri_count, K = mesh_count;
     for (int32_t i = 0; i < M; ++i)
         if (mesh_id[i] < 0 || mesh_id[i] >= K)
@@ -1393,16 +1453,10 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
             h->mat_passive = false;
         if (mat_type[j] == 1 && !(refl[j] >= 0.0f && refl[j] <= 1.0f)) h->mat_passive = false;
     }
-    // exact records and vertices
-    std::vector<ExactRec> xr((size_t)M);
+    // vertices (the hit triangle's normal in the shading)
     std::vector<float> vv((size_t)M * 9);
     for (int32_t i = 0; i < M; ++i) {
         const float *a = v0 + 4 * (size_t)i, *b = v1 + 4 * (size_t)i, *c = v2 + 4 * (size_t)i;
-        ExactRec &x = xr[(size_t)i];
-        x.v0x = a[0]; x.v0y = a[1]; x.v0z = a[2];
-        x.e1x = b[0] - a[0]; x.e1y = b[1] - a[1]; x.e1z = b[2] - a[2];
-        x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
-        x.pad0 = x.pad1 = x.pad2 = 0.0f;
         for (int k = 0; k < 3; ++k) { vv[9 * (size_t)i + k] = a[k]; vv[9 * (size_t)i + 3 + k] = b[k]; vv[9 * (size_t)i + 6 + k] = c[k]; }
     }
     {   // scene box for the ray coherence key
@@ -1424,13 +1478,11 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     }
     h->dcap = h->dcap_init;
     RETIF(build_records(h));
-    RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
     RETIF(dalloc(h, h->d_verts, vv.size() * 4));
     RETIF(dalloc(h, h->d_mat, (size_t)K * 4));
     RETIF(dalloc(h, h->d_ior, (size_t)K * 4));
     RETIF(dalloc(h, h->d_refl, (size_t)K * 4));
     RETIF(dalloc(h, h->d_diss, (size_t)K * 4));
-    HIPCHK(h, hipMemcpy(h->d_xrec.p, xr.data(), xr.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_verts.p, vv.data(), vv.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_mat.p, mat_type, (size_t)K * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_ior.p, ior, (size_t)K * 4, hipMemcpyHostToDevice));
@@ -1716,6 +1768,8 @@ static bool bsort_fits(const lpc_handle *h, int64_t n, const RayScan &S)
     return mx <= (uint32_t)LPC_BS_MAXB;
 }
 
+static int emitted_rays(lpc_handle *h, int64_t n, const RayScan &S, float max_ray_len, float ior_env);
+
 int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const float *dir4,
                        const float *pow, float max_ray_len, float ior_env)
 {
@@ -1740,6 +1794,13 @@ int lpc_trace_set_rays(lpc_handle *h, int64_t n, const float *origin4, const flo
         HIPCHK(h, hipMemcpyAsync(&S, h->d_scan.p, sizeof(RayScan), hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
+    return emitted_rays(h, n, S, max_ray_len, ior_env);
+}
+
+// The emitted rays' analysis (k_ray_scan) into the trace state, as the rays in
+// I: lpc_trace_set_rays and a staged batch that becomes current.
+static int emitted_rays(lpc_handle *h, int64_t n, const RayScan &S, float max_ray_len, float ior_env)
+{
     memcpy(&h->init_dmax2, &S.dmax2_bits, sizeof(double));
     h->pow_nonneg = S.neg_pow == 0u;
     // coherence key bits that can vary over these rays (k_raykey: [origin cell 15 |
@@ -1777,6 +1838,188 @@ int lpc_trace_reset(lpc_handle *h)
     h->m_total = 0;                             // measured record emptied (the first iteration resets the counters)
     h->m_inflight = 0;
     return 0;
+}
+
+// ---- streamed batches of new rays ------------------------------------------
+// A staged batch is copied by a helper thread: the caller's (n,4) rows
+// transposed into the slot's pinned staging as the population's SoA arrays (a
+// few host threads, chunk by chunk, each chunk's DMAs queued as soon as it is
+// ready: 28 B per ray cross PCIe), the emitted rays' fills and k_ray_scan, all on
+// the copy stream, which first
+// waits for the main-stream work queued when the batch was staged (the slot's
+// buffers may hold an earlier batch's emitted rays).  The main thread meanwhile
+// traces the batch before it.
+static void stage_worker(lpc_handle *h, lpc_handle::RaySlot *s, const float *origin4, const float *dir4,
+                         const float *pow, const float box_lo[3], const float box_scale[3], bool scan)
+{
+    auto fail = [&](hipError_t e, const char *what) {
+        s->rc = LPC_E_HIP;
+        s->err = std::string("stage_rays: ") + what + ": " + hipGetErrorString(e);
+    };
+    const double t0 = h->host_prof ? host_us() : 0.0;
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) { fail(e, "hipSetDevice"); return; }
+    const int64_t n = s->n;
+    hipStream_t cs = h->cstream;
+    const int mode = h->stage_mode;
+    if (mode == 2) {
+        // chunks: the host transposes chunk c + 1 into the pinned SoA arrays while
+        // the DMAs of chunk c run (28 B per ray cross PCIe)
+        float *pin = (float *)s->pin;
+        const int64_t CH = (int64_t)1 << 18;
+        const int T = std::max(1, std::min(4, host_threads()));
+        for (int64_t lo = 0; lo < n; lo += CH) {
+            const int64_t hi = std::min(n, lo + CH);
+            host_parts(hi - lo, T, [&](int64_t a, int64_t b, int) {
+                for (int64_t i = lo + a; i < lo + b; ++i) {
+                    const float *o = origin4 + 4 * i, *d = dir4 + 4 * i;
+                    pin[i] = o[0]; pin[n + i] = o[1]; pin[2 * n + i] = o[2];
+                    pin[3 * n + i] = d[0]; pin[4 * n + i] = d[1]; pin[5 * n + i] = d[2];
+                }
+                memcpy(pin + 6 * n + lo + a, pow + lo + a, (size_t)(b - a) * 4);
+            });
+            for (int k = 0; k < 7; ++k)
+                if ((e = hipMemcpyAsync(s->P.f(k) + lo, pin + (size_t)k * n + lo, (size_t)(hi - lo) * 4,
+                                        hipMemcpyHostToDevice, cs)) != hipSuccess) {
+                    fail(e, "copy");
+                    return;
+                }
+        }
+    } else {
+        // the (n,4) rows as they are: from the caller's memory (mode 0: the
+        // runtime's own staging of a pageable copy) or through the slot's pinned
+        // block (mode 1: host threads copy, one DMA), unpacked on the device
+        float4 *so = (float4 *)s->aos.p, *sd = so + n;
+        const char *src_o = (const char *)origin4, *src_d = (const char *)dir4, *src_p = (const char *)pow;
+        if (mode == 1) {
+            char *pin = (char *)s->pin;
+            host_parts(n, host_threads(), [&](int64_t lo, int64_t hi, int) {
+                memcpy(pin + (size_t)lo * 16, origin4 + 4 * lo, (size_t)(hi - lo) * 16);
+                memcpy(pin + (size_t)n * 16 + (size_t)lo * 16, dir4 + 4 * lo, (size_t)(hi - lo) * 16);
+                memcpy(pin + (size_t)n * 32 + (size_t)lo * 4, pow + lo, (size_t)(hi - lo) * 4);
+            });
+            src_o = pin; src_d = pin + (size_t)n * 16; src_p = pin + (size_t)n * 32;
+        }
+        if ((e = hipMemcpyAsync(so, src_o, (size_t)n * 16, hipMemcpyHostToDevice, cs)) != hipSuccess ||
+            (e = hipMemcpyAsync(sd, src_d, (size_t)n * 16, hipMemcpyHostToDevice, cs)) != hipSuccess ||
+            (e = hipMemcpyAsync(s->P.f(6), src_p, (size_t)n * 4, hipMemcpyHostToDevice, cs)) != hipSuccess) {
+            fail(e, "copy");
+            return;
+        }
+        hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, cs, n, (const float4 *)so, s->P.f(0), s->P.f(1),
+                           s->P.f(2));
+        hipLaunchKernelGGL(k_unpack4, dim3(grid1(n)), dim3(256), 0, cs, n, (const float4 *)sd, s->P.f(3), s->P.f(4),
+                           s->P.f(5));
+    }
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)s->P.pmid(), -2, (size_t)n, cs)) != hipSuccess) { fail(e, "fill"); return; }
+    if (scan) {                                     // the scene's key box is known: the analysis rides along
+        if ((e = hipMemsetAsync(s->scan.p, 0, sizeof(RayScan), cs)) != hipSuccess) { fail(e, "fill"); return; }
+        hipLaunchKernelGGL(k_ray_scan, dim3((unsigned)std::min<int64_t>(grid1(n), 2048)), dim3(256), 0, cs, s->P.in(),
+                           n, box_lo[0], box_lo[1], box_lo[2], box_scale[0], box_scale[1], box_scale[2],
+                           (RayScan *)s->scan.p);
+        if ((e = hipGetLastError()) != hipSuccess) { fail(e, "launch"); return; }
+        if ((e = hipMemcpyAsync(s->scan_host, s->scan.p, sizeof(RayScan), hipMemcpyDeviceToHost, cs)) != hipSuccess) {
+            fail(e, "copy");
+            return;
+        }
+    }
+    if ((e = hipEventRecord(s->ev, cs)) != hipSuccess) fail(e, "event");
+    if (h->host_prof) {
+        const double t1 = host_us();
+        (void)hipEventSynchronize(s->ev);
+        fprintf(stderr, "[lpc host] stage mode %d: %lld rays, enqueued %.1f us, done %.1f us\n", mode, (long long)n,
+                t1 - t0, host_us() - t0);
+    }
+}
+
+// Join the helpers and forget the staged batches (lpc_close).
+static void stage_drop(lpc_handle *h)
+{
+    for (auto &s : h->rslot)
+        if (s.th.joinable()) s.th.join();
+    h->rs_count = 0;
+    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+}
+
+int lpc_trace_stage_rays(lpc_handle *h, int64_t n, const float *origin4, const float *dir4, const float *pow,
+                         float max_ray_len, float ior_env)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (n <= 0 || !origin4 || !dir4 || !pow) return set_err(h, LPC_E_ARG, "stage_rays: need n > 0 rays and all buffers");
+    if (h->rs_count >= 2) return set_err(h, LPC_E_STATE, "stage_rays: two batches are staged already");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!h->cstream) {
+        HIPCHK(h, hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
+        HIPCHK(h, hipEventCreateWithFlags(&h->ev_stage, hipEventDisableTiming));
+    }
+    lpc_handle::RaySlot &s = h->rslot[(h->rs_head + h->rs_count) % 2];
+    if (s.th.joinable()) s.th.join();
+    if (!s.ev) HIPCHK(h, hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    if (!s.scan_host) HIPCHK(h, hipHostMalloc((void **)&s.scan_host, sizeof(RayScan), hipHostMallocDefault));
+    // buffers (allocations synchronise; they grow only with the batch size)
+    RETIF(pop_reserve(h, s.P, n));
+    RETIF(dalloc(h, s.scan, sizeof(RayScan)));
+    if (h->stage_mode != 2) RETIF(dalloc(h, s.aos, (size_t)n * 32));
+    const size_t pb = (size_t)n * (h->stage_mode == 2 ? 28 : 36);
+    if (h->stage_mode != 0 && s.pin_bytes < pb) {
+        if (s.pin) { (void)hipStreamSynchronize(h->cstream); (void)hipHostFree(s.pin); s.pin = nullptr; s.pin_bytes = 0; }
+        HIPCHK(h, hipHostMalloc(&s.pin, pb, hipHostMallocDefault));
+        s.pin_bytes = pb;
+    }
+    s.n = n;
+    s.max_ray_len = max_ray_len;
+    s.ior_env = ior_env;
+    s.rc = 0;
+    s.err.clear();
+    s.scan_gen = h->M ? h->scene_gen : -1;      // no scene yet: the scan runs when the batch is traced
+    // the slot's device buffers may hold an earlier batch's emitted rays: the copy
+    // stream starts after the main-stream work queued so far
+    HIPCHK(h, hipEventRecord(h->ev_stage, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->cstream, h->ev_stage, 0));
+    const float lo[3] = {h->box_lo[0], h->box_lo[1], h->box_lo[2]};
+    const float sc[3] = {h->box_scale[0], h->box_scale[1], h->box_scale[2]};
+    s.th = std::thread(stage_worker, h, &s, origin4, dir4, pow, lo, sc, s.scan_gen >= 0);
+    ++h->rs_count;
+    return 0;
+}
+
+static int trace_run(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                     int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap,
+                     bool wait);
+
+int lpc_trace_run_staged_async(lpc_handle *h, int32_t max_iter, double power_threshold, lpc_iter_stats *per_iter,
+                               int32_t *n_iter, int64_t *measured_count, double *mesh_power, int32_t mesh_power_cap)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (!h->rs_count) return set_err(h, LPC_E_STATE, "run_staged: no batch staged (lpc_trace_stage_rays)");
+    if (!h->M) return set_err(h, LPC_E_STATE, "no scene uploaded");
+    if (mesh_power && mesh_power_cap < h->K)
+        return set_err(h, LPC_E_ARG, "trace: mesh_power capacity below the scene's mesh count");
+    if (!n_iter || (max_iter > 0 && !per_iter)) return set_err(h, LPC_E_ARG, "trace_run: null output");
+    HIPCHK(h, hipSetDevice(h->device));
+    lpc_handle::RaySlot &s = h->rslot[h->rs_head];
+    if (s.th.joinable()) s.th.join();
+    h->rs_head ^= 1;
+    --h->rs_count;
+    if (s.rc) return set_err(h, s.rc, s.err);
+    // the analysis is read on the host (the copy ran during the previous trace);
+    // the trace's first kernels wait for the batch on the device
+    HIPCHK(h, hipEventSynchronize(s.ev));
+    HIPCHK(h, hipStreamWaitEvent(h->stream, s.ev, 0));
+    if (s.scan_gen != h->scene_gen) {           // staged before this scene: its analysis now, on the stream
+        RETIF(dalloc(h, s.scan, sizeof(RayScan)));
+        HIPCHK(h, hipMemsetAsync(s.scan.p, 0, sizeof(RayScan), h->stream));
+        hipLaunchKernelGGL(k_ray_scan, dim3((unsigned)std::min<int64_t>(grid1(s.n), 2048)), dim3(256), 0, h->stream,
+                           s.P.in(), s.n, h->box_lo[0], h->box_lo[1], h->box_lo[2], h->box_scale[0],
+                           h->box_scale[1], h->box_scale[2], (RayScan *)s.scan.p);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(s.scan_host, s.scan.p, sizeof(RayScan), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    std::swap(h->I, s.P);
+    RETIF(emitted_rays(h, s.n, *s.scan_host, s.max_ray_len, s.ior_env));
+    return trace_run(h, max_iter, power_threshold, per_iter, n_iter, measured_count, mesh_power, mesh_power_cap,
+                     false);
 }
 
 // All-reduce (sum) of the iteration's stats over the ranks of a sharded trace.

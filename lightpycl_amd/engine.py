@@ -28,12 +28,11 @@ def _rows(x, w):
     return x
 
 
-def _tri_vertices(mesh):
-    """tribuf()'s three vertex lists as float32 (n,4) arrays, gathered at once when
-    the mesh holds an ndarray of vertex rows and integer triangles (the
-    generators' meshes): the same rows, rounded to float32 the same way, as
-    np.array(tribuf()[k], dtype=np.float32), without a Python loop over
-    triangles.  None for other containers (the caller uses tribuf())."""
+def _tri_tables(mesh):
+    """(V as float32 (nv,4), T (n,3) integer) when the mesh holds an ndarray of
+    vertex rows and integer triangles (the generators' meshes), else None (the
+    caller uses tribuf()).  Gathering rows of float32(V) gives the same rows,
+    rounded to float32 the same way, as np.array(tribuf()[k], dtype=np.float32)."""
     V, T = _rows(getattr(mesh, "vertices", None), 4), _rows(getattr(mesh, "triangles", None), 3)
     if V is None or T is None or V.dtype.kind != "f":
         return None
@@ -41,12 +40,13 @@ def _tri_vertices(mesh):
         return None
     if len(T) and (T.min() < -len(V) or T.max() >= len(V)):
         return None
-    return [np.ascontiguousarray(V[T[:, k]], dtype=np.float32) for k in range(3)]
+    return np.ascontiguousarray(V, dtype=np.float32), T
 
 
 def flatten_meshes(meshes):
     """(v0, v1, v2, mesh_id, mat_type, ior, refl, diss) as iterative_tracer.py:121-151 builds
-    them: per-mesh material records and the concatenated tribuf() vertex rows."""
+    them: per-mesh material records and the concatenated tribuf() vertex rows
+    (gathered straight into the float32 outputs)."""
     K = len(meshes)
     if K == 0:
         raise ValueError("iterative_tracer needs at least one mesh")
@@ -54,25 +54,30 @@ def flatten_meshes(meshes):
     ior = np.zeros(K, np.float32)
     refl = np.zeros(K, np.float32)
     diss = np.zeros(K, np.float32)
-    v0s, v1s, v2s, ids = [], [], [], []
+    parts = []
     for j, mesh in enumerate(meshes):
         mat = mesh.getMaterialBuf()
         mat_type[j] = np.int32(mat.get("type"))
         ior[j] = np.float32(mat.get("IOR"))
         refl[j] = np.float32(mat.get("R"))
         diss[j] = np.float32(mat.get("dissipation"))
-        tv = _tri_vertices(mesh)
-        if tv is None:                          # general vertex containers: the reference's tribuf() lists
+        tt = _tri_tables(mesh)
+        if tt is None:                          # general vertex containers: the reference's tribuf() lists
             tb = mesh.tribuf()
-            tv = [np.array(tb[k], dtype=np.float32).reshape(-1, 4) for k in range(3)]
-        v0s.append(tv[0])
-        v1s.append(tv[1])
-        v2s.append(tv[2])
-        ids.append(np.zeros(len(tv[0]), np.int32) + j)
-    v0 = np.ascontiguousarray(np.concatenate(v0s), dtype=np.float32)
-    v1 = np.ascontiguousarray(np.concatenate(v1s), dtype=np.float32)
-    v2 = np.ascontiguousarray(np.concatenate(v2s), dtype=np.float32)
-    mesh_id = np.ascontiguousarray(np.concatenate(ids), dtype=np.int32)
+            tt = [np.array(tb[k], dtype=np.float32).reshape(-1, 4) for k in range(3)]
+        parts.append(tt)
+    counts = [len(p[1]) if len(p) == 2 else len(p[0]) for p in parts]
+    M = int(sum(counts))
+    v0, v1, v2 = (np.empty((M, 4), np.float32) for _ in range(3))
+    lo = 0
+    for p, c in zip(parts, counts):
+        for k, out in enumerate((v0, v1, v2)):
+            if len(p) == 2:
+                np.take(p[0], p[1][:, k], axis=0, out=out[lo:lo + c])
+            else:
+                out[lo:lo + c] = p[k]
+        lo += c
+    mesh_id = np.repeat(np.arange(K, dtype=np.int32), counts)
     return v0, v1, v2, mesh_id, mat_type, ior, refl, diss
 
 
@@ -218,6 +223,36 @@ class Engine:
                                           np.float32(max_ray_len), np.float32(ior_env)))
         return n
 
+    def stage_rays(self, origin4, dir4, pow_, max_ray_len=1e3, ior_env=1.0):
+        """lpc_trace_stage_rays: queue a batch of new rays (at most two staged),
+        copied to the device by a helper thread while the engine traces the batch
+        before it.  The arrays are kept alive here until :meth:`run_staged`
+        traces the batch."""
+        o, d = f32(origin4, (-1, 4)), f32(dir4, (-1, 4))
+        pw = f32(pow_).reshape(-1)
+        n = o.shape[0]
+        if d.shape[0] != n or pw.shape[0] != n:
+            raise ValueError("origin, direction and power must have the same ray count")
+        self._c(self.L.lpc_trace_stage_rays(self.h, n, ptr(o), ptr(d), ptr(pw), np.float32(max_ray_len),
+                                            np.float32(ior_env)))
+        self.__dict__.setdefault("_staged", []).append((o, d, pw))
+        return n
+
+    def run_staged(self, iterations, power_threshold):
+        """lpc_trace_run_staged_async: trace the oldest staged batch (it becomes
+        the emitted rays, as set_rays) to the reference's termination.  Returns
+        what :meth:`run_local` returns; the outputs are final, the last rows may
+        still move (:meth:`sync`)."""
+        arr, k, c, mp, pk, pc, pmp, mcap = self._bufs(iterations)
+        try:
+            self._c(self.L.lpc_trace_run_staged_async(self.h, max(int(iterations), 0), float(power_threshold), arr,
+                                                      pk, pc, pmp, mcap))
+        finally:
+            staged = getattr(self, "_staged", [])
+            if staged:
+                staged.pop(0)               # the helper has copied it (joined in the call)
+        return type(arr).from_buffer_copy(arr)[:k.value], (c.value, mp[: self.mesh_count].copy())
+
     def reset(self):
         self._c(self.L.lpc_trace_reset(self.h))
 
@@ -286,16 +321,12 @@ class Engine:
         """lpc_sync: wait for every kernel queued on the engine's stream."""
         self._c(self.L.lpc_sync(self.h))
 
-    def run_local(self, iterations, power_threshold, wait=True, reset=False):
-        """lpc_trace_run: iterate until the next population's power is below
-        power_threshold or no ray is kept (at most `iterations`).  Returns the
-        per-iteration stats and the measured (count, per-mesh power).
-        reset=True (with wait=False): lpc_trace_rerun_async, the reset and the
-        trace in one call (the bench's back-to-back batches)."""
+    def _bufs(self, iterations):
+        """Output buffers and argument objects of the trace calls, kept per
+        (iteration cap, mesh count): the library writes one power per mesh of the
+        CURRENT scene into mp, and refuses a buffer below that count (its capacity
+        travels with the call)."""
         cap = max(int(iterations), 0)
-        # output buffers and argument objects kept per (cap, mesh count): the library
-        # writes one power per mesh of the CURRENT scene into mp, and refuses a
-        # buffer below that count (its capacity travels with the call)
         key = (cap, int(self.mesh_count))
         bufs = self._run_bufs.get(key) if hasattr(self, "_run_bufs") else None
         if bufs is None:
@@ -304,7 +335,16 @@ class Engine:
             bufs = (arr, k, c, mp, ctypes.byref(k), ctypes.byref(c), mp.ctypes.data_as(ctypes.c_void_p),
                     ctypes.c_int32(mp.size))
             self.__dict__.setdefault("_run_bufs", {})[key] = bufs
-        arr, k, c, mp, pk, pc, pmp, mcap = bufs
+        return bufs
+
+    def run_local(self, iterations, power_threshold, wait=True, reset=False):
+        """lpc_trace_run: iterate until the next population's power is below
+        power_threshold or no ray is kept (at most `iterations`).  Returns the
+        per-iteration stats and the measured (count, per-mesh power).
+        reset=True (with wait=False): lpc_trace_rerun_async, the reset and the
+        trace in one call (the bench's back-to-back batches)."""
+        cap = max(int(iterations), 0)
+        arr, k, c, mp, pk, pc, pmp, mcap = self._bufs(cap)
         # wait=False: lpc_trace_run_async (the outputs are final; the last rows may
         # still move on the device and the next batch's launches queue behind them)
         if reset and not wait:

@@ -28,6 +28,7 @@ from __future__ import annotations
 import ctypes
 import pickle
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -49,16 +50,13 @@ def f32_sorted_sum(a):
     return np.float32(out.value)
 
 
-_SUM_POOL = None
+# the tracer's helper thread (created with the module, started on first use)
+_SUM_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="lpc-sum")
 
 
 def _background(fn, *args):
     """Run fn(*args) on the tracer's helper thread (numpy's sort and the ctypes
     call release the GIL): the input-power sum overlaps the scene and ray upload."""
-    global _SUM_POOL
-    if _SUM_POOL is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _SUM_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="lpc-sum")
     return _SUM_POOL.submit(fn, *args)
 
 
@@ -153,11 +151,14 @@ class CL_Tracer:
         ph = {}                                 # host-side phases of this call (self.phase_s)
         t_ph = clk()
         origin = dirs = power = None
+        # results mode keeps iteration 0's origins in its results tuple: a copy, as
+        # the reference's np.float32(...) is; aggregate mode only reads them
+        conv = np.float32 if keep_results else (lambda a: np.asarray(a, dtype=np.float32))
         for k, light in enumerate(light_source):                       # :99-113
             if k == 0:
-                origin = np.float32(light.rays_origin)
-                dirs = np.float32(light.rays_dir)
-                power = np.float32(light.rays_power)
+                origin = conv(light.rays_origin)
+                dirs = conv(light.rays_dir)
+                power = conv(light.rays_power)
             else:
                 origin = np.append(origin, light.rays_origin, axis=0).astype(np.float32)
                 dirs = np.append(dirs, light.rays_dir, axis=0).astype(np.float32)
@@ -167,6 +168,10 @@ class CL_Tracer:
         power = np.asarray(power, dtype=np.float32)
         in_pow = _background(f32_sorted_sum, power)                    # :115, beside the uploads
         pow_shape0 = power.shape
+        if not keep_results:
+            # aggregate mode: the rays go to the device on the engine's helper thread
+            # (lpc_trace_stage_rays) while the scene records are built below
+            n = self.engine.stage_rays(origin, dirs, power.reshape(-1), max_ray_len, ior_env)
         ph["sources"] = clk() - t_ph
         t_ph = clk()
         arrs = self._flatten(meshes)                                   # :121-151
@@ -178,7 +183,8 @@ class CL_Tracer:
         self.geometry = (arrs[0], arrs[1], arrs[2])
         ph["scene"] = clk() - t_ph
         t_ph = clk()
-        n = self.engine.set_rays(origin, dirs, power.reshape(-1), max_ray_len, ior_env)
+        if keep_results:
+            n = self.engine.set_rays(origin, dirs, power.reshape(-1), max_ray_len, ior_env)
         ph["set_rays"] = clk() - t_ph
         t_ph = clk()
         input_power = in_pow.result()
@@ -193,24 +199,31 @@ class CL_Tracer:
         thr = (1.0 - trace_until_dissipated) * input_power              # :383
         t0 = time.time()
         try:
-            for t_iter in range(int(trace_iterations)):                 # :241
+            if not keep_results:
+                # the whole loop (:241-391) in the library: the same stop rules on the
+                # device's float64 power sums, iteration i + 1 enqueued before
+                # iteration i's counters arrive
+                stats, _ = self.engine.run_staged(int(trace_iterations), float(thr))
+                for t_iter, st in enumerate(stats):
+                    self.iteration_counts.append(int(st.n_in))
+                    self.power_left.append(float(st.power_next) / float(input_power) if input_power else 0.0)
+                    if self.verbose:
+                        print(f"iteration {t_iter + 1}: {st.n_in} rays, {st.n_reflect + st.n_refract} children "
+                              f"kept, {100.0 * self.power_left[-1]:.4f} % power left")
+                trace_iterations = 0                                    # the host loop below has nothing left
+            for t_iter in range(int(trace_iterations)):                 # :241 (results mode)
                 self.iteration_counts.append(n)
-                if keep_results:
-                    # the results tuple (:335-355) copied to pinned host arrays on
-                    # the export stream while the next iterations run (complete
-                    # after the sync below); iteration 0's origins are the host's
-                    t_it = clk()
-                    st, ex = self.engine.iterate_export(with_origin=t_iter > 0)
-                    ph.setdefault("iterate_export", []).append(clk() - t_it)
-                    ph.setdefault("export_pool_call", []).extend(getattr(self.engine, "export_times", ()))
-                    org = origin if t_iter == 0 else ex["origin"]
-                    pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
-                    self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355
-                    power_in_scene, below = self._power_decision(st, thr)    # :372, :383
-                else:
-                    st, _ = self.engine.iterate()
-                    power_in_scene = st.power_next
-                    below = power_in_scene < thr
+                # the results tuple (:335-355) copied to pinned host arrays on the
+                # export stream while the next iterations run (complete after the
+                # sync below); iteration 0's origins are the host's
+                t_it = clk()
+                st, ex = self.engine.iterate_export(with_origin=t_iter > 0)
+                ph.setdefault("iterate_export", []).append(clk() - t_it)
+                ph.setdefault("export_pool_call", []).extend(getattr(self.engine, "export_times", ()))
+                org = origin if t_iter == 0 else ex["origin"]
+                pw = ex["pow"].reshape(pow_shape0) if t_iter == 0 else ex["pow"]
+                self.results.append((org, ex["dest"], pw, ex["meas"]))  # :355
+                power_in_scene, below = self._power_decision(st, thr)    # :372, :383
                 n = st.n_reflect + st.n_refract
                 self.power_left.append(float(power_in_scene) / float(input_power) if input_power else 0.0)
                 if self.verbose:

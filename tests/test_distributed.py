@@ -156,6 +156,39 @@ def _worker_shm(rank, world, port, name, n, out_path):
     dist.destroy_process_group()
 
 
+def test_sharded_trace_world8(oracle_mod, tmp_path):
+    """The N = 8 split rehearsed on the CPU (the 8-GPU node is the driver's): eight
+    gloo ranks, each tracing its contiguous shard through the sharded driver with
+    the library's shared-memory per-iteration exchange, give the single-process
+    trace's global per-iteration counts and per-mesh power (the partition loop
+    this replaces: iterative_tracer.py:246-271, 383-391)."""
+    from lightpycl_amd import scenes
+    out = str(tmp_path / "r.json")
+    mp.spawn(_worker_shm, args=(8, _free_port(), "lens", 2403, out), nprocs=8, join=True)
+    got = json.load(open(out))
+    sc = scenes.lens(n=2403, seed=2)
+    _, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
+                               keep_results=False)
+    assert got["counts"] == info["counts"] and len(info["counts"]) >= 4
+    np.testing.assert_allclose(got["mesh_power"], info["mesh_power"], rtol=1e-12, atol=1e-12)
+
+
+def test_config5_split_covers_blocks():
+    """bench.py's config-5 ray set (8 fixed blocks) split over 1, 2, 4, 8 and 16
+    ranks: the ranks' shards, concatenated in rank order, are the whole set in
+    order (world == 8: one block per rank; world > 8: blocks split by rays)."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    from lightpycl_amd import scenes
+    total = 8 * 96
+    whole = bench.config5_rays(scenes, 0, 1, total)
+    for world in (2, 4, 8, 16):
+        parts = [bench.config5_rays(scenes, r, world, total) for r in range(world)]
+        assert [len(q[2]) for q in parts] == [total // world] * world
+        for k in range(3):
+            np.testing.assert_array_equal(np.concatenate([q[k] for q in parts]), whole[k])
+
+
 def test_sharded_trace_shm_comm(oracle_mod, tmp_path):
     from lightpycl_amd import scenes
     out = str(tmp_path / "r.json")

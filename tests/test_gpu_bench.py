@@ -23,11 +23,11 @@ ARGS = ["--steps", "5", "--warmup", "1", "--no-cpu", "--no-configs", "--rays", "
         "--c5-rays", "1600000", "--c5-steps", "2"]
 
 
-def _bench(gpus):
+def _bench(gpus, args=ARGS):
     env = dict(os.environ, LPC_BENCH_REHEARSE="1")
     env.pop("WORLD_SIZE", None)
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus)] + ARGS,
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus)] + args,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-4000:]
@@ -54,3 +54,24 @@ def test_bench_gpus2_launches_two_ranks():
             assert x == pytest.approx(y, rel=1e-9, abs=1e-300)
     # at N = 1 the strong block traces the weak block's rays (seed 7)
     assert one["strong"]["global_counts"] == one["weak_global_counts"]
+
+
+ARGS8 = ["--steps", "3", "--warmup", "1", "--no-cpu", "--no-configs", "--rays", "40000", "--strong-steps", "3",
+         "--c5-rays", "320000", "--c5-steps", "1"]
+
+
+def test_bench_gpus8_rehearsal():
+    """The driver's N = 8 form rehearsed on the one GPU: eight ranks, the config-5
+    split with one block per rank (world == 8), per-rank times and ray-bounces in
+    the line, and the strong and config-5 blocks' global counts equal to N = 1."""
+    out = _bench(8, ARGS8)
+    assert out["n_gpus"] == 8 and out["parity"]["steps_identical"] is True
+    assert len(out["rank_ms_per_step"]["per_rank"]) == 8
+    assert len(out["rank_ray_bounces_per_step"]) == 8 and min(out["rank_ray_bounces_per_step"]) > 0
+    assert out["config5"]["rays_per_rank"] == 320000 // 8
+    one = _bench(1, ARGS8)
+    for blk in ("strong", "config5"):
+        a, b = out[blk], one[blk]
+        assert a["global_counts"] == b["global_counts"], (blk, a["global_counts"], b["global_counts"])
+        assert len(a["rank_ray_bounces_per_step"]) == 8
+        assert sum(a["rank_ray_bounces_per_step"]) == pytest.approx(b["rank_ray_bounces_per_step"][0], rel=1e-12)
