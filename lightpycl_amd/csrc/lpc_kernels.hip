@@ -203,8 +203,8 @@ static __device__ __forceinline__ void unit_dir(const f3 &D, float &nx, float &n
 
 // LDS of one wave's traversal: the node stack, the deferred exact tests -- dense
 // entries (a triangle and the mask of its >= LPC_DRAIN_U rays) and sparse pairs
-// (triangle << 6 | ray lane, appended at the leaf) -- and the per-ray state.
-// LPC_PAIRS keeps the wave at 6656 bytes: 24 waves (6 per SIMD) in 160 KB of LDS.
+// (record << 6 | ray lane, appended at the leaf) -- and the per-ray state.
+// LPC_PAIRS keeps the wave at 5376 bytes (6 waves per SIMD are VGPR-bound).
 #ifndef LPC_PAIRS
 #define LPC_PAIRS 512
 #endif

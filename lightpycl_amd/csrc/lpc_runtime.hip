@@ -269,8 +269,8 @@ struct lpc_handle {
     int64_t scene_gen = 0;                          // lpc_scene_upload count (the scan's key box)
     int rs_head = 0, rs_count = 0;
     hipStream_t cstream = nullptr;                  // copy stream of the staged batches
-    int stage_mode = 1;
-    bool xrec_leaf_order = true;                    // LPC_XREC_ORDER: exact records in leaf order (1) / by triangle (0)                             // LPC_STAGE_MODE: 0 pageable DMA, 1 pinned rows, 2 pinned SoA chunks
+    int stage_mode = 0;                             // LPC_STAGE_MODE: 0 pageable DMA (round 6 A/B: 1.23-1.28 G
+                                                    //   fresh rays), 1 pinned rows (0.83-0.93), 2 pinned SoA chunks (0.77-1.0)
     hipEvent_t ev_stage = nullptr;                  // main-stream work before a stage call (cstream waits)
 };
 
@@ -385,6 +385,7 @@ static void drop_piece_tables(lpc_handle *h)
 }
 
 static int host_threads();
+static void host_parts(int64_t n, int T, const std::function<void(int64_t, int64_t, int)> &fn);
 static void stage_drop(lpc_handle *h);
 
 // Per mesh run: an 8-wide sphere hierarchy over its triangles in a top-down
@@ -424,34 +425,39 @@ static int build_records(lpc_handle *h)
     h->sliver_dmin_host.clear();
     for (const SliverRec &q : out.slivers) h->sliver_dmin_host.push_back(q.dmin);
     h->Mpad = (int32_t)out.nodes.size();
-    // exact records in leaf order (a leaf's triangles adjacent: the drains' gathers
-    // touch few lines), each with its triangle index; LPC_XREC_ORDER=0 keeps
-    // round 5's layout (records by triangle index, leaf refs ~triangle) for A/B
-    if (!h->xrec_leaf_order) {
-        for (Node8 &N : out.nodes)
-            for (int k = 0; k < 8; ++k)
-                if (N.ref[k] < 0 && N.negA[k] != INFINITY) N.ref[k] = ~out.xorder[(size_t)~N.ref[k]];
-        out.xorder.resize((size_t)h->M);
-        for (int32_t i = 0; i < h->M; ++i) out.xorder[(size_t)i] = i;
-    }
-    std::vector<ExactRec> xr(std::max<size_t>(out.xorder.size(), 1));
-    memset(xr.data(), 0, xr.size() * sizeof(ExactRec));
-    for (size_t p = 0; p < out.xorder.size(); ++p) {
-        const int32_t i = out.xorder[p];
-        const float *a = &h->hv0[4 * (size_t)i], *b = &h->hv1[4 * (size_t)i], *c = &h->hv2[4 * (size_t)i];
-        ExactRec &x = xr[p];
-        x.v0x = a[0]; x.v0y = a[1]; x.v0z = a[2];
-        x.e1x = b[0] - a[0]; x.e1y = b[1] - a[1]; x.e1z = b[2] - a[2];
-        x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
-        x.idx = i;
-    }
+    // exact records in leaf order (a leaf's 8 records are 384 contiguous bytes:
+    // the walk stages them into LDS with one LDS-DMA load), each with its
+    // triangle index; 8 spare records at the end, so the last leaf's load stays
+    // inside the buffer (round 6; by triangle index before, A/B neutral)
+    const double tb0 = h->host_prof ? host_us() : 0.0;
+    const size_t nx = out.xorder.size();
+    std::vector<ExactRec> xr(nx + 8);
+    memset(xr.data() + nx, 0, 8 * sizeof(ExactRec));
+    host_parts((int64_t)nx, host_threads(), [&](int64_t lo, int64_t hi, int) {
+        for (int64_t p = lo; p < hi; ++p) {
+            const int32_t i = out.xorder[(size_t)p];
+            const float *a = &h->hv0[4 * (size_t)i], *b = &h->hv1[4 * (size_t)i], *c = &h->hv2[4 * (size_t)i];
+            ExactRec &x = xr[(size_t)p];
+            x.v0x = a[0]; x.v0y = a[1]; x.v0z = a[2];
+            x.e1x = b[0] - a[0]; x.e1y = b[1] - a[1]; x.e1z = b[2] - a[2];
+            x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
+            x.idx = i;
+            x.pad1 = x.pad2 = 0.0f;
+        }
+    });
+    const double tb1 = h->host_prof ? host_us() : 0.0;
     RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
+    const double tb2 = h->host_prof ? host_us() : 0.0;
     HIPCHK(h, hipMemcpy(h->d_xrec.p, xr.data(), xr.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
+    const double tb3 = h->host_prof ? host_us() : 0.0;
     RETIF(dalloc(h, h->d_nodes, out.nodes.size() * sizeof(Node8)));
     RETIF(dalloc(h, h->d_srec, out.slivers.size() * sizeof(SliverRec)));
     HIPCHK(h, hipMemcpy(h->d_nodes.p, out.nodes.data(), out.nodes.size() * sizeof(Node8), hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_srec.p, out.slivers.data(), out.slivers.size() * sizeof(SliverRec),
                         hipMemcpyHostToDevice));
+    if (h->host_prof)
+        fprintf(stderr, "[lpc host] records upload: exact records %.1f us, alloc %.1f us, copy %.1f us, nodes %.1f us\n",
+                tb1 - tb0, tb2 - tb1, tb3 - tb2, host_us() - tb3);
     return 0;
 }
 
@@ -1312,7 +1318,6 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
     h->stage_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_STAGE_MODE", h->stage_mode)));
-    h->xrec_leaf_order = env_int("LPC_XREC_ORDER", 1) != 0;
     {   // the side stream of the sliver kernels and its fork / join events
         const unsigned evf = hipEventDisableTiming;
         if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
@@ -1407,6 +1412,7 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     // the root items carry a mesh's scratch slot in 12 bits (q_item)
     if (mesh_count > LPC_Q_MAX_SLOTS + 1)
         return set_err(h, LPC_E_ARG, "scene has too many meshes (limit " + std::to_string(LPC_Q_MAX_SLOTS + 1) + ")");
+    const double tu0 = h->host_prof ? host_us() : 0.0;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     ++h->scene_gen;                     // staged batches' scans keyed to the old box are redone when traced
@@ -1455,10 +1461,12 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     }
     // vertices (the hit triangle's normal in the shading)
     std::vector<float> vv((size_t)M * 9);
-    for (int32_t i = 0; i < M; ++i) {
-        const float *a = v0 + 4 * (size_t)i, *b = v1 + 4 * (size_t)i, *c = v2 + 4 * (size_t)i;
-        for (int k = 0; k < 3; ++k) { vv[9 * (size_t)i + k] = a[k]; vv[9 * (size_t)i + 3 + k] = b[k]; vv[9 * (size_t)i + 6 + k] = c[k]; }
-    }
+    host_parts(M, host_threads(), [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) {
+            const float *a = v0 + 4 * (size_t)i, *b = v1 + 4 * (size_t)i, *c = v2 + 4 * (size_t)i;
+            for (int k = 0; k < 3; ++k) { vv[9 * (size_t)i + k] = a[k]; vv[9 * (size_t)i + 3 + k] = b[k]; vv[9 * (size_t)i + 6 + k] = c[k]; }
+        }
+    });
     {   // scene box for the ray coherence key
         float lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (const std::vector<float> *vs : {&h->hv0, &h->hv1, &h->hv2})
@@ -1477,7 +1485,9 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
         h->scene_scale = diag2 > 0.0 ? 0.5 * sqrt(diag2) : 1.0;
     }
     h->dcap = h->dcap_init;
+    const double tu1 = h->host_prof ? host_us() : 0.0;
     RETIF(build_records(h));
+    const double tu2 = h->host_prof ? host_us() : 0.0;
     RETIF(dalloc(h, h->d_verts, vv.size() * 4));
     RETIF(dalloc(h, h->d_mat, (size_t)K * 4));
     RETIF(dalloc(h, h->d_ior, (size_t)K * 4));
@@ -1490,6 +1500,9 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     HIPCHK(h, hipMemcpy(h->d_diss.p, diss, (size_t)K * 4, hipMemcpyHostToDevice));
     h->ws_rays = 0;   // K may have changed
     h->traced_ready = false;
+    if (h->host_prof)
+        fprintf(stderr, "[lpc host] scene upload: tables %.1f us, records %.1f us, device copies %.1f us\n", tu1 - tu0,
+                tu2 - tu1, host_us() - tu2);
     return 0;
 }
 
@@ -2159,7 +2172,9 @@ int lpc_trace_population(lpc_handle *h, int64_t *n)
 static int ensure_measured(lpc_handle *h, int64_t need)
 {
     if (need <= h->m_cap) return 0;
-    int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * h->m_cap, 1 << 16));
+    // the first reservation takes twice the need: a trace's next iterations then
+    // append without the growth copy (which waits for the stream)
+    int64_t cap = std::max<int64_t>(h->m_cap ? need : 2 * need, std::max<int64_t>(2 * h->m_cap, 1 << 16));
     DBuf nb;
     RETIF(dalloc(h, nb, (size_t)cap * 5 * 4));
     if (h->m_cap > 0) {         // all old rows: an iteration still in flight may append past m_total

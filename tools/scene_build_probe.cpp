@@ -45,6 +45,10 @@ extern "C" int sbp_build(const float *v0, const float *v1, const float *v2, cons
         if (!err.empty()) return -1;
         best = ms < best ? ms : best;
     }
+    // leaf refs back to triangle indices (the round-5 layout the serial build makes)
+    for (Node8 &N : out.nodes)
+        for (int k = 0; k < 8; ++k)
+            if (N.ref[k] < 0 && N.negA[k] != INFINITY) N.ref[k] = ~out.xorder[(size_t)~N.ref[k]];
     uint64_t h = 1469598103934665603ull;
     h = fnv(h, out.nodes.data(), out.nodes.size() * sizeof(Node8));
     h = fnv(h, out.node_self.data(), out.node_self.size() * sizeof(FiltRec));
