@@ -18,6 +18,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -246,9 +247,13 @@ static inline void build_run(const SceneBuildIn &in, size_t r, RunOut &out)
 
 }  // namespace detail
 
-// The scene's records, runs built on up to `threads` host threads.  Returns ""
-// or an error message.
-static inline std::string build_scene_records(const SceneBuildIn &in, SceneBuildOut &out, int threads)
+// parfor(n, fn): fn(0) .. fn(n - 1), in any order, on host threads (the
+// runtime's persistent pool; tools/scene_build_probe.cpp spawns threads).
+using ParFor = std::function<void(int, const std::function<void(int)> &)>;
+
+// The scene's records, the runs built as parallel tasks.  Returns "" or an
+// error message.
+static inline std::string build_scene_records(const SceneBuildIn &in, SceneBuildOut &out, const ParFor &parfor)
 {
     std::vector<detail::RunOut> runs(in.nr);
     // the larger runs first, so the pool's last thread does not start a big one late
@@ -257,18 +262,7 @@ static inline std::string build_scene_records(const SceneBuildIn &in, SceneBuild
     std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
         return in.run_hi[a] - in.run_lo[a] > in.run_hi[b] - in.run_lo[b];
     });
-    std::atomic<size_t> next(0);
-    auto worker = [&]() {
-        for (size_t q; (q = next.fetch_add(1)) < in.nr;) detail::build_run(in, order[q], runs[order[q]]);
-    };
-    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), in.nr));
-    if (T <= 1) {
-        worker();
-    } else {
-        std::vector<std::thread> pool;
-        for (int k = 0; k < T; ++k) pool.emplace_back(worker);
-        for (std::thread &th : pool) th.join();
-    }
+    parfor((int)in.nr, [&](int q) { detail::build_run(in, order[(size_t)q], runs[order[(size_t)q]]); });
     // concatenation in run order: the records of a serial build
     out = SceneBuildOut();
     size_t total = 0;

@@ -2207,6 +2207,38 @@ __global__ void k_acc_init(DevAcc *acc, unsigned long long m_total)
 }
 
 // SoA xyz -> (n,4) rows with w = 0
+// Scene upload: the hit triangles' vertices (9 floats each, the shading's
+// normal) and the exact records in leaf order (xorder: triangle per record),
+// from the (M,4) rows on the device.
+__global__ __launch_bounds__(256) void k_vertex_rows(int64_t M, const float4 *__restrict__ v0,
+                                                     const float4 *__restrict__ v1, const float4 *__restrict__ v2,
+                                                     float *__restrict__ verts)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const float4 a = v0[i], b = v1[i], c = v2[i];
+    float *o = verts + 9 * i;
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = b.x; o[4] = b.y; o[5] = b.z; o[6] = c.x; o[7] = c.y; o[8] = c.z;
+}
+
+__global__ __launch_bounds__(256) void k_exact_records(int64_t nx, const int32_t *__restrict__ xorder,
+                                                       const float4 *__restrict__ v0, const float4 *__restrict__ v1,
+                                                       const float4 *__restrict__ v2, ExactRec *__restrict__ xrec)
+{
+    LPC_EXACT
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nx) return;
+    const int32_t i = xorder[p];
+    const float4 a = v0[i], b = v1[i], c = v2[i];
+    ExactRec x;
+    x.v0x = a.x; x.v0y = a.y; x.v0z = a.z;
+    x.e1x = b.x - a.x; x.e1y = b.y - a.y; x.e1z = b.z - a.z;       // E1 = V1 - V0, E2 = V2 - V0 (float, .cl:72-73)
+    x.e2x = c.x - a.x; x.e2y = c.y - a.y; x.e2z = c.z - a.z;
+    x.idx = i;
+    x.pad1 = x.pad2 = 0.0f;
+    xrec[p] = x;
+}
+
 __global__ __launch_bounds__(256) void k_pack4(int64_t n, const float *__restrict__ x,
                                                const float *__restrict__ y,
                                                const float *__restrict__ z, float4 *__restrict__ out)

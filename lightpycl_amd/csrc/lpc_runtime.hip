@@ -17,7 +17,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <thread>
 #include <limits>
 #include <map>
@@ -124,7 +126,10 @@ struct lpc_handle {
     int cus = 0;
     // scene
     int32_t M = 0, K = 0, Mpad = 0;
-    std::vector<float> hv0, hv1, hv2;               // host copies (record rebuilds)
+    std::vector<float> hv0, hv1, hv2;               // host copies, made on demand from d_raw (record rebuilds, profiling)
+    const float *src_v[3] = {nullptr, nullptr, nullptr};   // the scene's (n,4) rows: the caller's during
+                                                    //   lpc_scene_upload, hv0..2 after host_vertices()
+    DBuf d_raw;                                     // the scene's v0 | v1 | v2 rows on the device ((M,4) each)
     std::vector<int32_t> run_lo, run_hi;
     std::vector<std::vector<int32_t>> run_levels;    // per run: (first node, count) per level, root first
     std::vector<FiltRec> node_self;                  // each node's own test (piece roots)
@@ -386,6 +391,7 @@ static void drop_piece_tables(lpc_handle *h)
 
 static int host_threads();
 static void host_parts(int64_t n, int T, const std::function<void(int64_t, int64_t, int)> &fn);
+static void host_pool_run(int n, const std::function<void(int)> &fn);
 static void stage_drop(lpc_handle *h);
 
 // Per mesh run: an 8-wide sphere hierarchy over its triangles in a top-down
@@ -394,16 +400,21 @@ static void stage_drop(lpc_handle *h);
 // test is degenerate (slivers) or far wider than the triangle (thin) go to the
 // run's line-filter list; triangles that can never be hit are dropped.  Results
 // do not depend on the order (ties are resolved by triangle index).
+static int host_vertices(lpc_handle *h);
+
 static int build_records(lpc_handle *h)
 {
     drop_piece_tables(h);   // pieces index the records built here
+    if (!h->src_v[0]) RETIF(host_vertices(h));       // a rebuild after the upload: the rows from the device
     SceneBuildIn in;
-    in.v0 = h->hv0.data(); in.v1 = h->hv1.data(); in.v2 = h->hv2.data();
+    in.v0 = h->src_v[0]; in.v1 = h->src_v[1]; in.v2 = h->src_v[2];
     in.run_lo = h->run_lo.data(); in.run_hi = h->run_hi.data(); in.nr = h->run_lo.size();
     in.dcap = h->dcap; in.scene_scale = h->scene_scale; in.thin_k = kThin; in.stack_max = LPC_STACK;
     SceneBuildOut out;
     const double t0 = h->host_prof ? host_us() : 0.0;
-    const std::string err = build_scene_records(in, out, host_threads());
+    const std::string err = build_scene_records(in, out, [](int n, const std::function<void(int)> &fn) {
+        host_pool_run(n, fn);
+    });
     if (!err.empty()) return set_err(h, LPC_E_ARG, err);
     if (h->host_prof)
         fprintf(stderr, "[lpc host] scene records %.1f us (%zu nodes, %zu slivers, %d threads)\n", host_us() - t0,
@@ -429,35 +440,45 @@ static int build_records(lpc_handle *h)
     // the walk stages them into LDS with one LDS-DMA load), each with its
     // triangle index; 8 spare records at the end, so the last leaf's load stays
     // inside the buffer (round 6; by triangle index before, A/B neutral)
+    // (k_exact_records from the rows on the device and the leaf order)
     const double tb0 = h->host_prof ? host_us() : 0.0;
     const size_t nx = out.xorder.size();
-    std::vector<ExactRec> xr(nx + 8);
-    memset(xr.data() + nx, 0, 8 * sizeof(ExactRec));
-    host_parts((int64_t)nx, host_threads(), [&](int64_t lo, int64_t hi, int) {
-        for (int64_t p = lo; p < hi; ++p) {
-            const int32_t i = out.xorder[(size_t)p];
-            const float *a = &h->hv0[4 * (size_t)i], *b = &h->hv1[4 * (size_t)i], *c = &h->hv2[4 * (size_t)i];
-            ExactRec &x = xr[(size_t)p];
-            x.v0x = a[0]; x.v0y = a[1]; x.v0z = a[2];
-            x.e1x = b[0] - a[0]; x.e1y = b[1] - a[1]; x.e1z = b[2] - a[2];
-            x.e2x = c[0] - a[0]; x.e2y = c[1] - a[1]; x.e2z = c[2] - a[2];
-            x.idx = i;
-            x.pad1 = x.pad2 = 0.0f;
-        }
-    });
+    RETIF(dalloc(h, h->d_xrec, (nx + 8) * sizeof(ExactRec)));
+    RETIF(dalloc(h, h->d_tmp, std::max<size_t>(nx, 1) * 4));
+    if (nx) HIPCHK(h, hipMemcpy(h->d_tmp.p, out.xorder.data(), nx * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemsetAsync((ExactRec *)h->d_xrec.p + nx, 0, 8 * sizeof(ExactRec), h->stream));
+    if (nx) {
+        const float4 *raw = (const float4 *)h->d_raw.p;
+        hipLaunchKernelGGL(k_exact_records, dim3(grid1((int64_t)nx)), dim3(256), 0, h->stream, (int64_t)nx,
+                           (const int32_t *)h->d_tmp.p, raw, raw + h->M, raw + 2 * (size_t)h->M,
+                           (ExactRec *)h->d_xrec.p);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));      // d_tmp is reused
     const double tb1 = h->host_prof ? host_us() : 0.0;
-    RETIF(dalloc(h, h->d_xrec, xr.size() * sizeof(ExactRec)));
-    const double tb2 = h->host_prof ? host_us() : 0.0;
-    HIPCHK(h, hipMemcpy(h->d_xrec.p, xr.data(), xr.size() * sizeof(ExactRec), hipMemcpyHostToDevice));
-    const double tb3 = h->host_prof ? host_us() : 0.0;
     RETIF(dalloc(h, h->d_nodes, out.nodes.size() * sizeof(Node8)));
     RETIF(dalloc(h, h->d_srec, out.slivers.size() * sizeof(SliverRec)));
     HIPCHK(h, hipMemcpy(h->d_nodes.p, out.nodes.data(), out.nodes.size() * sizeof(Node8), hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_srec.p, out.slivers.data(), out.slivers.size() * sizeof(SliverRec),
                         hipMemcpyHostToDevice));
     if (h->host_prof)
-        fprintf(stderr, "[lpc host] records upload: exact records %.1f us, alloc %.1f us, copy %.1f us, nodes %.1f us\n",
-                tb1 - tb0, tb2 - tb1, tb3 - tb2, host_us() - tb3);
+        fprintf(stderr, "[lpc host] records upload: exact records %.1f us, nodes %.1f us\n", tb1 - tb0, host_us() - tb1);
+    return 0;
+}
+
+// Host copies of the scene's rows, from the device (a filter-record rebuild or
+// the profiling fan flags after lpc_scene_upload returned).
+static int host_vertices(lpc_handle *h)
+{
+    if (h->hv0.size() != 4 * (size_t)h->M) {
+        std::vector<float> *hv[3] = {&h->hv0, &h->hv1, &h->hv2};
+        for (int k = 0; k < 3; ++k) {
+            hv[k]->resize(4 * (size_t)h->M);
+            HIPCHK(h, hipMemcpy(hv[k]->data(), (const float *)h->d_raw.p + (size_t)k * 4 * h->M, (size_t)h->M * 16,
+                                hipMemcpyDeviceToHost));
+        }
+    }
+    for (int k = 0; k < 3; ++k) h->src_v[k] = (k == 0 ? h->hv0 : k == 1 ? h->hv1 : h->hv2).data();
     return 0;
 }
 
@@ -699,6 +720,7 @@ static int spill_setup(lpc_handle *h, int64_t n, SpillArgs *SP)
     *SP = SpillArgs{nullptr, nullptr, 0u, 0, 31, h->tm_cur, nullptr};
     if (h->prof_stats) {                // diagnostic: the fan triangles (apex valence >= 32), built once
         if (!h->d_fan.p) {
+            RETIF(host_vertices(h));
             std::map<std::array<uint32_t, 3>, int32_t> val;
             auto key = [&](const std::vector<float> &v, int32_t i) {
                 std::array<uint32_t, 3> k;
@@ -1358,7 +1380,7 @@ int lpc_close(lpc_handle *h)
     if (h->ev_stage) (void)hipEventDestroy(h->ev_stage);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    DBuf *bufs[] = {&h->d_nodes, &h->w_pk, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
+    DBuf *bufs[] = {&h->d_raw, &h->d_nodes, &h->w_pk, &h->d_xrec, &h->d_verts, &h->d_mat, &h->d_ior, &h->d_refl,
                     &h->d_diss, &h->w_key, &h->w_sc, &h->w_rs, &h->d_live,
                     &h->w_shf, &h->w_shi, &h->w_blk_cnt, &h->w_blk_off, &h->w_blk_pow, &h->w_soa,
                     &h->w_stage, &h->w_sort, &h->w_sort_tmp, &h->w_bhist, &h->d_srec, &h->A.buf, &h->B.buf, &h->T.buf, &h->I.buf, &h->m_buf,
@@ -1422,9 +1444,15 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
             return set_err(h, LPC_E_ARG, "mesh_id[" + std::to_string(i) + "] out of range");
     h->M = M; h->K = K;
     dfree(h->d_fan);                                // profiling flags of the previous scene
-    h->hv0.assign(v0, v0 + 4 * (size_t)M);
-    h->hv1.assign(v1, v1 + 4 * (size_t)M);
-    h->hv2.assign(v2, v2 + 4 * (size_t)M);
+    // the rows go to the device as they are (the vertex and exact records are
+    // built there); the host reads the caller's arrays during this call and keeps
+    // no copy (host_vertices fetches one for a later rebuild)
+    h->hv0.clear(); h->hv1.clear(); h->hv2.clear();
+    h->src_v[0] = v0; h->src_v[1] = v1; h->src_v[2] = v2;
+    RETIF(dalloc(h, h->d_raw, (size_t)M * 48));
+    for (int k = 0; k < 3; ++k)
+        HIPCHK(h, hipMemcpyAsync((float *)h->d_raw.p + (size_t)k * 4 * M, k == 0 ? v0 : k == 1 ? v1 : v2,
+                                 (size_t)M * 16, hipMemcpyHostToDevice, h->stream));
     // runs of equal mesh_id and the slot each one flushes into (.cl:260-265, 286)
     h->run_lo.clear(); h->run_hi.clear();
     for (int32_t i = 0; i < M; ++i) {
@@ -1459,20 +1487,20 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
             h->mat_passive = false;
         if (mat_type[j] == 1 && !(refl[j] >= 0.0f && refl[j] <= 1.0f)) h->mat_passive = false;
     }
-    // vertices (the hit triangle's normal in the shading)
-    std::vector<float> vv((size_t)M * 9);
-    host_parts(M, host_threads(), [&](int64_t lo, int64_t hi, int) {
-        for (int64_t i = lo; i < hi; ++i) {
-            const float *a = v0 + 4 * (size_t)i, *b = v1 + 4 * (size_t)i, *c = v2 + 4 * (size_t)i;
-            for (int k = 0; k < 3; ++k) { vv[9 * (size_t)i + k] = a[k]; vv[9 * (size_t)i + 3 + k] = b[k]; vv[9 * (size_t)i + 6 + k] = c[k]; }
-        }
-    });
+    // vertices (the hit triangle's normal in the shading), from the rows on the device
+    RETIF(dalloc(h, h->d_verts, (size_t)M * 36));
+    {
+        const float4 *raw = (const float4 *)h->d_raw.p;
+        hipLaunchKernelGGL(k_vertex_rows, dim3(grid1(M)), dim3(256), 0, h->stream, (int64_t)M, raw, raw + M,
+                           raw + 2 * (size_t)M, (float *)h->d_verts.p);
+        HIPCHK(h, hipGetLastError());
+    }
     {   // scene box for the ray coherence key
         float lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (const std::vector<float> *vs : {&h->hv0, &h->hv1, &h->hv2})
+        for (const float *vs : {v0, v1, v2})
             for (int32_t i = 0; i < M; ++i)
                 for (int k = 0; k < 3; ++k) {
-                    const float v = (*vs)[4 * (size_t)i + k];
+                    const float v = vs[4 * (size_t)i + k];
                     if (std::isfinite(v)) { lo3[k] = std::min(lo3[k], v); hi3[k] = std::max(hi3[k], v); }
                 }
         double diag2 = 0.0;
@@ -1486,14 +1514,14 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     }
     h->dcap = h->dcap_init;
     const double tu1 = h->host_prof ? host_us() : 0.0;
-    RETIF(build_records(h));
+    const int brc = build_records(h);
+    h->src_v[0] = h->src_v[1] = h->src_v[2] = nullptr;     // the caller's arrays are theirs again
+    RETIF(brc);
     const double tu2 = h->host_prof ? host_us() : 0.0;
-    RETIF(dalloc(h, h->d_verts, vv.size() * 4));
     RETIF(dalloc(h, h->d_mat, (size_t)K * 4));
     RETIF(dalloc(h, h->d_ior, (size_t)K * 4));
     RETIF(dalloc(h, h->d_refl, (size_t)K * 4));
     RETIF(dalloc(h, h->d_diss, (size_t)K * 4));
-    HIPCHK(h, hipMemcpy(h->d_verts.p, vv.data(), vv.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_mat.p, mat_type, (size_t)K * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_ior.p, ior, (size_t)K * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->d_refl.p, refl, (size_t)K * 4, hipMemcpyHostToDevice));
@@ -1506,16 +1534,90 @@ int lpc_scene_upload(lpc_handle *h, int32_t tri_count, const float *v0, const fl
     return 0;
 }
 
+// The process's host worker threads (host_threads() - 1 of them beside the
+// caller), created at first use and kept: a thread start costs tens of us on
+// the GPU boxes, which a scene upload or a ray pass would otherwise pay per call.
+// One caller at a time; a concurrent caller (a staging helper thread) runs its
+// tasks itself.
+namespace {
+class HostPool {
+public:
+    explicit HostPool(int workers)
+    {
+        for (int k = 0; k < workers; ++k) th_.emplace_back([this]() { loop(); });
+    }
+    ~HostPool()
+    {
+        { std::lock_guard<std::mutex> lk(m_); stop_ = true; }
+        cv_.notify_all();
+        for (std::thread &t : th_) t.join();
+    }
+    void run(int n, const std::function<void(int)> &fn)
+    {
+        std::unique_lock<std::mutex> busy(call_, std::try_to_lock);
+        if (!busy.owns_lock() || th_.empty() || n <= 1) {
+            for (int i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &fn;
+            n_ = n;
+            next_.store(0);
+            active_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (int i; (i = next_.fetch_add(1)) < n;) fn(i);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this]() { return active_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)> *job;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&]() { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+                n = n_;
+            }
+            for (int i; (i = next_.fetch_add(1)) < n;) (*job)(i);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--active_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_, call_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    int n_ = 0, active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    std::atomic<int> next_{0};
+};
+}  // namespace
+
+static void host_pool_run(int n, const std::function<void(int)> &fn)
+{
+    static HostPool pool(std::max(0, host_threads() - 1));
+    pool.run(n, fn);
+}
+
 // Host passes over the caller's rays (set_rays, bounce_host) split over threads:
 // fn(lo, hi, part) for T contiguous parts, results combined by the caller in
 // part order (so every combine is deterministic).
 static void host_parts(int64_t n, int T, const std::function<void(int64_t, int64_t, int)> &fn)
 {
     if (T <= 1 || n < (1 << 16)) { fn(0, n, 0); return; }
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back([&, t]() { fn(n * t / T, n * (t + 1) / T, t); });
-    fn(0, n / T, 0);
-    for (auto &x : th) x.join();
+    host_pool_run(T, [&](int t) { fn(n * t / T, n * (t + 1) / T, t); });
 }
 
 static int host_threads()

@@ -81,6 +81,24 @@ def flatten_meshes(meshes):
     return v0, v1, v2, mesh_id, mat_type, ior, refl, diss
 
 
+def array_digest(a):
+    """A 128-bit digest of an array's bytes, shape and dtype (xxh3; without the
+    xxhash module, a copy of the array stands in for it): the scene and mesh
+    caches compare these instead of keeping copies of the arrays."""
+    a = np.ascontiguousarray(a)
+    try:
+        import xxhash
+    except ImportError:
+        return (a.shape, a.dtype.str, a.copy())
+    return (a.shape, a.dtype.str, xxhash.xxh3_128_digest(a.view(np.uint8).reshape(-1)))
+
+
+def _same_digest(x, y):
+    if x[0] != y[0] or x[1] != y[1]:
+        return False
+    return np.array_equal(x[2], y[2]) if isinstance(x[2], np.ndarray) else x[2] == y[2]
+
+
 def default_device() -> int:
     for key in ("LPC_DEVICE", "LOCAL_RANK"):
         if os.environ.get(key, "") != "":
@@ -169,18 +187,18 @@ class Engine:
         # the same scene as the last upload (a tracer called again on its meshes,
         # as the reference's examples do): keep the device records, skip the
         # rebuild (the filter hierarchy is built on the host at every upload).
-        # Compared bit for bit with a kept copy (as integers: -0.0 is not 0.0).
+        # Compared by a digest of the bytes (-0.0 is not 0.0).
         arrs = (v0, v1, v2, mesh_id, mat_type, ior, refl, diss)
+        digest = tuple(array_digest(a) for a in arrs)
         last = getattr(self, "_scene_last", None)
-        if last is not None and all(a.shape == b.shape and np.array_equal(a.view(np.int32), b)
-                                    for a, b in zip(arrs, last)):
+        if last is not None and all(_same_digest(a, b) for a, b in zip(digest, last)):
             return
         self._scene_last = None
         self._c(self.L.lpc_scene_upload(self.h, M, ptr(v0), ptr(v1), ptr(v2), ptr(mesh_id), K,
                                         ptr(mat_type), ptr(ior), ptr(refl), ptr(diss)))
         self.tri_count, self.mesh_count = M, K
         self.mat_type = mat_type
-        self._scene_last = tuple(np.array(a, copy=True).view(np.int32) for a in arrs)
+        self._scene_last = digest
 
     def upload_meshes(self, meshes):
         arrs = flatten_meshes(meshes)

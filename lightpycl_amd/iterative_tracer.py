@@ -33,7 +33,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from . import _lib
-from .engine import Engine, flatten_meshes, select_device
+from .engine import Engine, _same_digest, array_digest, flatten_meshes, select_device
 
 
 def f32_sorted_sum(a):
@@ -101,11 +101,11 @@ class CL_Tracer:
     def _flatten(self, meshes):
         """flatten_meshes(meshes), reused when this tracer last flattened the same
         mesh objects and their vertex / triangle tables and materials still hold
-        the same bits (compared with kept copies); meshes whose tables are not
-        numpy arrays are flattened every time."""
+        the same bits (compared by digests of the tables); meshes whose tables are
+        not numpy arrays are flattened every time."""
         def bits(a):
             a = np.ascontiguousarray(a)
-            return a.view(f"u{a.itemsize}") if a.dtype.kind in "fiu" and a.itemsize in (1, 2, 4, 8) else None
+            return array_digest(a) if a.dtype.kind in "fiu" and a.itemsize in (1, 2, 4, 8) else None
 
         def mat(m):
             b = m.getMaterialBuf()
@@ -117,12 +117,11 @@ class CL_Tracer:
             for m, (mid, v, t, mt) in zip(meshes, cache[0]):
                 V, T = getattr(m, "vertices", None), getattr(m, "triangles", None)
                 if (id(m) != mid or type(V) is not np.ndarray or type(T) is not np.ndarray or
-                        V.shape != v.shape or T.shape != t.shape or mat(m) != mt):
+                        V.shape != v[0] or T.shape != t[0] or mat(m) != mt):
                     same = False
                     break
                 bv, bt = bits(V), bits(T)
-                if bv is None or bt is None or bv.dtype != v.dtype or bt.dtype != t.dtype or \
-                        not np.array_equal(bv, v) or not np.array_equal(bt, t):
+                if bv is None or bt is None or not _same_digest(bv, v) or not _same_digest(bt, t):
                     same = False
                     break
             if same:
@@ -136,7 +135,7 @@ class CL_Tracer:
             if bv is None or bt is None:
                 keep = None
                 break
-            keep.append((id(m), bv.copy(), bt.copy(), mat(m)))
+            keep.append((id(m), bv, bt, mat(m)))
         self._flat_cache = (keep, arrs) if keep is not None else None
         return arrs
 

@@ -38,9 +38,18 @@ extern "C" int sbp_build(const float *v0, const float *v1, const float *v2, cons
     in.dcap = dcap; in.scene_scale = scene_scale; in.thin_k = 1.0; in.stack_max = 64;
     double best = 1e30;
     SceneBuildOut out;
+    // tasks taken in index order by `threads` spawned threads
+    const ParFor parfor = [threads](int n, const std::function<void(int)> &fn) {
+        std::atomic<int> next(0);
+        auto w = [&]() { for (int i; (i = next.fetch_add(1)) < n;) fn(i); };
+        std::vector<std::thread> th;
+        for (int k = 1; k < threads; ++k) th.emplace_back(w);
+        w();
+        for (std::thread &x : th) x.join();
+    };
     for (int r = 0; r < reps; ++r) {
         const auto t0 = std::chrono::steady_clock::now();
-        const std::string err = build_scene_records(in, out, threads);
+        const std::string err = build_scene_records(in, out, parfor);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (!err.empty()) return -1;
         best = ms < best ? ms : best;
