@@ -2,9 +2,11 @@
 
 The drop-in's results mode hands the caller numpy arrays (the reference's
 per-iteration results tuples, iterative_tracer.py:335-355).  They live in
-page-locked memory so that the device-to-host copy of an iteration is one DMA
-on the export stream that overlaps the next iteration's kernels
-(lpc_trace_iterate_export).  Pinning pages costs milliseconds per tens of MB,
+page-locked, device-mapped memory so that the copy of an iteration to the host
+runs on the export stream beside the next iteration's kernels
+(lpc_trace_iterate_export: a copy kernel writing the mapped block over PCIe,
+since round 5; a DMA for a block the device cannot map).  Pinning pages costs
+milliseconds per tens of MB,
 so blocks are recycled: a block returns to the pool when the last numpy array
 viewing it is garbage-collected (the arrays keep the block alive through their
 ``base``), and the next trace of a similar size reuses it.
@@ -64,19 +66,24 @@ class PinnedPool:
             if ptr is not None:
                 self._idle -= size
         if ptr is None:
-            # an empty size class: pin two blocks, one now and one spare -- a caller
-            # that keeps the previous call's results alive (comparing or storing
-            # them) needs two sets in turn, and pinning on the next call would cost
-            # it milliseconds
+            # an empty size class: pin the block and, when it fits under keep_bytes,
+            # a spare -- a caller that keeps the previous call's results alive (the
+            # tracer's own .results, until its next call replaces them) needs two
+            # sets in turn, and pinning on the next call would cost that call
+            # milliseconds.  A spare that would not fit is
+            # not pinned at all (it would be unpinned at once)
             L = _lib.load()
+            with self._lock:
+                spare = self._idle + size <= self.keep_bytes
             got = []
-            for _ in range(2):
+            for _ in range(2 if spare else 1):
                 p = ctypes.c_void_p()
                 _lib.check(L.lpc_host_alloc(size, ctypes.byref(p)), None)
                 got.append(p.value)
                 self.allocated += 1
             ptr = got[0]
-            self._put(got[1], size)
+            if spare:
+                self._put(got[1], size)
         arr = (ctypes.c_char * size).from_address(ptr)
         arr._owner = _Owner(self, ptr, size)
         return arr

@@ -33,15 +33,29 @@ def _free_port():
     return p
 
 
+def _scene(name, n):
+    """The named scene; "neg_mirror": cube_field's mirrors with reflectivity -0.5
+    (the reference's mirror child carries P * R, .cl:443: a negative R flips the
+    sign, so a rank's power left can grow from one iteration to the next -- the
+    sharded trace must not stop a rank on a local bound then)."""
+    from lightpycl_amd import scenes
+    if name == "neg_mirror":
+        sc = scenes.cube_field(n=n, seed=2, count=150)
+        for m in sc.meshes[1:]:
+            if m.getMaterialBuf()["type"] == 1:
+                m.reflectivity = -0.5
+        return sc
+    return scenes.BUILDERS[name](n=n, seed=2)
+
+
 def _child(rank, world, port, name, n, hook, out_path):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from lightpycl_amd import scenes
     from lightpycl_amd.distributed import ShardedTrace, ShmComm, TorchComm, shard_bounds
     from lightpycl_amd.engine import Engine
-    sc = scenes.BUILDERS[name](n=n, seed=2)
+    sc = _scene(name, n)
     o = np.asarray(sc.sources[0].rays_origin, np.float32)
     d = np.asarray(sc.sources[0].rays_dir, np.float32)
     p = np.asarray(sc.sources[0].rays_power, np.float32).reshape(-1)
@@ -81,7 +95,7 @@ def _child(rank, world, port, name, n, hook, out_path):
 
 
 @pytest.mark.parametrize("name,n,hook", [("synthetic", 20000, "shm"), ("lens", 20000, "shm"),
-                                         ("lens", 9000, "gloo")])
+                                         ("lens", 9000, "gloo"), ("neg_mirror", 12000, "shm")])
 def test_sharded_trace_two_processes(oracle_mod, checker, tmp_path, name, n, hook):
     import torch.multiprocessing as mp
     from lightpycl_amd import scenes
@@ -93,7 +107,7 @@ def test_sharded_trace_two_processes(oracle_mod, checker, tmp_path, name, n, hoo
     with open(os.path.join(ROOT, "gpurun_out", "sharded.jsonl"), "a") as f:
         f.write(json.dumps(dict(scene=name, n=n, hook=hook, calls=got["xchg_calls"],
                                 us_per_exchange=got["xchg_us"] / max(got["xchg_calls"], 1))) + "\n")
-    sc = scenes.BUILDERS[name](n=n, seed=2)
+    sc = _scene(name, n)
     res, info = oracle_mod.trace(sc.sources, sc.meshes, sc.iterations, sc.tau, sc.max_ray_len, sc.ior_env,
                                  bounce_fn=checker[0])
     assert got["counts"] == info["counts"]

@@ -18,6 +18,7 @@ freshab) for p in 1 2; do for m in 0 1 2; do LPC_STAGE_MODE=$m run 300 fresh_m${
          for m in 0 1 2; do LPC_HOSTPROF=1 LPC_STAGE_MODE=$m run 300 fresh_hp_m$m.json python -u tools/fresh_probe.py; done ;;
 fresh) LPC_HOSTPROF=${HP:-0} run 300 fresh.json python -u tools/fresh_probe.py ;;
 stream) run 600 pytest_stream.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_stream.py ;;
+dispatch) run 120 dispatch.json tools/_dispatch_probe ;;
 quick) run 300 quick.json python -u bench.py --no-cpu --no-configs --no-strong ;;
 bench) run 900 bench.json python -u bench.py ;;
 ab) AB_STEPS=${AB_STEPS:-300} run 900 ab.log python -u tools/ab.py ${AB_REPS:-3} $AB_CFGS ;;
