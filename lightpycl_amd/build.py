@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "lpc_runtime.hip")
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("lpc_runtime.hip", "lpc_kernels.hip", "lpc_math.hpp",
-                                               "lpc_internal.hpp", "lpc_comm.hpp")] + [os.path.join(ROOT, "include", "lpc.h")]
+                                               "lpc_internal.hpp", "lpc_comm.hpp", "lpc_build.hpp")] + [os.path.join(ROOT, "include", "lpc.h")]
 OUT = os.path.join(HERE, "liblpc.so")
 ARCH = os.environ.get("LPC_ARCH", "gfx950")
 
