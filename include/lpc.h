@@ -198,8 +198,9 @@ int lpc_trace_rerun_async(lpc_handle *h, int32_t max_iter, double power_threshol
 /* The reference uploads each partition's rays inside its loop
  * (iterative_tracer.py:280-284) and its examples trace batch after batch of new
  * sources.  lpc_trace_stage_rays queues the next batch (at most two staged): a
- * helper thread copies the caller's (n,4) rows and power into pinned staging and
- * DMAs them to the device on a copy stream, with the emitted rays' analysis,
+ * helper thread copies the caller's (n,4) rows and power to the device on a copy
+ * stream (straight from the caller's memory; DESIGN.md section 7f measured the
+ * pinned-staging variants slower) and runs the emitted rays' analysis there,
  * while the handle traces the batch before it.  The caller's arrays must stay
  * valid and unchanged until the lpc_trace_run_staged_async that traces the batch
  * returns.  lpc_trace_run_staged_async makes the oldest staged batch the emitted
