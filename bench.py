@@ -47,6 +47,7 @@ import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -110,6 +111,9 @@ def parse():
     ap.add_argument("--strong-steps", type=int, default=100, help="timed steps of the strong-scaling block")
     ap.add_argument("--c5-steps", type=int, default=5, help="timed traces of the config-5 block")
     ap.add_argument("--c5-rays", type=int, default=100_000_000, help="config 5: global rays (8 blocks)")
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("LPC_BENCH_INFLIGHT", 3)),
+                    help="traces in flight per GPU: engines (handles, each its own stream) tracing the "
+                         "workload's rays from their own host threads (1: one engine, traces back to back)")
     return ap.parse_args()
 
 
@@ -603,62 +607,124 @@ def main():
     from lightpycl_amd.distributed import ShardedTrace, ShmComm, TorchComm
 
     sc = scenes.synthetic(n=a.rays, seed=7 + rank)
-    eng = Engine(local)
-    eng.upload_meshes(sc.meshes)
+    E = max(1, int(a.inflight))
     o, d, p = rays_of(sc)
-    eng.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
-    in_pow = float(np.sum(p, dtype=np.float64))
     comm = TorchComm(dist, local) if dist else None
-    # per-iteration exchange: the library's shared-memory hook on one node,
+    # E engines (traces in flight), each with the scene and the workload's rays,
+    # its own stream and, over several ranks, its own per-iteration exchange: the
+    # library's shared-memory hook on one node (one segment per engine),
     # torch.distributed through the hook when the ranks span nodes
-    shm = ShmComm.from_dist(dist, fallback=comm) if dist else None
-    runner = ShardedTrace(eng, comm, iter_comm=shm)
+    engines, shms, runners = [], [], []
+    for _ in range(E):
+        e = Engine(local)
+        e.upload_meshes(sc.meshes)
+        e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+        s_ = ShmComm.from_dist(dist, fallback=comm) if dist else None
+        engines.append(e)
+        shms.append(s_)
+        runners.append(ShardedTrace(e, comm, iter_comm=s_))
+    eng, shm, runner = engines[0], shms[0], runners[0]
+    in_pow = float(np.sum(p, dtype=np.float64))
     in_pow_all = float(comm.allreduce_sum([in_pow])[0]) if comm else in_pow
 
-    def step():
-        # the trace returns once its outputs are final, so the next step's launches
-        # queue behind its last row moves (sync() waits for all)
-        return runner.run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_pow_all, reset=True)
+    def step(j=0):
+        # the trace returns once its outputs are final, so the engine's next step's
+        # launches queue behind its last row moves (sync() waits for all)
+        return runners[j].run(sc.iterations, sc.tau, in_pow, wait=False, input_power_global=in_pow_all,
+                              reset=True)
 
     def sync():
-        eng.sync()
+        for e in engines:
+            e.sync()
         if dist:
             import torch
             torch.cuda.synchronize(local)
             dist.barrier()
+
+    def steps_inflight(n):
+        """n steps over the E engines, each engine's share in order on a host
+        thread of its own (ctypes releases the GIL inside the library calls), so
+        up to E traces run on the GPU at once.  Returns every step's result."""
+        share = [n // E + (1 if j < n % E else 0) for j in range(E)]
+        out = [[] for _ in range(E)]
+        errs = []
+
+        def worker(j):
+            try:
+                for _ in range(share[j]):
+                    out[j].append(step(j))
+            except BaseException as ex:          # re-raised on the main thread
+                errs.append(ex)
+        if E == 1:
+            worker(0)
+        else:
+            th = [threading.Thread(target=worker, args=(j,)) for j in range(E)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if errs:
+            raise errs[0]
+        return [r for rs in out for r in rs]
 
     # the first iteration alone, for the parity leg (same stats the timed trace starts with)
     eng.reset()
     st0, _ = eng.iterate()
     first = {"stats": st0, "population": p}
     eng.sync()
-    for _ in range(a.warmup):
-        step()
+    for j in range(E):
+        for _ in range(a.warmup):
+            step(j)
     if not a.no_prof:
         # HIP events around the walk kernel's launches only (created without the
         # system-scope fence, which cost ~7 us per launch; PROF_EVERY > 1 samples
-        # every k-th launch)
-        eng.prof_enable(True, light=True, every=PROF_EVERY)
+        # every k-th launch), on every engine
+        for e in engines:
+            e.prof_enable(True, light=True, every=PROF_EVERY)
         # untimed: the same number of steps once with events, so the timed region
-        # takes its events from the pool instead of creating them
-        for _ in range(a.steps):
-            step()
-    eng.prof_read(reset=True)
+        # takes its events from the pools instead of creating them
+        steps_inflight(a.steps)
+    for e in engines:
+        e.prof_read(reset=True)
     sync()
     t0 = time.perf_counter()
-    bounces = 0
-    iters = 0
-    results = []
-    for _ in range(a.steps):
-        r = step()
-        bounces += r["bounces"]
-        iters += r["iterations"]
-        results.append((r["global_counts"], [float(x) for x in r["mesh_power"]]))
+    res = steps_inflight(a.steps)
     sync()
     dt = time.perf_counter() - t0
-    prof = eng.prof_read(reset=True)
-    eng.prof_enable(False)
+    bounces = sum(r["bounces"] for r in res)
+    iters = sum(r["iterations"] for r in res)
+    results = [(r["global_counts"], [float(x) for x in r["mesh_power"]]) for r in res]
+    profs = [e.prof_read(reset=True) for e in engines]
+    prof = {k: sum(pr[k] for pr in profs) for k in ("kernel_ms", "intersect_launches", "xchg_us", "xchg_calls")}
+    for e in engines:
+        e.prof_enable(False)
     steps_identical = all(x == results[0] for x in results)
+    # the same steps on one engine, back to back (the per-trace time without
+    # overlap; beside the headline, not a separate workload)
+    seq = None
+    if E > 1:
+        for _ in range(3):
+            step(0)
+        sync()
+        t1 = time.perf_counter()
+        rs = [step(0) for _ in range(a.steps)]
+        sync()
+        dts = time.perf_counter() - t1
+        if dist:
+            import torch
+            dv = "cpu" if rehearse else f"cuda:{local}"
+            tt = torch.tensor([dts], dtype=torch.float64, device=dv)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dts = float(tt[0])
+        bs = float(sum(r["bounces"] for r in rs))
+        if dist:
+            import torch
+            tb = torch.tensor([bs], dtype=torch.float64, device=("cpu" if rehearse else f"cuda:{local}"))
+            dist.all_reduce(tb, op=dist.ReduceOp.SUM)
+            bs = float(tb[0])
+        seq = {"ray_bounces_per_s": bs / dts, "ms_per_step": dts / a.steps * 1e3, "steps": a.steps,
+               "identical_to_inflight": all((r["global_counts"], [float(x) for x in r["mesh_power"]]) == results[0]
+                                            for r in rs)}
     # trace-end histogram over RCCL (the north star's all-reduce), outside the timed region
     eng.reset()
     hr = runner.run(sc.iterations, sc.tau, in_pow, hist=(sc.hist_limits, sc.hist_points),
@@ -704,9 +770,11 @@ def main():
     else:
         bounces_all = float(bounces)
     def finish():
-        runner.close()                          # the hook out of the engine before its comm closes
-        if isinstance(shm, ShmComm):
-            shm.close()
+        for r_ in runners:
+            r_.close()                          # the hook out of the engine before its comm closes
+        for s_ in shms:
+            if isinstance(s_, ShmComm):
+                s_.close()
         if dist:
             dist.destroy_process_group()
 
@@ -748,6 +816,12 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": dt / a.steps * 1e3,
+        "inflight": {"traces_in_flight_per_gpu": E,
+                     "note": "the timed steps run on E engines (liblpc handles, each its own HIP stream, scene "
+                             "records and copy of the workload's rays) from E host threads, so up to E traces "
+                             "of the same workload share the GPU; every step is a whole trace of the 1 M rays "
+                             "(counts and per-mesh power identical in every step); ms_per_step = wall time / "
+                             "steps", "sequential": seq},
         "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
         "rank_ray_bounces_per_step": [b / a.steps for b in rank_b],
         "higher_is_better": True,
@@ -758,7 +832,8 @@ def main():
         "config": {"workload": f"synthetic compound scene: measure hemisphere + 9 refractive spheres, "
                                f"{M} triangles, {a.rays} rays per GPU, trace to termination",
                    "rays_per_gpu": a.rays, "triangles": int(M), "meshes": int(eng.mesh_count),
-                   "parallelism": f"ray-sharded x{world}", "iterations_per_step": iters / a.steps},
+                   "parallelism": f"ray-sharded x{world}, {E} traces in flight per GPU",
+                   "iterations_per_step": iters / a.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": WALK_KERNEL, "avg_launch_ms": avg_ms,
@@ -767,7 +842,9 @@ def main():
                      "traffic_by_bounce": split,
                      "note": f"achieved = algorithmic bytes per launch (156 B x rays + 40 B x triangles) / "
                              f"{WALK_KERNEL}'s own average launch time (HIP events on its stream over the "
-                             f"timed region, launches_timed of launches_all); traffic = "
+                             f"timed region, launches_timed of launches_all; with traces in flight the "
+                             f"launches of different engines overlap, so this per-launch figure understates "
+                             f"the chip's aggregate rate); traffic = "
                              f"2*FETCH_SIZE+WRITE_SIZE per {WALK_KERNEL} launch from profiles/pmc_intersect.json "
                              f"(null when that summary was collected on other kernel sources)"},
         # the bound that actually limits the walk kernel: executed VALU issue
@@ -812,8 +889,10 @@ def main():
                                        f"(seeds 7..{6 + C5_BLOCKS}) over {world} rank(s)")
     out["weak_global_counts"] = [int(x) for x in hr["global_counts"]]
     if world == 1 and not a.no_configs:
-        runner.close()
-        eng.close()
+        for r_ in runners:
+            r_.close()
+        for e in engines:
+            e.close()
         out["configs"] = run_configs(Engine, ShardedTrace, scenes)
         out["cold"] = cold_block(scenes, Engine, ShardedTrace, a.rays)
         out["fresh_rays"] = fresh_rays_block(scenes, Engine, a.rays)

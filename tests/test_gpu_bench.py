@@ -2,7 +2,9 @@
 with no WORLD_SIZE starts N ranks itself (torch.distributed.run as a child
 process).  On the one-GPU test box LPC_BENCH_REHEARSE=1 puts both ranks on GPU 0
 (gloo for the trace-end exchange); the line must say n_gpus == 2, carry both
-ranks' times, and every timed step must give identical counts.  The strong
+ranks' times, and every timed step must give identical counts -- the timed steps
+run with three traces in flight per rank (three engines, three shared-memory
+exchange segments), checked against the same steps on one engine.  The strong
 block (one fixed global ray set split with shard_bounds) and the config-5 block
 (fixed ray blocks split over the ranks) must give the global per-iteration
 counts of the N = 1 trace of the same rays (the reference's global termination,
@@ -42,6 +44,10 @@ def test_bench_gpus2_launches_two_ranks():
     assert out["rank_ms_per_step"]["max"] == pytest.approx(out["ms_per_step"], rel=1e-9)
     assert out["exchange"]["rehearsal_one_gpu"] is True
     assert out["value"] > 0
+    # the timed steps ran with traces in flight (three engines per rank), and the
+    # same steps back to back on one engine gave the same counts and power
+    assert out["inflight"]["traces_in_flight_per_gpu"] == 3
+    assert out["inflight"]["sequential"]["identical_to_inflight"] is True
 
     one = _bench(1)
     for blk in ("strong", "config5"):
@@ -66,6 +72,7 @@ def test_bench_gpus8_rehearsal():
     the line, and the strong and config-5 blocks' global counts equal to N = 1."""
     out = _bench(8, ARGS8)
     assert out["n_gpus"] == 8 and out["parity"]["steps_identical"] is True
+    assert out["inflight"]["sequential"]["identical_to_inflight"] is True
     assert len(out["rank_ms_per_step"]["per_rank"]) == 8
     assert len(out["rank_ray_bounces_per_step"]) == 8 and min(out["rank_ray_bounces_per_step"]) > 0
     assert out["config5"]["rays_per_rank"] == 320000 // 8
