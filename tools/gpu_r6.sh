@@ -26,7 +26,7 @@ abcfg) run 900 abcfg.log python -u tools/ab_cfg.py $ABCFG_ARGS ;;
 stats) run 300 stats_synth.log python -u tools/trace_stats.py synthetic 1000000
        run 300 stats_dense.log python -u tools/trace_stats.py synthetic_dense 200000 ;;
 stats_eye) run 300 stats_eye.log python -u tools/trace_stats.py eye 300000 ;;
-kt) prof 300 --kernel-trace --stats -d $R/$O/kt -o kt --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-configs --no-strong > $O/kt.log 2>&1 || { echo kt failed; exit 1; }
+kt) prof 300 --kernel-trace --stats -d $R/$O/kt -o kt --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-configs --no-strong $KT_ARGS > $O/kt.log 2>&1 || { echo kt failed; exit 1; }
     python tools/kt_timeline.py $O/kt 60 > $O/timeline.txt; python tools/kt_steps.py $O/kt > $O/steps.txt ;;
 ktstats) prof 300 --kernel-trace --stats -d $R/$O/kts -o kts --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu --no-configs --no-strong > $O/kts.log 2>&1 || { echo ktstats failed; exit 1; } ;;
 pmcwalk) for grp in "$PMC1" "$PMC2" "$PMC3"; do [ -z "$grp" ] && continue; tag=$(echo $grp | md5sum | cut -c1-6)
