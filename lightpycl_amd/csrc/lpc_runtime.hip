@@ -157,8 +157,9 @@ struct lpc_handle {
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
-    int64_t sliver_merge = 4000000;                 // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
-                                                    // this population size (0: always; -1: never)
+    int64_t sliver_merge = 0;                       // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
+                                                    // this population size (0: always; -1: never,
+                                                    // k_slivers on the side stream)
     DBuf w_fc;                                      // k_shade_stage tile counts / power / max |dir|^2
     DBuf w_gsum;                                    // per 256-tile group counts, two buffers (zero when unused)
     int64_t gcap = 0;
@@ -1154,11 +1155,13 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // in the grid, culled there)
     const unsigned *dm2_dev = ds ? ds->dm2 : nullptr;
     const long long *nd_dev = ds ? ds->nd : nullptr;
-    // LPC_SLIVER_MERGE: from this population size the sliver units run in the
-    // walk's own grid (k_rootwalk's tail) on this stream; below, k_slivers runs
-    // beside the hierarchy stage on a second stream (both only add to the slots
-    // with order-independent atomics; joined at the end), launched after the
-    // hierarchy stage's kernels (the host reaches k_roots_s / k_rootwalk sooner)
+    // LPC_SLIVER_MERGE: from this population size (default 0: every size) the
+    // sliver units run in the walk's own grid (k_rootwalk's tail) on this stream;
+    // below, k_slivers runs beside the hierarchy stage on a second stream (both
+    // only add to the slots with order-independent atomics; joined at the end),
+    // launched after the hierarchy stage's kernels (the host reaches k_roots_s /
+    // k_rootwalk sooner).  One stream per trace keeps several traces in flight
+    // from interleaving fork / join events
     const bool merge_try = h->sliver_merge >= 0 && n >= h->sliver_merge && nsp > 0 && pt->npieces > 0;
     const bool side = !merge_try && nsp > 0 && h->stream2 && h->ev_side[0];
     hipStream_t ss = h->stream;

@@ -97,8 +97,10 @@ _POLICIES = [
     dict(LPC_BUDGET="0", LPC_HALF="0"), dict(LPC_BUDGET="3", LPC_SPILL_CAP="3000"),
     # no hand-over from 0 rays per triangle (always) / hand-over at every size
     dict(LPC_LARGE_PER_TRI="0"), dict(LPC_LARGE_PER_TRI="1000000", LPC_BUDGET="3"),
-    # slivers in the walk's grid (k_rootwalk's tail) at every size
-    dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="0", LPC_BUDGET="2", LPC_SPILL_CAP="100"),
+    # slivers on the side stream (k_slivers beside the walk) at every size; below
+    # 4 M rays only; the default runs them in the walk's grid at every size
+    dict(LPC_SLIVER_MERGE="-1"), dict(LPC_SLIVER_MERGE="-1", LPC_BUDGET="2", LPC_SPILL_CAP="100"),
+    dict(LPC_SLIVER_MERGE="4000000"),
     # a filter-record rebuild below the emitted |D| (Dcap 0.5: unit directions exceed it)
     dict(LPC_DCAP_MILLI="500"),
 ]
@@ -525,13 +527,14 @@ def test_population_paths_match_reference(oracle_mod, exact_ref, monkeypatch, na
     assert_aggregate_equal(lib, ref, f"{name} {env}")
 
 
-@pytest.mark.parametrize("cfg", [dict(), dict(LPC_SLIVER_MERGE="0"), dict(LPC_SLIVER_MERGE="-1"),
-                                 dict(LPC_SLIVER_MERGE="0", LPC_RESORT_MIN="4096"), dict(LPC_RESORT_MIN="4096")])
+@pytest.mark.parametrize("cfg", [dict(), dict(LPC_SLIVER_MERGE="4000000"), dict(LPC_SLIVER_MERGE="-1"),
+                                 dict(LPC_SLIVER_MERGE="-1", LPC_RESORT_MIN="4096"), dict(LPC_RESORT_MIN="4096")])
 def test_eye_results_mode_policies_match_reference(oracle_mod, exact_ref, monkeypatch, cfg):
     """The eye (thin triangles on the sliver path), results mode: every results
     tuple element for element equals the reference host loop over the
     reference's kernels, with the sliver units merged into the walk's grid at
-    every size / never, and re-sorted chained populations."""
+    every size (the default) / from 4 M rays / never, and re-sorted chained
+    populations."""
     from lightpycl_amd.iterative_tracer import CL_Tracer
     if exact_ref is None:
         pytest.skip("oracle/_ref not built")
