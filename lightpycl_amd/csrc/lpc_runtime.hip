@@ -207,6 +207,7 @@ struct lpc_handle {
     int host_prof = 0;                              // LPC_HOSTPROF: host-side timing of each iteration (stderr);
                                                     //   2: also each launch's hand-over queue lengths (synchronising)
     hipStream_t stream2 = nullptr;                  // side stream: the sliver kernels beside the hierarchy stage
+    bool side_tried = false;                        // stream2 / ev_side created on first use (side_stream)
     // results export (lpc_trace_iterate_export): k_export packs a chunk's part of
     // the results tuple into xst[par] on the main stream, the export stream copies
     // it to the caller's host block while the next kernels run
@@ -987,6 +988,28 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
 // ds != NULL (a speculative trace iteration, chained traced population): n is
 // the bound, the kernels read the population size on the device and the
 // launch shapes follow ds->pred.
+// the side stream of the sliver kernels and its fork / join events, created on
+// first use (a handle whose slivers run in the walk's grid holds one stream, so
+// several handles in flight each keep a hardware queue of their own); false:
+// all on the main stream
+static bool side_stream(lpc_handle *h)
+{
+    if (!h->side_tried) {
+        h->side_tried = true;
+        const unsigned evf = hipEventDisableTiming;
+        if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
+            (void)hipGetLastError();
+            if (h->stream2) (void)hipStreamDestroy(h->stream2);
+            for (hipEvent_t &e : h->ev_side)
+                if (e) { (void)hipEventDestroy(e); e = nullptr; }
+            h->stream2 = nullptr;
+        }
+    }
+    return h->stream2 && h->ev_side[0] && h->ev_side[1];
+}
+
 static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_ray_len,
                          float *st_user, int32_t *si_user, int32_t *sc_user,
                          double dmax2 = INFINITY, RaysIn *traced = nullptr, const DevSize *ds = nullptr)
@@ -1163,7 +1186,7 @@ static int run_intersect(lpc_handle *h, const RaysIn &in, int64_t n, float max_r
     // k_rootwalk sooner).  One stream per trace keeps several traces in flight
     // from interleaving fork / join events
     const bool merge_try = h->sliver_merge >= 0 && n >= h->sliver_merge && nsp > 0 && pt->npieces > 0;
-    const bool side = !merge_try && nsp > 0 && h->stream2 && h->ev_side[0];
+    const bool side = !merge_try && nsp > 0 && side_stream(h);
     hipStream_t ss = h->stream;
     if (side) {
         ss = h->stream2;
@@ -1343,15 +1366,6 @@ int lpc_open(int device, lpc_handle **out)
     h->spill_cap = std::max<int64_t>(env_int("LPC_SPILL_CAP", h->spill_cap), 64);
     h->host_prof = (int)env_int("LPC_HOSTPROF", 0);
     h->stage_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, env_int("LPC_STAGE_MODE", h->stage_mode)));
-    {   // the side stream of the sliver kernels and its fork / join events
-        const unsigned evf = hipEventDisableTiming;
-        if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&h->ev_side[0], evf) != hipSuccess ||
-            hipEventCreateWithFlags(&h->ev_side[1], evf) != hipSuccess) {
-            h->stream2 = nullptr;       // all on the main stream
-            h->ev_side[0] = h->ev_side[1] = nullptr;
-        }
-    }
     if (hipHostMalloc((void **)&h->acc_map, kAccRing * sizeof(DevAcc), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
         hipHostGetDevicePointer((void **)&h->acc_map_dev, h->acc_map, 0) != hipSuccess) {
