@@ -614,11 +614,15 @@ def main():
     # its own stream and, over several ranks, its own per-iteration exchange: the
     # library's shared-memory hook on one node (one segment per engine),
     # torch.distributed through the hook when the ranks span nodes
+    # (in flight: the walk grid TracePool uses for engines side by side)
+    from lightpycl_amd.pool import INFLIGHT_WALK_GRID
     engines, shms, runners = [], [], []
     for _ in range(E):
         e = Engine(local)
         e.upload_meshes(sc.meshes)
         e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+        if E > 1:
+            e.set_walk_grid(INFLIGHT_WALK_GRID)
         s_ = ShmComm.from_dist(dist, fallback=comm) if dist else None
         engines.append(e)
         shms.append(s_)
@@ -703,6 +707,7 @@ def main():
     # overlap; beside the headline, not a separate workload)
     seq = None
     if E > 1:
+        eng.set_walk_grid(0)                    # one trace alone: the library default
         for _ in range(3):
             step(0)
         sync()
@@ -821,7 +826,9 @@ def main():
                              "records and copy of the workload's rays) from E host threads, so up to E traces "
                              "of the same workload share the GPU; every step is a whole trace of the 1 M rays "
                              "(counts and per-mesh power identical in every step); ms_per_step = wall time / "
-                             "steps", "sequential": seq},
+                             "steps; the engines' walk grid is walk_grid single-wave blocks (the sequential figure: one "
+                             "engine, the library default)",
+                     "walk_grid": INFLIGHT_WALK_GRID if E > 1 else None, "sequential": seq},
         "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
         "rank_ray_bounces_per_step": [b / a.steps for b in rank_b],
         "higher_is_better": True,

@@ -266,6 +266,12 @@ int lpc_trace_measured(lpc_handle *h, int64_t *count, double *mesh_power, int32_
 int lpc_trace_fetch_measured(lpc_handle *h, float *pos4, float *pow, int32_t *mesh);
 /* Rays per device chunk (0 = library default). */
 int lpc_set_chunk(lpc_handle *h, int64_t rays_per_chunk);
+/* Hierarchy-walk grid in single-wave blocks (64 .. 2^22; 0 = library default,
+ * 65 536).  A launch policy with no reference counterpart, results unchanged:
+ * handles that trace side by side on one GPU (lightpycl_amd.pool.TracePool,
+ * bench.py's traces in flight) run faster with 16 384, one trace alone with the
+ * default.  LPC_E_ARG out of range. */
+int lpc_set_walk_grid(lpc_handle *h, int64_t blocks);
 
 /* ---- trace-end projection + binning (iterative_tracer.py:503-562) -------- */
 /* angular_project (.cl:509-538) / stereograph_project (.cl:488-506) of n host

@@ -83,6 +83,7 @@ _PROTOS = {
     "lpc_trace_measured": [_P, _P, _P, _I32],
     "lpc_trace_fetch_measured": [_P, _P, _P, _P],
     "lpc_set_chunk": [_P, _I64],
+    "lpc_set_walk_grid": [_P, _I64],
     "lpc_project_hist": [_P, _INT, _I64, _P, _P, _P, _P, _P, _INT, _P, _INT, _F64, _P, _P, _P,
                          _P],
     "lpc_prof_enable": [_P, _INT],

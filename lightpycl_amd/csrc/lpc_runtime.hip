@@ -157,6 +157,7 @@ struct lpc_handle {
     bool acc_pending = false;                       // next slot reset also resets the iteration counters
     int64_t acc_pending_total = 0;
     int64_t m_inflight = 0;                         // populations of the iterations enqueued, not yet read
+    int64_t walk_grid = kWalkWaves;                 // k_rootwalk blocks (lpc_set_walk_grid, LPC_WALK_GRID)
     int64_t sliver_merge = 0;                       // LPC_SLIVER_MERGE: sliver units in k_rootwalk's grid from
                                                     // this population size (0: always; -1: never,
                                                     // k_slivers on the side stream)
@@ -945,7 +946,7 @@ static int run_queue(lpc_handle *h, const RaysIn &in, const float *rs, int64_t n
     RETIF(ray_base(h, in, rs, n, &ray));
     SpillArgs SP;
     RETIF(spill_setup(h, n, &SP));
-    const unsigned grid = (unsigned)kWalkWaves;        // single-wave blocks
+    const unsigned grid = (unsigned)h->walk_grid;      // single-wave blocks
     // profiling: the launch's own start/stop timestamps (hipExtLaunchKernel), no
     // event packets between the kernels
     hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -1359,6 +1360,7 @@ int lpc_open(int device, lpc_handle **out)
     h->chunk = std::max<int64_t>(0, env_int("LPC_CHUNK", h->chunk));
     h->resort_min = std::max<int64_t>(1, env_int("LPC_RESORT_MIN", h->resort_min));
     h->sliver_merge = env_int("LPC_SLIVER_MERGE", h->sliver_merge);
+    h->walk_grid = std::min<int64_t>(std::max<int64_t>(env_int("LPC_WALK_GRID", h->walk_grid), 64), 1 << 22);
     h->spec = env_int("LPC_SPEC", h->spec) != 0;
     h->dcap_init = (double)env_int("LPC_DCAP_MILLI", 16000) / 1000.0;
     h->spill_budget = (int)env_int("LPC_BUDGET", h->spill_budget);
@@ -1865,6 +1867,15 @@ int lpc_reflect_refract_rays(lpc_handle *h, int64_t n, const float *dev_origin4,
 }
 
 // ---- device-resident trace ------------------------------------------------------
+int lpc_set_walk_grid(lpc_handle *h, int64_t blocks)
+{
+    if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");
+    if (blocks != 0 && (blocks < 64 || blocks > (1 << 22))) return set_err(h, LPC_E_ARG, "walk grid out of range");
+    RETIF(settle(h));                   // a trace still running (lpc_trace_iterate / _run_async)
+    h->walk_grid = blocks ? blocks : kWalkWaves;
+    return 0;
+}
+
 int lpc_set_chunk(lpc_handle *h, int64_t rays_per_chunk)
 {
     if (!h) return set_err(nullptr, LPC_E_ARG, "null handle");

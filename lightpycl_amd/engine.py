@@ -231,6 +231,11 @@ class Engine:
     def set_chunk(self, rays):
         self._c(self.L.lpc_set_chunk(self.h, int(rays)))
 
+    def set_walk_grid(self, blocks):
+        """Hierarchy-walk grid in single-wave blocks (0: the library default);
+        a launch policy, results unchanged (lpc_set_walk_grid)."""
+        self._c(self.L.lpc_set_walk_grid(self.h, int(blocks)))
+
     def set_rays(self, origin4, dir4, pow_, max_ray_len=1e3, ior_env=1.0):
         o, d = f32(origin4, (-1, 4)), f32(dir4, (-1, 4))
         pw = f32(pow_).reshape(-1)

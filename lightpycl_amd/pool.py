@@ -23,6 +23,11 @@ import numpy as np
 
 from .engine import Engine
 
+# Walk grid of engines that trace side by side: 16 384 single-wave blocks ran the
+# headline 2.4 % faster than the default 65 536 with three in flight, and one
+# trace alone 7-15 % slower on the larger configs.
+INFLIGHT_WALK_GRID = 16384
+
 
 class TracePool:
     """``submit`` batches; each future gives the batch's per-iteration counts,
@@ -34,6 +39,8 @@ class TracePool:
         self.engines = [Engine(device) for _ in range(max(1, int(engines)))]
         for e in self.engines:
             e.upload_meshes(meshes)
+            if len(self.engines) > 1:
+                e.set_walk_grid(INFLIGHT_WALK_GRID)
         self._q = [queue.Queue() for _ in self.engines]
         self._next = 0
         self._lock = threading.Lock()

@@ -47,3 +47,34 @@ def test_pool_batches_equal_one_engine(name, n, k, engines):
         assert g["measured_count"] == r[1], b
         assert g["mesh_power"].tolist() == r[2], b
         np.testing.assert_array_equal(measured_rows(*g["measured"]), r[3], err_msg=f"batch {b}")
+
+
+def test_walk_grid_results_unchanged():
+    """lpc_set_walk_grid is a launch policy: a trace under walk grids of 64,
+    16 384 (TracePool's) and the default gives the same per-iteration counts,
+    per-mesh power bits and measured rays; out-of-range grids are refused."""
+    from lightpycl_amd._lib import LpcError
+    from lightpycl_amd.engine import Engine
+    from parity_util import measured_rows
+    sc = scenes.BUILDERS["synthetic"](n=50000, seed=3)
+    ls = sc.sources[0]
+    o, d = np.asarray(ls.rays_origin, np.float32), np.asarray(ls.rays_dir, np.float32)
+    p = np.asarray(ls.rays_power, np.float32).reshape(-1)
+    thr = (1.0 - sc.tau) * float(np.sum(p, dtype=np.float64))
+    e = Engine(0)
+    try:
+        e.upload_meshes(sc.meshes)
+        for bad in (-1, 63, (1 << 22) + 1):
+            with pytest.raises(LpcError):
+                e.set_walk_grid(bad)
+        got = []
+        for g in (0, 64, 16384, 0):
+            e.set_walk_grid(g)
+            e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+            st, (c, mp) = e.run_local(sc.iterations, thr)
+            got.append(([int(x.n_in) for x in st], int(c), mp.tolist(), measured_rows(*e.fetch_measured())))
+    finally:
+        e.close()
+    for g in got[1:]:
+        assert g[0] == got[0][0] and g[1] == got[0][1] and g[2] == got[0][2]
+        np.testing.assert_array_equal(g[3], got[0][3])
