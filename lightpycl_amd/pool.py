@@ -10,7 +10,7 @@ thread per handle (ctypes releases the GIL inside the library calls), so up to
 ``engines`` traces run at once.  Each batch is traced exactly as by one engine
 alone (the same kernels on the same rays: counts, per-mesh power and measured
 rays identical; tests/test_gpu_pool.py); with three in flight the headline
-workload runs 1.54x the ray-bounces/s of back-to-back traces (bench.py
+workload runs 1.52x the ray-bounces/s of back-to-back traces (bench.py
 ``inflight``).
 """
 from __future__ import annotations
