@@ -81,7 +81,10 @@ const int kAccRing = 8;   // mapped counter slots (iterations in flight: at most
 const int64_t kSortMin = 4096;          // populations below this are traced unsorted
 const int64_t kOnesweepMin = 500000;    // rocPRIM onesweep radix sort from this many rays (merge sort below)
 const int kRootsPerBlock = 16;          // k_roots_s packets per block (one task per packet)
-const int64_t kQTarget = 65536;         // (packet, piece) root tests to aim for: the piece level
+#ifndef LPC_Q_TARGET
+#define LPC_Q_TARGET 65536               // compile-time A/B builds (tools/build_variant.py)
+#endif
+const int64_t kQTarget = LPC_Q_TARGET;  // (packet, piece) root tests to aim for: the piece level
 #ifndef LPC_CHAIN_PIECES
 #define LPC_CHAIN_PIECES 4              // compile-time A/B builds (tools/build_variant.py)
 #endif
@@ -103,7 +106,10 @@ const int kSpillLevels = 3;             // k_spill levels (hand-over depth) for 
 const int kSpillLevelsSmall = 1;        // ... below (round 5 A/B: 4 levels, level budgets 10 or 14 / 8, two
                                         //   levels below: neutral or slower)
 const int64_t kSpillSmallN = 262144;
-const int64_t kSpillBlocks = 4096;      // k_spill level l grid: max(kSpillMinBlocks, kSpillBlocks >> l) x 4 waves
+#ifndef LPC_SPILL_BLOCKS
+#define LPC_SPILL_BLOCKS 4096            // compile-time A/B builds (tools/build_variant.py)
+#endif
+const int64_t kSpillBlocks = LPC_SPILL_BLOCKS;  // k_spill level l grid: max(kSpillMinBlocks, kSpillBlocks >> l) x 4 waves
 const int64_t kSpillMinBlocks = 256;
 const int kSpillPairShift = 5;          // exact pairs per node visit in the hand-over budget (log2; round 5
                                         //   A/B with the pair list: 4 and 6 equal)
