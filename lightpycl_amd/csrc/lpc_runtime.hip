@@ -102,7 +102,10 @@ const int64_t kChainPiecesRuns = 8;
 const int64_t kWalkWaves = LPC_WALK_GRID;   // k_rootwalk grid (single-wave blocks, grid-stride)
 const int64_t kSliverMergePpw = 4;      // packets per merged sliver unit (k_rootwalk's tail)
 const int64_t kSliverWaves = 16384;     // k_slivers: (packet, piece) waves to aim for
-const int kSpillLevels = 3;             // k_spill levels (hand-over depth) for populations >= kSpillSmallN
+#ifndef LPC_SPILL_LEVELS
+#define LPC_SPILL_LEVELS 3               // compile-time A/B builds (tools/build_variant.py)
+#endif
+const int kSpillLevels = LPC_SPILL_LEVELS;  // k_spill levels (hand-over depth) for populations >= kSpillSmallN
 const int kSpillLevelsSmall = 1;        // ... below (round 5 A/B: 4 levels, level budgets 10 or 14 / 8, two
                                         //   levels below: neutral or slower)
 const int64_t kSpillSmallN = 262144;
