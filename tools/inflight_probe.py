@@ -1,6 +1,6 @@
 """Traces in flight: E engines (handles, each its own stream and copy of the
-scene) on one GPU, each re-tracing the headline's 1 M rays from its own host
-thread, against one engine alone.  Prints one JSON line per E: total
+scene; with E > 1 TracePool's walk grid) on one GPU, each re-tracing the
+headline's 1 M rays from its own host thread, against one engine alone.  Prints one JSON line per E: total
 ray-bounces/s and the per-trace time seen by each thread.
 
     python tools/inflight_probe.py [traces per engine] [E ...]
@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     from lightpycl_amd import scenes
     from lightpycl_amd.engine import Engine
+    from lightpycl_amd.pool import INFLIGHT_WALK_GRID
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     Es = [int(a) for a in sys.argv[2:]] or [1, 2, 3]
     sc = scenes.synthetic(n=1_000_000, seed=7)
@@ -33,6 +34,8 @@ def main():
             e = Engine(0)
             e.upload_meshes(sc.meshes)
             e.set_rays(o, d, p, sc.max_ray_len, sc.ior_env)
+            if E > 1:
+                e.set_walk_grid(INFLIGHT_WALK_GRID)     # as TracePool does
             engines.append(e)
         bounces = []
         for e in engines:                       # warm-up, and the bounces of one trace
