@@ -16,6 +16,7 @@ workload runs 1.52x the ray-bounces/s of back-to-back traces (bench.py
 from __future__ import annotations
 
 import concurrent.futures as cf
+import os
 import queue
 import threading
 
@@ -26,7 +27,8 @@ from .engine import Engine
 # Walk grid of engines that trace side by side: 16 384 single-wave blocks ran the
 # headline 2.4 % faster than the default 65 536 with three in flight, and one
 # trace alone 7-15 % slower on the larger configs.
-INFLIGHT_WALK_GRID = 16384
+# LPC_INFLIGHT_WALK_GRID overrides it (A/B runs).
+INFLIGHT_WALK_GRID = int(os.environ.get("LPC_INFLIGHT_WALK_GRID", "16384"))
 
 
 class TracePool:
